@@ -1,0 +1,983 @@
+// render.hip -- the MI355X wavefront integrator and the C-ABI (include/kirk_hip.h).
+//
+// One khp_render call replaces KIRK's PathTracer::render/processSegment/
+// traceRays (CPU_PathTracer.cpp:17-209).  Instead of KIRK's per-pixel AoS
+// loop with a fork-join per bounce, the paths of a whole batch (owned pixels x
+// samples) live in SoA buffers in HBM and each bounce runs three kernels:
+//   extend  : persistent, wave-fetched closest-hit BVH2 traversal
+//   shade   : light hit test, environment/light/material shaders, BSDF sample,
+//             NEE shadow-ray setup; wave ballot compaction of the next ray
+//             queue and of the shadow queue
+//   shadow  : persistent any-hit traversal, then the deferred colour add
+// followed by one accumulate kernel per batch (KIRK's running mean).  All
+// counts stay on the device, so a frame is enqueued without host syncs.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "device.h"
+
+using namespace khp;
+
+// ============================================================================
+//  wavefront state
+// ============================================================================
+struct Counters {
+    uint32_t nq[2];        // ray queue sizes
+    uint32_t nsh;          // shadow queue size
+    uint32_t fetch_ext, fetch_sh;
+    uint32_t pad[3];
+    unsigned long long ext_rays, sh_rays;
+    unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests;
+};
+
+struct Wave {
+    float* qo[2][3];
+    float* qd[2][3];
+    uint32_t* qpid[2];
+    float* ht;
+    int32_t* hslot;
+    float* hu;
+    float* hv;
+    float* T[3];
+    float* C[3];
+    int32_t* flags;
+    uint32_t* key;
+    float4* sh;          // 6 float4 per shadow record
+    Counters* cnt;
+    const uint32_t* pix;  // owned pixel ids (y*W+x)
+    uint32_t P;           // pixels in this chunk
+    uint32_t p_off;       // chunk offset into pix
+    uint32_t W, H;
+    uint32_t seed;
+    uint32_t sample0;     // global sample index of chunk sample 0
+    uint32_t n_samples;   // samples in this chunk
+    uint32_t depth;
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// wave-level stream compaction: one atomic per wave, order-preserving in the wave.
+__device__ __forceinline__ uint32_t wave_alloc(bool pred, uint32_t* counter) {
+    unsigned long long mask = __ballot(pred);
+    uint32_t lane = lane_id();
+    uint32_t prefix = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    uint32_t base = 0;
+    if (lane == 0 && mask) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+    base = __shfl(base, 0);
+    return base + prefix;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// ---- generate: camera rays (PathTracer::generatePrimaryRays, CPU_PathTracer.cpp:118-127;
+//      Camera::getRayFromPixel, Camera.cpp:59-66) -------------------------------------------
+__global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
+    uint32_t n = Wv.P * Wv.n_samples;
+    uint32_t pid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pid == 0) Wv.cnt->nq[0] = n;
+    if (pid >= n) return;
+    uint32_t s_local = pid / Wv.P, p_local = pid - s_local * Wv.P;
+    uint32_t pixel = Wv.pix[Wv.p_off + p_local];
+    uint32_t x = pixel % Wv.W, y = pixel / Wv.W;
+    uint32_t key = path_key(Wv.seed, pixel, Wv.sample0 + s_local);
+    float u1 = draw_u01(key, dim_of(0, P_CAM_X)), u2 = draw_u01(key, dim_of(0, P_CAM_Y));
+    const khp_camera& cam = S.cam;
+    float s1 = ((float)x + u1) * cam.pixel_size, s2 = ((float)y + u2) * cam.pixel_size;
+    v3 dir = ((ld3(cam.bottom_left) + ld3(cam.axis_x) * s1) + ld3(cam.axis_y) * s2) - ld3(cam.position);
+    Ray r = make_ray(ld3(cam.position), dir);
+    Wv.qo[0][0][pid] = r.o.x; Wv.qo[0][1][pid] = r.o.y; Wv.qo[0][2][pid] = r.o.z;
+    Wv.qd[0][0][pid] = r.d.x; Wv.qd[0][1][pid] = r.d.y; Wv.qd[0][2][pid] = r.d.z;
+    Wv.qpid[0][pid] = pid;
+    Wv.T[0][pid] = 1.0f; Wv.T[1][pid] = 1.0f; Wv.T[2][pid] = 1.0f;
+    Wv.C[0][pid] = 0.0f; Wv.C[1][pid] = 0.0f; Wv.C[2][pid] = 0.0f;
+    Wv.flags[pid] = 0;
+    Wv.key[pid] = key;
+}
+
+__global__ void k_prep(Counters* c, int cur) {
+    int nxt = cur ^ 1;
+    c->sh_rays += c->nsh;   // shadow rays of the previous bounce
+    c->nq[nxt] = 0;
+    c->nsh = 0;
+    c->fetch_ext = 0;
+    c->fetch_sh = 0;
+    c->ext_rays += c->nq[cur];
+}
+
+// ---- extend: closest hit for every queued ray ------------------------------------------
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_extend(DevScene S, Wave Wv, int cur) {
+    const uint32_t n = Wv.cnt->nq[cur];
+    TravStats st{0, 0};
+    for (;;) {
+        uint32_t base = 0;
+        if (lane_id() == 0) base = atomicAdd(&Wv.cnt->fetch_ext, 64u);
+        base = __shfl(base, 0);
+        if (base >= n) break;
+        uint32_t i = base + lane_id();
+        if (i < n) {
+            Ray r;
+            r.o = mk(Wv.qo[cur][0][i], Wv.qo[cur][1][i], Wv.qo[cur][2][i]);
+            r.d = mk(Wv.qd[cur][0][i], Wv.qd[cur][1][i], Wv.qd[cur][2][i]);
+            Hit h;
+            trace_closest<STATS>(S, r, h, st);
+            Wv.ht[i] = h.t;
+            Wv.hslot[i] = h.slot;
+            Wv.hu[i] = h.u;
+            Wv.hv[i] = h.v;
+        }
+    }
+    if (STATS) {
+        unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
+        if (lane_id() == 0) {
+            atomicAdd(&Wv.cnt->node_visits, a);
+            atomicAdd(&Wv.cnt->prim_tests, b);
+        }
+    }
+}
+
+// ---- shade: traceRay light test + shaders (CPU_PathTracer.cpp:141-208; SimpleShader.h;
+//      MarschnerHairShader.h; LightShader.h; EnvironmentShader.h) ------------------------
+__global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
+    const uint32_t n = Wv.cnt->nq[cur];
+    const int nxt = cur ^ 1;
+    const bool last = bounce + 1 >= Wv.depth;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {
+        uint32_t i = base + threadIdx.x;
+        bool active = i < n;
+        bool emit_ray = false, emit_sh = false;
+        Ray nr;
+        nr.o = nr.d = mk(0, 0, 0);
+        uint32_t pid = 0;
+        // shadow record payload
+        Ray shr;
+        shr.o = shr.d = mk(0, 0, 0);
+        float sh_tmax = 0.0f;
+        v3 lc = mk(0, 0, 0), Told = mk(0, 0, 0), AT = mk(0, 0, 0), ET = mk(0, 0, 0);
+        bool has_emit = false;
+        if (active) {
+            pid = Wv.qpid[cur][i];
+            Ray r;
+            r.o = mk(Wv.qo[cur][0][i], Wv.qo[cur][1][i], Wv.qo[cur][2][i]);
+            r.d = mk(Wv.qd[cur][0][i], Wv.qd[cur][1][i], Wv.qd[cur][2][i]);
+            float lambda = Wv.ht[i];
+            int32_t slot = Wv.hslot[i];
+            v3 T = mk(Wv.T[0][pid], Wv.T[1][pid], Wv.T[2][pid]);
+            v3 C = mk(Wv.C[0][pid], Wv.C[1][pid], Wv.C[2][pid]);
+            int flags = Wv.flags[pid];
+            uint32_t key = Wv.key[pid];
+            // KIRK's linear ray-light test (CPU_PathTracer.cpp:185-208)
+            float t_lights = FLT_MAX_;
+            int t_index = -1;
+            for (int li = 0; li < S.n_lights; ++li) {
+                float t = FLT_MAX_;
+                if (light_isect(S.lights[li], r, t)) {
+                    t_lights = gmin(t_lights, t);
+                    t_index = (t == t_lights) ? li : t_index;
+                }
+            }
+            bool light_hit = false;
+            if (t_lights < lambda) {
+                lambda = t_lights;
+                light_hit = true;
+            }
+            if (lambda == FLT_MAX_) {  // EnvironmentShader::shade
+                C = C + mk(S.env.color[0], S.env.color[1], S.env.color[2]) * T;
+                T = mk(0, 0, 0);
+            } else if (light_hit) {    // LightShader::shade
+                C = C + light_emit(S.lights[t_index], r.d) * T;
+                T = mk(0, 0, 0);
+            } else {
+                Aux ax = S.aux[slot];
+                const float4* pr = S.prims + 4 * (size_t)slot;
+                ShadeCtx s;
+                s.m = &S.mats[ax.mat];
+                v3 nrm;
+                if (ax.is_cone) {  // Cylinder::calcNormal (Cylinder.cpp:230-237)
+                    float4 c0 = pr[0], c1 = pr[1], c2 = pr[2], c3 = pr[3];
+                    v3 base3 = mk(c0.x, c0.y, c0.z);
+                    s.U = mk(c1.x, c1.y, c1.z);
+                    s.V = mk(c2.x, c2.y, c2.z);
+                    s.W = mk(c3.x, c3.y, c3.z);
+                    v3 Q = follow(r, lambda);
+                    float tt = dot(Q, s.V) - ax.base_d;
+                    v3 q1 = Q - s.V * tt;
+                    v3 nn = normalize(q1 - base3);
+                    nrm = normalize(nn + s.V * c1.w);
+                } else {           // Triangle::calcNormal (Triangle.cpp:244-248)
+                    const float* tn = S.tri_nrm + 9 * (size_t)ax.obj;
+                    float bu = Wv.hu[i], bv = Wv.hv[i];
+                    float bx = (1.0f - bu) - bv;
+                    nrm = normalize((ld3(tn) * bx + ld3(tn + 3) * bu) + ld3(tn + 6) * bv);
+                    s.U = s.V = s.W = mk(0, 0, 0);
+                }
+                s.n = nrm;
+                const khp_material* m = s.m;
+                v3 loc = follow(r, lambda);
+                float h0 = draw_u01(key, dim_of(bounce, P_HAIR_ALPHA)), h1 = draw_u01(key, dim_of(bounce, P_HAIR_BETA));
+                v3 counter = -normalize(r.d);
+                // NEE setup: SimpleShader::calcDirectLight (SimpleShader.h:101-152) and
+                // MarschnerHairShader::calcDirectLight (MarschnerHairShader.h:87-138)
+                bool need_shadow = false;
+                if (S.n_lights > 0) {
+                    int li = (int)((double)draw_u01(key, dim_of(bounce, P_LIGHT_SEL)) * (double)S.n_lights);
+                    const DevLight& L = S.lights[li];
+                    float att;
+                    Ray h2l = light_dir(L, loc, draw_u01(key, dim_of(bounce, P_LIGHT_0)),
+                                        draw_u01(key, dim_of(bounce, P_LIGHT_1)), att);
+                    v3 lightpos = h2l.o + h2l.d;
+                    h2l.o = h2l.o + faceforward(nrm, h2l.o - lightpos, nrm) * 1e-4f;
+                    h2l.d = normalize(h2l.d);
+                    if (L.color[0] > 0.0f || L.color[1] > 0.0f || L.color[2] > 0.0f) {
+                        v3 f = bsdf_eval(s, h2l.d, -r.d);
+                        float ad = fabsf(dot(h2l.d, nrm));
+                        lc = mk(L.color[0] * ((att * f.x) * ad), L.color[1] * ((att * f.y) * ad),
+                                L.color[2] * ((att * f.z) * ad));
+                        sh_tmax = length(lightpos - h2l.o);
+                        shr = h2l;
+                        need_shadow = true;
+                    }
+                }
+                v3 ev = bsdf_eval(s, nrm, nrm);
+                v3 amb = mk(S.env.ambient[0], S.env.ambient[1], S.env.ambient[2]) * (ev * ONE_OVER_PI);
+                Told = T;
+                AT = amb * T;
+                bool add_now = true;  // colour add not deferred to the shadow kernel
+                if (m->shader == KHP_SHADER_MARSCHNER_HAIR) {  // MarschnerHairShader::shade
+                    float smp[2] = {0.0f, 0.0f};
+                    v3 out;
+                    float pdf = 0.0f;
+                    bool valid;
+                    v3 refl = bsdf_sample(s, counter, nrm, smp, h0, h1, out, pdf, flags, valid);
+                    v3 off = out * 1e-4f;
+                    if (!(flags & F_SPECULAR)) off = faceforward(-(nrm * 1e-4f), nrm, out);
+                    nr = make_ray(loc + off, out);
+                    if ((flags & F_CYL_T) || (flags & F_CYL_TR)) {
+                        need_shadow = false;
+                        add_now = false;
+                    } else {
+                        if (is_zero(refl) || pdf <= 1E-4f || gmax(T.x, gmax(T.y, T.z)) < 0.01f) T = mk(0, 0, 0);
+                        else T = T * ((refl * 3.0f) * fabsf(k_cosf(smp[0])));
+                    }
+                } else {  // SimpleShader::shade
+                    float smp[2] = {draw_u01(key, dim_of(bounce, P_BSDF_0)), draw_u01(key, dim_of(bounce, P_BSDF_1))};
+                    v3 out;
+                    float pdf = 0.0f;
+                    int fl = 0;
+                    bool valid;
+                    v3 refl = bsdf_sample(s, counter, nrm, smp, h0, h1, out, pdf, fl, valid);
+                    if (is_zero(refl) || pdf <= 1E-4f || gmax(T.x, gmax(T.y, T.z)) < 0.01f) {
+                        T = mk(0, 0, 0);
+                    } else if ((fl & F_EMISSIVE) == F_EMISSIVE) {
+                        has_emit = true;
+                        ET = mk(m->emission[0], m->emission[1], m->emission[2]) * T;
+                        T = mk(0, 0, 0);
+                    } else {
+                        float ad = fabsf(dot(out, nrm));
+                        T = T * ((refl * ad) / pdf);
+                        flags = fl;
+                        v3 off = out * 1e-4f;
+                        if ((fl & F_SPECULAR) != F_SPECULAR) off = faceforward(-(nrm * 1e-4f), nrm, out);
+                        nr = make_ray(loc + off, out);
+                    }
+                }
+                if (add_now) {
+                    if (need_shadow) {
+                        emit_sh = true;  // colour is added by k_shadow
+                    } else {
+                        v3 acc = (mk(0, 0, 0) + mk(0, 0, 0) * Told) + AT;
+                        if (has_emit) acc = acc + ET;
+                        C = C + acc;
+                    }
+                }
+            }
+            Wv.T[0][pid] = T.x; Wv.T[1][pid] = T.y; Wv.T[2][pid] = T.z;
+            if (!emit_sh) { Wv.C[0][pid] = C.x; Wv.C[1][pid] = C.y; Wv.C[2][pid] = C.z; }
+            Wv.flags[pid] = flags;
+            emit_ray = !last && !is_zero(T) && !is_zero(nr.d);
+        }
+        uint32_t qi = wave_alloc(emit_ray, &Wv.cnt->nq[nxt]);
+        if (emit_ray) {
+            Wv.qo[nxt][0][qi] = nr.o.x; Wv.qo[nxt][1][qi] = nr.o.y; Wv.qo[nxt][2][qi] = nr.o.z;
+            Wv.qd[nxt][0][qi] = nr.d.x; Wv.qd[nxt][1][qi] = nr.d.y; Wv.qd[nxt][2][qi] = nr.d.z;
+            Wv.qpid[nxt][qi] = pid;
+        }
+        uint32_t si = wave_alloc(emit_sh, &Wv.cnt->nsh);
+        if (emit_sh) {
+            float4* rec = Wv.sh + 6 * (size_t)si;
+            rec[0] = make_float4(shr.o.x, shr.o.y, shr.o.z, sh_tmax);
+            rec[1] = make_float4(shr.d.x, shr.d.y, shr.d.z, f_from_bits(pid));
+            rec[2] = make_float4(lc.x, lc.y, lc.z, has_emit ? 1.0f : 0.0f);
+            rec[3] = make_float4(Told.x, Told.y, Told.z, 0.0f);
+            rec[4] = make_float4(AT.x, AT.y, AT.z, 0.0f);
+            if (has_emit) rec[5] = make_float4(ET.x, ET.y, ET.z, 0.0f);
+        }
+    }
+}
+
+// ---- shadow: BVH::isIntersection + light occlusion loop, then colour += acc ------------
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_shadow(DevScene S, Wave Wv) {
+    const uint32_t n = Wv.cnt->nsh;
+    TravStats st{0, 0};
+    for (;;) {
+        uint32_t base = 0;
+        if (lane_id() == 0) base = atomicAdd(&Wv.cnt->fetch_sh, 64u);
+        base = __shfl(base, 0);
+        if (base >= n) break;
+        uint32_t i = base + lane_id();
+        if (i < n) {
+            const float4* rec = Wv.sh + 6 * (size_t)i;
+            float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3], e = rec[4];
+            Ray r;
+            r.o = mk(a.x, a.y, a.z);
+            r.d = mk(b.x, b.y, b.z);
+            float tmax = a.w;
+            uint32_t pid = bits_from_f(b.w);
+            bool occ = trace_any<STATS>(S, r, tmax, st);
+            if (!occ) {
+                for (int li = 0; li < S.n_lights; ++li) {
+                    float t;
+                    if (light_isect(S.lights[li], r, t) && (t < tmax)) {
+                        occ = true;
+                        break;
+                    }
+                }
+            }
+            v3 lc = mk(c.x, c.y, c.z) * (occ ? 0.0f : 1.0f);
+            v3 dl = mk(0, 0, 0) + lc;
+            v3 acc = (mk(0, 0, 0) + dl * mk(d.x, d.y, d.z)) + mk(e.x, e.y, e.z);
+            if (c.w != 0.0f) {
+                float4 f = rec[5];
+                acc = acc + mk(f.x, f.y, f.z);
+            }
+            Wv.C[0][pid] = Wv.C[0][pid] + acc.x;
+            Wv.C[1][pid] = Wv.C[1][pid] + acc.y;
+            Wv.C[2][pid] = Wv.C[2][pid] + acc.z;
+        }
+    }
+    if (STATS) {
+        unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
+        if (lane_id() == 0) {
+            atomicAdd(&Wv.cnt->sh_node_visits, a);
+            atomicAdd(&Wv.cnt->sh_prim_tests, b);
+        }
+    }
+}
+
+// ---- accumulate: PathTracer::drawTexture running mean (CPU_PathTracer.cpp:61-90) -------
+__global__ void k_tail(Counters* c) {
+    c->sh_rays += c->nsh;
+    c->nsh = 0;
+}
+
+__global__ __launch_bounds__(256) void k_accumulate(Wave Wv, float* fb) {
+    uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= Wv.P) return;
+    uint32_t pixel = Wv.pix[Wv.p_off + p];
+    float* o = fb + 3 * (size_t)pixel;
+    float r = o[0], g = o[1], b = o[2];
+    for (uint32_t s = 0; s < Wv.n_samples; ++s) {
+        uint32_t pid = s * Wv.P + p;
+        float cr = Wv.C[0][pid], cg = Wv.C[1][pid], cb = Wv.C[2][pid];
+        uint32_t k = Wv.sample0 + s;
+        if (k == 0) {
+            r = cr; g = cg; b = cb;
+        } else {
+            float kk = (float)(k + 1);
+            r = r + (cr - r) / kk;
+            g = g + (cg - g) / kk;
+            b = b + (cb - b) / kk;
+        }
+    }
+    o[0] = r; o[1] = g; o[2] = b;
+}
+
+// ---- batch ray queries for khp_trace_* ---------------------------------------------------
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_trace_closest(DevScene S, uint32_t n, const float* orig, const float* dir,
+                                                       float* t_out, int32_t* obj_out, float* uv_out,
+                                                       unsigned long long* stats) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    TravStats st{0, 0};
+    if (i < n) {
+        Ray r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
+        Hit h;
+        trace_closest<STATS>(S, r, h, st);
+        t_out[i] = h.t;
+        obj_out[i] = h.slot >= 0 ? (int32_t)S.aux[h.slot].obj : -1;
+        if (uv_out) {
+            uv_out[2 * (size_t)i] = h.u;
+            uv_out[2 * (size_t)i + 1] = h.v;
+        }
+    }
+    if (STATS) {
+        unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
+        if (lane_id() == 0) {
+            atomicAdd(&stats[0], a);
+            atomicAdd(&stats[1], b);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_trace_any(DevScene S, uint32_t n, const float* orig, const float* dir,
+                                                   const float* tmax, uint8_t* hit_out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ray r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
+    TravStats st{0, 0};
+    hit_out[i] = trace_any<false>(S, r, tmax[i], st) ? 1 : 0;
+}
+
+// ---- multi-GPU: pack owned pixels / scatter a rank's pixels ------------------------------
+__global__ void k_pack(const float* fb, const uint32_t* pix, uint32_t P, float* out) {
+    uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const float* s = fb + 3 * (size_t)pix[p];
+    out[3 * (size_t)p] = s[0];
+    out[3 * (size_t)p + 1] = s[1];
+    out[3 * (size_t)p + 2] = s[2];
+}
+__global__ void k_unpack(float* fb, const uint32_t* pix, uint32_t P, const float* in) {
+    uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    float* d = fb + 3 * (size_t)pix[p];
+    d[0] = in[3 * (size_t)p];
+    d[1] = in[3 * (size_t)p + 1];
+    d[2] = in[3 * (size_t)p + 2];
+}
+
+// ============================================================================
+//  host side
+// ============================================================================
+static thread_local std::string g_err;
+
+static khp_status fail(khp_status s, const std::string& msg) {
+    g_err = msg;
+    return s;
+}
+
+#define HIPCHK(expr)                                                                                     \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess) return fail(KHP_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct DevMem {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevMem() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t ensure(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n ? n : 16);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    template <typename T>
+    T* as() const { return (T*)p; }
+};
+
+struct TimedLaunch {
+    int kind;  // 0 extend, 1 shade, 2 shadow, 3 other
+    hipEvent_t a, b;
+};
+
+struct khp_ctx {
+    int device = 0;
+    uint32_t flags = 0;
+    hipStream_t stream = nullptr;
+    int n_cu = 256;
+    HostScene hs;
+    bool scene_set = false, built = false;
+    DevMem prims, aux, trinrm, nodes, mats, lights;
+    DevScene S{};
+    // wavefront
+    size_t cap = 0;
+    DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb, cnt;
+    // framebuffer + pixel list
+    DevMem fb, pix, stage, stage2, stage_pix;
+    uint32_t fbW = 0, fbH = 0;
+    std::vector<uint32_t> pix_host;
+    uint32_t pix_key[5] = {0, 0, 0, 0, 0};
+    // timing
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_next = 0;
+    std::vector<TimedLaunch> launches;
+    int grid_ext = 0, grid_sh = 0, grid_shade = 0;
+    khp_stats st{};
+    // rccl
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+static hipEvent_t next_event(khp_ctx* c) {
+    if (c->ev_next == c->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->ev_pool.push_back(e);
+    }
+    return c->ev_pool[c->ev_next++];
+}
+
+extern "C" int khp_abi_version(void) { return KHP_ABI_VERSION; }
+extern "C" const char* khp_last_error(void) { return g_err.c_str(); }
+
+extern "C" khp_status khp_create(khp_ctx** out, int device, uint32_t flags) {
+    if (!out) return fail(KHP_EINVAL, "out is null");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(KHP_EDEVICE, "no HIP device available");
+    if (device < 0 || device >= n) return fail(KHP_EINVAL, "device ordinal out of range");
+    HIPCHK(hipSetDevice(device));
+    khp_ctx* c = new khp_ctx();
+    c->device = device;
+    c->flags = flags;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(KHP_EDEVICE, "hipStreamCreate failed");
+    }
+    *out = c;
+    return KHP_OK;
+}
+
+extern "C" void khp_destroy(khp_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" khp_status khp_set_scene(khp_ctx* c, const khp_scene* s) {
+    if (!c) return fail(KHP_EINVAL, "ctx is null");
+    auto t0 = std::chrono::steady_clock::now();
+    std::string err = flatten_scene(s, c->hs);
+    if (!err.empty()) return fail(KHP_EINVAL, err);
+    c->scene_set = true;
+    c->built = false;
+    c->st.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return KHP_OK;
+}
+
+template <typename T>
+static hipError_t upload(DevMem& m, const T* data, size_t count, hipStream_t s) {
+    hipError_t e = m.ensure(count * sizeof(T));
+    if (e != hipSuccess) return e;
+    if (count) return hipMemcpyAsync(m.p, data, count * sizeof(T), hipMemcpyHostToDevice, s);
+    return hipSuccess;
+}
+
+extern "C" khp_status khp_build_accel(khp_ctx* c) {
+    if (!c) return fail(KHP_EINVAL, "ctx is null");
+    if (!c->scene_set) return fail(KHP_ENOTREADY, "khp_set_scene first");
+    HIPCHK(hipSetDevice(c->device));
+    auto t0 = std::chrono::steady_clock::now();
+    unsigned nt = std::thread::hardware_concurrency();
+    build_bvh(c->hs, (int)std::max(1u, std::min(nt, 32u)));
+    make_device_layout(c->hs);
+    auto t1 = std::chrono::steady_clock::now();
+    c->st.build_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    if (c->hs.depth + 1 > (uint32_t)STACK_MAX)
+        return fail(KHP_EUNSUPPORTED, "BVH deeper than the traversal stack (" + std::to_string(c->hs.depth) + ")");
+    HostScene& hs = c->hs;
+    HIPCHK(upload(c->prims, hs.slot_rec.data(), hs.slot_rec.size(), c->stream));
+    HIPCHK(upload(c->aux, hs.slot_aux.data(), hs.slot_aux.size(), c->stream));
+    HIPCHK(upload(c->trinrm, hs.tri_nrm.data(), hs.tri_nrm.size(), c->stream));
+    HIPCHK(upload(c->nodes, hs.dnodes.data(), hs.dnodes.size(), c->stream));
+    HIPCHK(upload(c->mats, hs.mats.data(), hs.mats.size(), c->stream));
+    HIPCHK(upload(c->lights, hs.lights.data(), hs.lights.size(), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->st.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    DevScene& S = c->S;
+    S.prims = c->prims.as<float4>();
+    S.aux = c->aux.as<Aux>();
+    S.tri_nrm = c->trinrm.as<float>();
+    S.nodes = c->nodes.as<DevNode>();
+    S.mats = c->mats.as<khp_material>();
+    S.lights = c->lights.as<DevLight>();
+    S.n_lights = (int32_t)hs.lights.size();
+    S.root_ref = hs.root_ref;
+    S.root_cnt = hs.root_cnt;
+    memcpy(S.root_box, hs.root_box, sizeof(S.root_box));
+    S.env = hs.env;
+    S.cam = hs.cam;
+    c->st.n_objects = hs.n_obj;
+    c->st.n_nodes = hs.nodes.size();
+    c->st.n_leaves = hs.nodes.size() - hs.dnodes.size();
+    c->st.bvh_depth = hs.depth;
+    c->st.max_leaf_size = hs.max_leaf;
+    c->st.device_bytes = c->prims.bytes + c->aux.bytes + c->trinrm.bytes + c->nodes.bytes + c->mats.bytes +
+                         c->lights.bytes;
+    // persistent grid sizes
+    int nb = 0;
+    if (c->flags & KHP_CTX_STATS)
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<true>, 256, 0));
+    else
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, 256, 0));
+    c->grid_ext = std::max(1, nb) * c->n_cu;
+    nb = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, 256, 0));
+    c->grid_sh = std::max(1, nb) * c->n_cu;
+    nb = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade, 256, 0));
+    c->grid_shade = std::max(1, nb) * c->n_cu;
+    c->built = true;
+    return KHP_OK;
+}
+
+static khp_status ensure_wave(khp_ctx* c, size_t cap) {
+    if (cap <= c->cap) return KHP_OK;
+    for (int q = 0; q < 2; ++q)
+        for (int k = 0; k < 7; ++k) HIPCHK(c->qbuf[q][k].ensure(cap * 4));
+    HIPCHK(c->ht.ensure(cap * 4));
+    HIPCHK(c->hslot.ensure(cap * 4));
+    HIPCHK(c->hu.ensure(cap * 4));
+    HIPCHK(c->hv.ensure(cap * 4));
+    for (int k = 0; k < 3; ++k) {
+        HIPCHK(c->Tb[k].ensure(cap * 4));
+        HIPCHK(c->Cb[k].ensure(cap * 4));
+    }
+    HIPCHK(c->flagsb.ensure(cap * 4));
+    HIPCHK(c->keyb.ensure(cap * 4));
+    HIPCHK(c->shb.ensure(cap * 6 * sizeof(float4)));
+    HIPCHK(c->cnt.ensure(sizeof(Counters)));
+    c->cap = cap;
+    return KHP_OK;
+}
+
+static void owned_pixels(uint32_t W, uint32_t H, uint32_t T, uint32_t rank, uint32_t nranks,
+                         std::vector<uint32_t>& out) {
+    out.clear();
+    uint32_t tx_n = (W + T - 1) / T, ty_n = (H + T - 1) / T;
+    uint32_t bpr = T / 8;
+    for (uint32_t tid = 0; tid < tx_n * ty_n; ++tid) {
+        if (nranks > 1 && tid % nranks != rank) continue;
+        uint32_t tx = tid % tx_n, ty = tid / tx_n;
+        for (uint32_t blk = 0; blk < bpr * bpr; ++blk) {
+            uint32_t bx = blk % bpr, by = blk / bpr;
+            for (uint32_t j = 0; j < 64; ++j) {
+                uint32_t x = tx * T + bx * 8 + (j & 7), y = ty * T + by * 8 + (j >> 3);
+                if (x < W && y < H) out.push_back(y * W + x);
+            }
+        }
+    }
+}
+
+static khp_status prepare_pixels(khp_ctx* c, const khp_render_params* p) {
+    uint32_t T = p->tile_size ? p->tile_size : 64;
+    uint32_t nranks = p->tile_nranks > 1 ? p->tile_nranks : 1;
+    uint32_t rank = nranks > 1 ? p->tile_rank : 0;
+    uint32_t key[5] = {p->width, p->height, T, rank, nranks};
+    if (memcmp(key, c->pix_key, sizeof(key)) == 0 && c->pix.p) return KHP_OK;
+    owned_pixels(p->width, p->height, T, rank, nranks, c->pix_host);
+    HIPCHK(upload(c->pix, c->pix_host.data(), c->pix_host.size(), c->stream));
+    memcpy(c->pix_key, key, sizeof(key));
+    return KHP_OK;
+}
+
+static khp_status check_params(khp_ctx* c, const khp_render_params* p) {
+    if (!c || !p) return fail(KHP_EINVAL, "null argument");
+    if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
+    if (p->width == 0 || p->height == 0 || p->depth == 0) return fail(KHP_EINVAL, "width/height/depth must be > 0");
+    if ((uint64_t)p->width * p->height >= (1ull << 31)) return fail(KHP_EINVAL, "image too large");
+    uint32_t T = p->tile_size ? p->tile_size : 64;
+    if (T % 8 != 0) return fail(KHP_EINVAL, "tile_size must be a multiple of 8");
+    if (p->tile_nranks > 1 && p->tile_rank >= p->tile_nranks) return fail(KHP_EINVAL, "tile_rank >= tile_nranks");
+    return KHP_OK;
+}
+
+static void timed(khp_ctx* c, int kind, bool begin) {
+    hipEvent_t e = next_event(c);
+    if (!e) return;
+    (void)hipEventRecord(e, c->stream);
+    if (begin) c->launches.push_back(TimedLaunch{kind, e, nullptr});
+    else c->launches.back().b = e;
+}
+
+extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* out_rgb) {
+    khp_status s = check_params(c, p);
+    if (s != KHP_OK) return s;
+    HIPCHK(hipSetDevice(c->device));
+    const size_t npix = (size_t)p->width * p->height;
+    if (c->fbW != p->width || c->fbH != p->height || !c->fb.p) {
+        HIPCHK(c->fb.ensure(npix * 3 * sizeof(float)));
+        HIPCHK(hipMemsetAsync(c->fb.p, 0, npix * 3 * sizeof(float), c->stream));
+        c->fbW = p->width;
+        c->fbH = p->height;
+    }
+    s = prepare_pixels(c, p);
+    if (s != KHP_OK) return s;
+    const uint32_t P_all = (uint32_t)c->pix_host.size();
+    size_t cap_paths = (size_t)1 << 24;
+    if (const char* e = getenv("KHP_MAX_PATHS")) cap_paths = std::max<size_t>(4096, strtoull(e, nullptr, 10));
+    uint32_t P_chunk = (uint32_t)std::min<size_t>(P_all, cap_paths);
+    uint32_t S_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(p->spp, cap_paths / std::max<uint32_t>(P_chunk, 1)));
+    s = ensure_wave(c, (size_t)P_chunk * S_chunk);
+    if (s != KHP_OK) return s;
+    HIPCHK(hipMemsetAsync(c->cnt.p, 0, sizeof(Counters), c->stream));
+    const bool stats = (c->flags & KHP_CTX_STATS) != 0;
+    c->launches.clear();
+    c->ev_next = 0;
+    Wave Wv{};
+    for (int q = 0; q < 2; ++q) {
+        for (int k = 0; k < 3; ++k) {
+            Wv.qo[q][k] = c->qbuf[q][k].as<float>();
+            Wv.qd[q][k] = c->qbuf[q][3 + k].as<float>();
+        }
+        Wv.qpid[q] = c->qbuf[q][6].as<uint32_t>();
+    }
+    Wv.ht = c->ht.as<float>();
+    Wv.hslot = c->hslot.as<int32_t>();
+    Wv.hu = c->hu.as<float>();
+    Wv.hv = c->hv.as<float>();
+    for (int k = 0; k < 3; ++k) {
+        Wv.T[k] = c->Tb[k].as<float>();
+        Wv.C[k] = c->Cb[k].as<float>();
+    }
+    Wv.flags = c->flagsb.as<int32_t>();
+    Wv.key = c->keyb.as<uint32_t>();
+    Wv.sh = c->shb.as<float4>();
+    Wv.cnt = c->cnt.as<Counters>();
+    Wv.pix = c->pix.as<uint32_t>();
+    Wv.W = p->width;
+    Wv.H = p->height;
+    Wv.seed = p->seed;
+    Wv.depth = p->depth;
+    hipEvent_t ev_start = next_event(c);
+    (void)hipEventRecord(ev_start, c->stream);
+    for (uint32_t p0 = 0; p0 < P_all; p0 += P_chunk) {
+        uint32_t P = std::min(P_chunk, P_all - p0);
+        for (uint32_t s0 = 0; s0 < p->spp; s0 += S_chunk) {
+            uint32_t ns = std::min(S_chunk, p->spp - s0);
+            Wv.P = P;
+            Wv.p_off = p0;
+            Wv.sample0 = p->first_sample + s0;
+            Wv.n_samples = ns;
+            uint32_t npaths = P * ns;
+            timed(c, 3, true);
+            hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, c->stream, c->S, Wv);
+            timed(c, 3, false);
+            for (uint32_t b = 0; b < p->depth; ++b) {
+                int cur = b & 1;
+                hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, c->stream, Wv.cnt, cur);
+                timed(c, 0, true);
+                if (stats)
+                    hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(256), 0, c->stream, c->S, Wv, cur);
+                else
+                    hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(256), 0, c->stream, c->S, Wv, cur);
+                timed(c, 0, false);
+                timed(c, 1, true);
+                hipLaunchKernelGGL(k_shade, dim3(c->grid_shade), dim3(256), 0, c->stream, c->S, Wv, cur, b);
+                timed(c, 1, false);
+                timed(c, 2, true);
+                if (stats)
+                    hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), 0, c->stream, c->S, Wv);
+                else
+                    hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), 0, c->stream, c->S, Wv);
+                timed(c, 2, false);
+            }
+            hipLaunchKernelGGL(k_tail, dim3(1), dim3(1), 0, c->stream, Wv.cnt);
+            timed(c, 3, true);
+            hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, c->stream, Wv, c->fb.as<float>());
+            timed(c, 3, false);
+        }
+    }
+    hipEvent_t ev_end = next_event(c);
+    (void)hipEventRecord(ev_end, c->stream);
+    HIPCHK(hipGetLastError());
+    if (out_rgb && !(p->flags & KHP_RENDER_NO_READBACK)) {
+        hipMemcpyKind kind = (p->flags & KHP_RENDER_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        HIPCHK(hipMemcpyAsync(out_rgb, c->fb.p, npix * 3 * sizeof(float), kind, c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, ev_start, ev_end));
+    c->st.render_ms = ms;
+    c->st.extend_ms = c->st.shade_ms = c->st.shadow_ms = c->st.other_ms = 0.0;
+    c->st.extend_launches = 0;
+    for (auto& l : c->launches) {
+        float t = 0.0f;
+        if (l.b && hipEventElapsedTime(&t, l.a, l.b) == hipSuccess) {
+            if (l.kind == 0) { c->st.extend_ms += t; c->st.extend_launches++; }
+            else if (l.kind == 1) c->st.shade_ms += t;
+            else if (l.kind == 2) c->st.shadow_ms += t;
+            else c->st.other_ms += t;
+        }
+    }
+    Counters hc;
+    HIPCHK(hipMemcpy(&hc, c->cnt.p, sizeof(hc), hipMemcpyDeviceToHost));
+    c->st.extend_rays = hc.ext_rays;
+    c->st.shadow_rays = hc.sh_rays;
+    c->st.node_visits = hc.node_visits;
+    c->st.prim_tests = hc.prim_tests;
+    c->st.shadow_node_visits = hc.sh_node_visits;
+    c->st.shadow_prim_tests = hc.sh_prim_tests;
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_read_framebuffer(khp_ctx* c, float* out_rgb) {
+    if (!c || !out_rgb) return fail(KHP_EINVAL, "null argument");
+    if (!c->fb.p) return fail(KHP_ENOTREADY, "nothing rendered yet");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(out_rgb, c->fb.p, (size_t)c->fbW * c->fbH * 3 * sizeof(float), hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_trace_closest(khp_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out,
+                                        int32_t* obj_out, float* uv_out) {
+    if (!c || (n && (!orig || !dir || !t_out || !obj_out))) return fail(KHP_EINVAL, "null argument");
+    if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
+    if (n == 0) return KHP_OK;
+    HIPCHK(hipSetDevice(c->device));
+    DevMem o, d, t, ob, uv, stb;
+    HIPCHK(upload(o, orig, 3 * (size_t)n, c->stream));
+    HIPCHK(upload(d, dir, 3 * (size_t)n, c->stream));
+    HIPCHK(t.ensure(4 * (size_t)n));
+    HIPCHK(ob.ensure(4 * (size_t)n));
+    HIPCHK(uv.ensure(8 * (size_t)n));
+    HIPCHK(stb.ensure(16));
+    HIPCHK(hipMemsetAsync(stb.p, 0, 16, c->stream));
+    hipLaunchKernelGGL(k_trace_closest<true>, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->S, n,
+                       o.as<float>(), d.as<float>(), t.as<float>(), ob.as<int32_t>(), uv.as<float>(),
+                       stb.as<unsigned long long>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(t_out, t.p, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(obj_out, ob.p, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    if (uv_out) HIPCHK(hipMemcpyAsync(uv_out, uv.p, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long sv[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(sv, stb.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->st.node_visits = sv[0];
+    c->st.prim_tests = sv[1];
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_trace_any(khp_ctx* c, uint32_t n, const float* orig, const float* dir, const float* tmax,
+                                    uint8_t* hit_out) {
+    if (!c || (n && (!orig || !dir || !tmax || !hit_out))) return fail(KHP_EINVAL, "null argument");
+    if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
+    if (n == 0) return KHP_OK;
+    HIPCHK(hipSetDevice(c->device));
+    DevMem o, d, tm, h;
+    HIPCHK(upload(o, orig, 3 * (size_t)n, c->stream));
+    HIPCHK(upload(d, dir, 3 * (size_t)n, c->stream));
+    HIPCHK(upload(tm, tmax, (size_t)n, c->stream));
+    HIPCHK(h.ensure((size_t)n));
+    hipLaunchKernelGGL(k_trace_any, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->S, n, o.as<float>(),
+                       d.as<float>(), tm.as<float>(), h.as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(hit_out, h.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_get_stats(khp_ctx* c, khp_stats* out) {
+    if (!c || !out) return fail(KHP_EINVAL, "null argument");
+    *out = c->st;
+    return KHP_OK;
+}
+
+// ---- RCCL ---------------------------------------------------------------------------------
+#define NCCLCHK(expr)                                                                                       \
+    do {                                                                                                    \
+        ncclResult_t r_ = (expr);                                                                           \
+        if (r_ != ncclSuccess) return fail(KHP_EDEVICE, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+extern "C" khp_status khp_comm_unique_id(uint8_t out_id[128]) {
+    if (!out_id) return fail(KHP_EINVAL, "null argument");
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    memcpy(out_id, &id, 128);
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint8_t id[128]) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(KHP_EINVAL, "bad comm arguments");
+    HIPCHK(hipSetDevice(c->device));
+    ncclUniqueId uid;
+    memcpy(&uid, id, 128);
+    if (c->comm) {
+        ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+    }
+    NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_gather_framebuffer(khp_ctx* c, const khp_render_params* p, int root) {
+    khp_status s = check_params(c, p);
+    if (s != KHP_OK) return s;
+    if (!c->comm) return fail(KHP_ENOTREADY, "khp_comm_init first");
+    if (!c->fb.p || c->fbW != p->width || c->fbH != p->height) return fail(KHP_ENOTREADY, "render first");
+    if (root < 0 || root >= c->nranks) return fail(KHP_EINVAL, "bad root");
+    if (p->tile_nranks != (uint32_t)c->nranks) return fail(KHP_EINVAL, "tile_nranks must equal the comm size");
+    HIPCHK(hipSetDevice(c->device));
+    uint32_t T = p->tile_size ? p->tile_size : 64;
+    if (c->rank != root) {
+        std::vector<uint32_t> mine;
+        owned_pixels(p->width, p->height, T, (uint32_t)c->rank, (uint32_t)c->nranks, mine);
+        HIPCHK(upload(c->stage_pix, mine.data(), mine.size(), c->stream));
+        HIPCHK(c->stage.ensure(mine.size() * 3 * sizeof(float) + 16));
+        uint32_t P = (uint32_t)mine.size();
+        if (P) hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
+                                  c->stage_pix.as<uint32_t>(), P, c->stage.as<float>());
+        NCCLCHK(ncclSend(c->stage.p, (size_t)P * 3, ncclFloat32, root, c->comm, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return KHP_OK;
+    }
+    // root: receive every other rank's pixels, then scatter them into the framebuffer
+    std::vector<std::vector<uint32_t>> lists((size_t)c->nranks);
+    size_t total = 0;
+    for (int r = 0; r < c->nranks; ++r) {
+        if (r == root) continue;
+        owned_pixels(p->width, p->height, T, (uint32_t)r, (uint32_t)c->nranks, lists[r]);
+        total += lists[r].size();
+    }
+    HIPCHK(c->stage.ensure(total * 3 * sizeof(float) + 16));
+    HIPCHK(c->stage2.ensure(total * sizeof(uint32_t) + 16));
+    std::vector<uint32_t> flat;
+    flat.reserve(total);
+    for (int r = 0; r < c->nranks; ++r) flat.insert(flat.end(), lists[r].begin(), lists[r].end());
+    HIPCHK(hipMemcpyAsync(c->stage2.p, flat.data(), flat.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(ncclGroupStart());
+    size_t off = 0;
+    for (int r = 0; r < c->nranks; ++r) {
+        if (r == root) continue;
+        NCCLCHK(ncclRecv(c->stage.as<float>() + off * 3, lists[r].size() * 3, ncclFloat32, r, c->comm, c->stream));
+        off += lists[r].size();
+    }
+    NCCLCHK(ncclGroupEnd());
+    if (total)
+        hipLaunchKernelGGL(k_unpack, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, c->stream,
+                           c->fb.as<float>(), c->stage2.as<uint32_t>(), (uint32_t)total, c->stage.as<float>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return KHP_OK;
+}

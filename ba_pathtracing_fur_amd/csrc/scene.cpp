@@ -1,0 +1,624 @@
+// scene.cpp -- host side of the core: flatten (Triangle / Cylinder ctor
+// state), binned-SAH BVH build, device record layout, and the host helpers of
+// the C-ABI (camera, fibers -> cones, seeded generators, registries).
+// Built with -ffp-contract=off so every float matches the device and the
+// documented semantics bit-for-bit.
+#include "scene.h"
+
+#include <string.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <thread>
+
+namespace khp {
+
+static constexpr float RAY_EPS = 1e-4f;  // KIRK::cRayEpsilon (Common/Ray.h:9)
+
+static void set_comp(v3& a, int i, float v) {
+    if (i == 0) a.x = v;
+    else if (i == 1) a.y = v;
+    else a.z = v;
+}
+
+// Light ctors + QuadLight::calcParams + Light::transform(identity)
+// (Common/Light.h ctors, Light.cpp:112-118, 216-220, 263-276).
+void light_init(DevLight& L, const khp_light& in) {
+    memset(&L, 0, sizeof(L));
+    L.kind = in.kind;
+    for (int i = 0; i < 3; ++i) {
+        L.color[i] = in.color[i];
+        L.position[i] = in.position[i];
+    }
+    L.c = in.att_const;
+    L.l = in.att_lin;
+    L.q = in.att_quad;
+    L.radius = in.radius;
+    v3 dir1 = normalize(ld3(in.direction));
+    if (in.kind == KHP_LIGHT_POINT) dir1 = normalize(mk(0.0f, 0.0f, 0.0f));
+    if (in.kind == KHP_LIGHT_SPOT) {
+        L.outer = in.outer_angle;
+        L.inner = (in.inner_angle < 0.0f || in.inner_angle > in.outer_angle) ? in.outer_angle : in.inner_angle;
+    }
+    if (in.kind == KHP_LIGHT_QUAD) {
+        v3 n = dir1, s;
+        if (fabsf(n.x) > fabsf(n.y)) s = mk(-n.z, 0.0f, n.x) / sqrtf(n.x * n.x + n.z * n.z);
+        else s = mk(0.0f, n.z, -n.y) / sqrtf(n.y * n.y + n.z * n.z);
+        v3 t = cross(n, s);
+        float sx = in.size[0], sy = in.size[1];
+        v3 p = ld3(in.position);
+        v3 vs[4] = {(p + (s * -sx) / 2.0f) + (t * -sy) / 2.0f, (p + (s * sx) / 2.0f) + (t * -sy) / 2.0f,
+                    (p + (s * sx) / 2.0f) + (t * sy) / 2.0f, (p + (s * -sx) / 2.0f) + (t * sy) / 2.0f};
+        for (int k = 0; k < 4; ++k) {
+            L.vert[k][0] = vs[k].x;
+            L.vert[k][1] = vs[k].y;
+            L.vert[k][2] = vs[k].z;
+        }
+        L.radius = sqrtf((sx * sy) / PIF);
+    }
+    v3 d = normalize(dir1);
+    L.direction[0] = d.x;
+    L.direction[1] = d.y;
+    L.direction[2] = d.z;
+}
+
+// Triangle::Triangle (Common/Triangle.cpp:3-129), identity model matrix.
+static void tri_ctor(HostScene& hs, uint32_t id, v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc, uint32_t mat) {
+    v3 bmin = vmin(vmin(a, b), c) - mk(RAY_EPS, RAY_EPS, RAY_EPS);
+    v3 bmax = vmax(vmax(a, b), c) + mk(RAY_EPS, RAY_EPS, RAY_EPS);
+    v3 diff = bmax - bmin;
+    int lA = 0;
+    float longest = diff.x;
+    if (diff.y > longest) { longest = diff.y; lA = 1; }
+    if (diff.z > longest) { longest = diff.z; lA = 2; }
+    v3 Na = normalize(na), Nb = normalize(nb), Nc = normalize(nc);
+    v3 A = a, B = b, C = c, nA = Na, nB = Nb, nC = Nc;
+    float ca = comp(a, lA), cb = comp(b, lA), cc = comp(c, lA);
+    // six orderings, later matches override earlier ones (ties)
+    if (ca <= cb && cb <= cc) { A = a; B = b; C = c; nA = Na; nB = Nb; nC = Nc; }
+    if (cb <= ca && ca <= cc) { A = b; B = a; C = c; nA = Nb; nB = Na; nC = Nc; }
+    if (ca <= cc && cc <= cb) { A = a; B = c; C = b; nA = Na; nB = Nc; nC = Nb; }
+    if (cc <= ca && ca <= cb) { A = c; B = a; C = b; nA = Nc; nB = Na; nC = Nb; }
+    if (cb <= cc && cc <= ca) { A = b; B = c; C = a; nA = Nb; nB = Nc; nC = Na; }
+    if (cc <= cb && cb <= ca) { A = c; B = b; C = a; nA = Nc; nB = Nb; nC = Na; }
+    v3 ab = B - A, ac = C - A, bc = C - B;
+    if (comp(ab, lA) == 0.0f) set_comp(ab, lA, 0.0001f);
+    if (comp(ac, lA) == 0.0f) set_comp(ac, lA, 0.0001f);
+    if (comp(bc, lA) == 0.0f) set_comp(bc, lA, 0.0001f);
+    v3 cen = ((A + B) + C) / 3.0f;
+    float* r = &hs.rec[16 * (size_t)id];
+    float rr[16] = {A.x, A.y, A.z, f_from_bits(TRI_TAG), ab.x, ab.y, ab.z, 0.0f,
+                    ac.x, ac.y, ac.z, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    memcpy(r, rr, sizeof(rr));
+    float* bb = &hs.bounds[6 * (size_t)id];
+    bb[0] = bmin.x; bb[1] = bmin.y; bb[2] = bmin.z; bb[3] = bmax.x; bb[4] = bmax.y; bb[5] = bmax.z;
+    float* ce = &hs.centroid[3 * (size_t)id];
+    ce[0] = cen.x; ce[1] = cen.y; ce[2] = cen.z;
+    float* tn = &hs.tri_nrm[9 * (size_t)id];
+    float nn[9] = {nA.x, nA.y, nA.z, nB.x, nB.y, nB.z, nC.x, nC.y, nC.z};
+    memcpy(tn, nn, sizeof(nn));
+    hs.aux[id] = Aux{0.0f, mat, id, 0u};
+}
+
+// Cylinder::Cylinder + computeBounds (Common/Cylinder.cpp:5-67, 306-336).
+static void cone_ctor(HostScene& hs, uint32_t id, uint32_t ci, v3 base, v3 apex, float r0, float r1, uint32_t mat) {
+    v3 v = apex - base;
+    float height = length(v);
+    v = normalize(v);
+    v3 tmp = mk(0.0f, 1.0f, 0.0f);
+    if (1.0f - fabsf(dot(tmp, v)) < RAY_EPS) tmp = mk(0.0f, 0.0f, 1.0f);
+    v3 u = normalize(cross(v, tmp));
+    v3 w = normalize(cross(u, v));
+    u = normalize(u);
+    v = normalize(v);
+    w = normalize(w);
+    float slope = (r0 - r1) / height;
+    float base_d = dot(base, v);
+    float min_d = dot(v, base), max_d = dot(v, apex);
+    if (max_d < min_d) std::swap(min_d, max_d);
+    float radius = (r0 > r1) ? r0 + 1e-6f : r1 + 1e-6f;
+    v3 l0 = mk(-radius, 0.0f, -radius), l1 = mk(radius, height, radius);
+    v3 corners[8] = {mk(l0.x, l1.y, l1.z), mk(l0.x, l0.y, l1.z), mk(l1.x, l0.y, l1.z), mk(l1.x, l1.y, l1.z),
+                     mk(l1.x, l1.y, l0.z), mk(l1.x, l0.y, l0.z), mk(l0.x, l0.y, l0.z), mk(l0.x, l1.y, l0.z)};
+    v3 bmin = mk(FLT_MAX, FLT_MAX, FLT_MAX), bmax = mk(-FLT_MAX, -FLT_MAX, -FLT_MAX);
+    for (int i = 0; i < 8; ++i) {
+        v3 q = corners[i];
+        v3 P = mk((u.x * q.x + v.x * q.y) + w.x * q.z, (u.y * q.x + v.y * q.y) + w.y * q.z,
+                  (u.z * q.x + v.z * q.y) + w.z * q.z) + base;
+        if (P.x < bmin.x) bmin.x = P.x;
+        if (P.x > bmax.x) bmax.x = P.x;
+        if (P.y < bmin.y) bmin.y = P.y;
+        if (P.y > bmax.y) bmax.y = P.y;
+        if (P.z < bmin.z) bmin.z = P.z;
+        if (P.z > bmax.z) bmax.z = P.z;
+    }
+    v3 cen = base + (apex - base) * 0.4f;  // Cylinder.cpp:50
+    float rr[16] = {base.x, base.y, base.z, r0, u.x, u.y, u.z, slope, v.x, v.y, v.z, min_d, w.x, w.y, w.z, max_d};
+    memcpy(&hs.rec[16 * (size_t)id], rr, sizeof(rr));
+    float* bb = &hs.bounds[6 * (size_t)id];
+    bb[0] = bmin.x; bb[1] = bmin.y; bb[2] = bmin.z; bb[3] = bmax.x; bb[4] = bmax.y; bb[5] = bmax.z;
+    float* ce = &hs.centroid[3 * (size_t)id];
+    ce[0] = cen.x; ce[1] = cen.y; ce[2] = cen.z;
+    hs.cone_height[ci] = height;
+    hs.aux[id] = Aux{base_d, mat, id, 1u};
+}
+
+std::string flatten_scene(const khp_scene* s, HostScene& hs) {
+    if (!s) return "scene is null";
+    uint64_t n = (uint64_t)s->n_tris + s->n_cones;
+    if (n == 0) return "Your scene is empty!";  // BoundingBox.cpp:121-122
+    if (n >= (1ull << 31)) return "too many objects";
+    if (s->n_tris && (!s->tri_v || !s->tri_n || !s->tri_mat)) return "triangle arrays missing";
+    if (s->n_cones && (!s->cone_base_r0 || !s->cone_apex_r1 || !s->cone_mat)) return "cone arrays missing";
+    if (s->n_materials == 0 || !s->materials) return "no materials";
+    if (s->n_lights && !s->lights) return "lights missing";
+    for (uint32_t i = 0; i < s->n_materials; ++i) {
+        const khp_material& m = s->materials[i];
+        if (m.bsdf < 0 || m.bsdf >= KHP_BSDF_COUNT) return "unknown BSDF kind";
+        if (m.shader < 0 || m.shader >= KHP_SHADER_COUNT) return "unknown shader kind";
+    }
+    for (uint32_t i = 0; i < s->n_lights; ++i)
+        if (s->lights[i].kind < 0 || s->lights[i].kind > KHP_LIGHT_SUN) return "unknown light kind";
+    hs = HostScene();
+    hs.n_tris = s->n_tris;
+    hs.n_cones = s->n_cones;
+    hs.n_obj = (uint32_t)n;
+    hs.rec.resize(16 * n);
+    hs.aux.resize(n);
+    hs.bounds.resize(6 * n);
+    hs.centroid.resize(3 * n);
+    hs.tri_nrm.resize(9 * (size_t)s->n_tris);
+    hs.cone_height.resize(s->n_cones);
+    for (uint32_t i = 0; i < s->n_tris; ++i)
+        if (s->tri_mat[i] >= s->n_materials) return "triangle material index out of range";
+    for (uint32_t i = 0; i < s->n_cones; ++i)
+        if (s->cone_mat[i] >= s->n_materials) return "cone material index out of range";
+    unsigned nt = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+    auto work = [&](unsigned t) {
+        for (uint32_t i = t; i < s->n_tris; i += nt) {
+            const float* v = s->tri_v + 9 * (size_t)i;
+            const float* nn = s->tri_n + 9 * (size_t)i;
+            tri_ctor(hs, i, ld3(v), ld3(v + 3), ld3(v + 6), ld3(nn), ld3(nn + 3), ld3(nn + 6), s->tri_mat[i]);
+        }
+        for (uint32_t i = t; i < s->n_cones; i += nt) {
+            const float* b = s->cone_base_r0 + 4 * (size_t)i;
+            const float* a = s->cone_apex_r1 + 4 * (size_t)i;
+            cone_ctor(hs, s->n_tris + i, i, ld3(b), ld3(a), b[3], a[3], s->cone_mat[i]);
+        }
+    };
+    if (n < 65536) nt = 1;
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& t : th) t.join();
+    hs.mats.assign(s->materials, s->materials + s->n_materials);
+    hs.lights.resize(s->n_lights);
+    for (uint32_t i = 0; i < s->n_lights; ++i) light_init(hs.lights[i], s->lights[i]);
+    hs.env = s->env;
+    hs.cam = s->camera;
+    return std::string();
+}
+
+// ---- binned SAH BVH (CPU_BVH.cpp:16-44, 95-138, 357-552; BoundingBox.cpp) ----
+struct Box {
+    v3 mn, mx;
+};
+static inline float smin(float a, float b) { return (b < a) ? b : a; }  // std::min
+static inline float smax(float a, float b) { return (a < b) ? b : a; }  // std::max
+static inline Box box_empty() { return Box{mk(FLT_MAX, FLT_MAX, FLT_MAX), mk(-FLT_MAX, -FLT_MAX, -FLT_MAX)}; }
+static inline void grow(Box& b, v3 p) {
+    b.mn = mk(smin(b.mn.x, p.x), smin(b.mn.y, p.y), smin(b.mn.z, p.z));
+    b.mx = mk(smax(b.mx.x, p.x), smax(b.mx.y, p.y), smax(b.mx.z, p.z));
+}
+static inline void grow(Box& b, const Box& o) {
+    b.mn = mk(smin(b.mn.x, o.mn.x), smin(b.mn.y, o.mn.y), smin(b.mn.z, o.mn.z));
+    b.mx = mk(smax(b.mx.x, o.mx.x), smax(b.mx.y, o.mx.y), smax(b.mx.z, o.mx.z));
+}
+static inline float area(const Box& b) {
+    v3 s = b.mx - b.mn;
+    return 2.0f * (s.x * s.y + s.x * s.z + s.y * s.z);
+}
+static inline bool worth(const Box& b) {
+    v3 d = b.mx - b.mn;
+    return d.x > 0.0f && d.y > 0.0f && d.z > 0.0f;
+}
+
+struct Builder {
+    HostScene& hs;
+    const float* cen;
+    uint32_t* ids;
+    float cget(uint32_t oid, int axis) const { return cen[3 * (size_t)oid + axis]; }
+    v3 cvec(uint32_t oid) const { return ld3(&cen[3 * (size_t)oid]); }
+
+    void partition(uint32_t first, uint32_t second, uint32_t& lsec, uint32_t& rfirst, const Box& cb, Box& lcb,
+                   Box& rcb) const {
+        float best = FLT_MAX;
+        int best_axis = 0, best_plane = 0;
+        constexpr int NB = 16, NP = 15;
+        float cbmins[3], ks[3];
+        for (int axis = 0; axis < 3; ++axis) {
+            const float cbmin = comp(cb.mn, axis);
+            const float cbmax = comp(cb.mx, axis);
+            const float cbdiff = cbmax - cbmin;
+            const float epsilon = 0.1f;
+            const float k = ((float)NB * (1.0f - epsilon)) / cbdiff;
+            cbmins[axis] = cbmin;
+            ks[axis] = k;
+            Box bb[NB];
+            uint32_t bn[NB];
+            for (int i = 0; i < NB; ++i) { bb[i] = box_empty(); bn[i] = 0; }
+            for (uint32_t id = first; id <= second; ++id) {
+                uint32_t oid = ids[id];
+                int bin = (int)(k * (cget(oid, axis) - cbmin));
+                grow(bb[bin], cvec(oid));
+                ++bn[bin];
+            }
+            uint32_t ln[NP];
+            Box lb[NP];
+            lb[0] = box_empty();
+            grow(lb[0], bb[0]);
+            ln[0] = bn[0];
+            for (int p = 1; p < NP; ++p) {
+                lb[p] = box_empty();
+                grow(lb[p], lb[p - 1]);
+                grow(lb[p], bb[p]);
+                ln[p] = ln[p - 1] + bn[p];
+            }
+            uint32_t rn[NP];
+            Box rb[NP];
+            for (int p = NP - 1; p >= 0; --p) {
+                rb[p] = box_empty();
+                grow(rb[p], bb[p + 1]);
+                rn[p] = bn[p + 1];
+                if (p != NP - 1) {
+                    grow(rb[p], rb[p + 1]);
+                    rn[p] += rn[p + 1];
+                }
+                float cost = area(lb[p]) * (float)ln[p] + area(rb[p]) * (float)rn[p];
+                if (cost < best) {
+                    best = cost;
+                    best_axis = axis;
+                    best_plane = p;
+                    lcb = lb[p];
+                    rcb = rb[p];
+                }
+            }
+        }
+        const float cbmin = cbmins[best_axis], k = ks[best_axis];
+        int left = (int)first, right = (int)second;
+        bool ls = false, rs = false;
+        while (left < right) {
+            if (!ls) {
+                int b = (int)(k * (cget(ids[left], best_axis) - cbmin));
+                if (b > best_plane) ls = true;
+                else ++left;
+            }
+            if (!rs) {
+                int b = (int)(k * (cget(ids[right], best_axis) - cbmin));
+                if (b <= best_plane) rs = true;
+                else --right;
+            }
+            if (ls && rs) {
+                std::swap(ids[left], ids[right]);
+                ls = rs = false;
+                ++left;
+                --right;
+            }
+        }
+        if (left > right) { lsec = (uint32_t)right; rfirst = (uint32_t)left; }
+        else if (ls) { lsec = (uint32_t)(left - 1); rfirst = (uint32_t)left; }
+        else if (rs) { lsec = (uint32_t)right; rfirst = (uint32_t)(right + 1); }
+        else {
+            int b = (int)(k * (cget(ids[left], best_axis) - cbmin));
+            if (b > best_plane) { lsec = (uint32_t)(left - 1); rfirst = (uint32_t)left; }
+            else { lsec = (uint32_t)left; rfirst = (uint32_t)(left + 1); }
+        }
+    }
+
+    // BVHNode::split; nodes appended to `out` in DFS preorder, child indices relative to `out`.
+    int32_t split(uint32_t first, uint32_t second, const Box& cb, uint32_t depth, std::vector<BuildNode>& out,
+                  uint32_t& maxdepth, uint32_t& maxleaf, int par) const {
+        int32_t ni = (int32_t)out.size();
+        out.push_back(BuildNode{});
+        Box bv = box_empty();
+        const float* bounds = hs.bounds.data();
+        for (uint32_t id = first; id <= second; ++id) {
+            const float* b = &bounds[6 * (size_t)ids[id]];
+            bv.mn = mk(smin(bv.mn.x, b[0]), smin(bv.mn.y, b[1]), smin(bv.mn.z, b[2]));
+            bv.mx = mk(smax(bv.mx.x, b[3]), smax(bv.mx.y, b[4]), smax(bv.mx.z, b[5]));
+        }
+        out[ni].mn = bv.mn;
+        out[ni].mx = bv.mx;
+        if (depth > maxdepth) maxdepth = depth;
+        if (second - first > 1u && worth(cb)) {
+            uint32_t lsec, rfirst;
+            Box lcb, rcb;
+            partition(first, second, lsec, rfirst, cb, lcb, rcb);
+            out[ni].count = 0;
+            if (par > 0 && second - first > 32768u) {
+                std::vector<BuildNode> L, R;
+                uint32_t ld = 0, rd = 0, lm = 0, rm = 0;
+                std::thread t([&] { split(first, lsec, lcb, depth + 1, L, ld, lm, par - 1); });
+                split(rfirst, second, rcb, depth + 1, R, rd, rm, par - 1);
+                t.join();
+                int32_t lbase = (int32_t)out.size();
+                for (auto nd : L) {
+                    if (nd.count == 0) { nd.left += lbase; nd.right += lbase; }
+                    out.push_back(nd);
+                }
+                int32_t rbase = (int32_t)out.size();
+                for (auto nd : R) {
+                    if (nd.count == 0) { nd.left += rbase; nd.right += rbase; }
+                    out.push_back(nd);
+                }
+                out[ni].left = lbase;
+                out[ni].right = rbase;
+                maxdepth = std::max(maxdepth, std::max(ld, rd));
+                maxleaf = std::max(maxleaf, std::max(lm, rm));
+            } else {
+                int32_t l = split(first, lsec, lcb, depth + 1, out, maxdepth, maxleaf, 0);
+                int32_t r = split(rfirst, second, rcb, depth + 1, out, maxdepth, maxleaf, 0);
+                out[ni].left = l;
+                out[ni].right = r;
+            }
+        } else {
+            out[ni].first = (int32_t)first;
+            out[ni].count = (int32_t)(second - first + 1);
+            out[ni].left = out[ni].right = -1;
+            maxleaf = std::max(maxleaf, second - first + 1);
+        }
+        return ni;
+    }
+};
+
+void build_bvh(HostScene& hs, int n_threads) {
+    hs.ids.resize(hs.n_obj);
+    Box cb = box_empty();
+    for (uint32_t i = 0; i < hs.n_obj; ++i) {
+        hs.ids[i] = i;
+        grow(cb, ld3(&hs.centroid[3 * (size_t)i]));
+    }
+    Builder b{hs, hs.centroid.data(), hs.ids.data()};
+    hs.nodes.clear();
+    hs.nodes.reserve(2 * (size_t)hs.n_obj);
+    int par = 0;
+    while ((1 << par) < n_threads && par < 8) ++par;
+    hs.depth = 0;
+    hs.max_leaf = 0;
+    b.split(0, hs.n_obj - 1, cb, 1, hs.nodes, hs.depth, hs.max_leaf, par);
+}
+
+void make_device_layout(HostScene& hs) {
+    // interior index per preorder node
+    std::vector<int32_t> inner(hs.nodes.size(), -1);
+    int32_t ni = 0;
+    for (size_t i = 0; i < hs.nodes.size(); ++i)
+        if (hs.nodes[i].count == 0) inner[i] = ni++;
+    hs.dnodes.assign((size_t)ni, DevNode{});
+    auto child_ref = [&](int32_t c, int32_t& ref, int32_t& cnt) {
+        const BuildNode& n = hs.nodes[c];
+        if (n.count > 0) { ref = n.first; cnt = n.count; }
+        else { ref = inner[c]; cnt = 0; }
+    };
+    for (size_t i = 0; i < hs.nodes.size(); ++i) {
+        const BuildNode& n = hs.nodes[i];
+        if (n.count != 0) continue;
+        DevNode& d = hs.dnodes[inner[i]];
+        const BuildNode& L = hs.nodes[n.left];
+        const BuildNode& R = hs.nodes[n.right];
+        float a[4] = {L.mn.x, L.mn.y, L.mn.z, L.mx.x};
+        float b[4] = {L.mx.y, L.mx.z, R.mn.x, R.mn.y};
+        float c[4] = {R.mn.z, R.mx.x, R.mx.y, R.mx.z};
+        memcpy(d.a, a, sizeof(a));
+        memcpy(d.b, b, sizeof(b));
+        memcpy(d.c, c, sizeof(c));
+        child_ref(n.left, d.ref[0], d.cnt[0]);
+        child_ref(n.right, d.ref[1], d.cnt[1]);
+    }
+    child_ref(0, hs.root_ref, hs.root_cnt);
+    const BuildNode& r = hs.nodes[0];
+    float rb[6] = {r.mn.x, r.mn.y, r.mn.z, r.mx.x, r.mx.y, r.mx.z};
+    memcpy(hs.root_box, rb, sizeof(rb));
+    hs.slot_rec.resize(16 * (size_t)hs.n_obj);
+    hs.slot_aux.resize(hs.n_obj);
+    for (uint32_t s = 0; s < hs.n_obj; ++s) {
+        uint32_t o = hs.ids[s];
+        memcpy(&hs.slot_rec[16 * (size_t)s], &hs.rec[16 * (size_t)o], 16 * sizeof(float));
+        hs.slot_aux[s] = hs.aux[o];
+    }
+}
+
+}  // namespace khp
+
+// ============================================================================
+//  C-ABI host helpers
+// ============================================================================
+using namespace khp;
+
+static const char* kBsdfNames[KHP_BSDF_COUNT] = {
+    "LambertianReflectionBSDF", "SpecularReflectionBSDF", "SpecularTransmissionBSDF", "GlossyBSDF",
+    "GlassBSDF", "MilkGlassBSDF", "LambertianTransmissionBSDF", "EmissionBSDF", "TransparentBSDF",
+    "MarschnerHairBSDF", "DEonHairBSDF"};
+
+extern "C" int khp_bsdf_kind_from_name(const char* name) {
+    if (!name) return -1;
+    for (int i = 0; i < KHP_BSDF_COUNT; ++i)
+        if (strcmp(name, kBsdfNames[i]) == 0) return i;
+    return -1;
+}
+extern "C" const char* khp_bsdf_name(int kind) {
+    return (kind >= 0 && kind < KHP_BSDF_COUNT) ? kBsdfNames[kind] : nullptr;
+}
+extern "C" int khp_shader_kind_from_name(const char* name) {
+    if (!name) return -1;
+    // ShaderFactory names (SimpleShader.h:29, MarschnerHairShader.h:29)
+    if (strcmp(name, "SimpleShader") == 0) return KHP_SHADER_SIMPLE;
+    if (strcmp(name, "MarschnerHairShader") == 0) return KHP_SHADER_MARSCHNER_HAIR;
+    return -1;
+}
+
+// Camera::applyParameters (Common/Camera.cpp:6-37), identity node transform.
+extern "C" khp_status khp_camera_setup(const float position[3], const float look_at[3], const float up[3],
+                                       float sensor_w, float sensor_h, float focal_length, uint32_t width,
+                                       uint32_t height, khp_camera* out) {
+    if (!position || !look_at || !up || !out || width == 0 || height == 0 || focal_length <= 0.0f)
+        return KHP_EINVAL;
+    v3 pos = ld3(position), la = ld3(look_at), upv = ld3(up);
+    float aspect = (float)width / (float)height;
+    v3 az = normalize(-la);
+    v3 ax = normalize(cross(upv, az));
+    v3 ay = normalize(cross(az, ax));
+    float diam = sqrtf(sensor_w * sensor_w + sensor_h * sensor_h);
+    float fov = 2.0f * k_atanf(diam / (2.0f * focal_length));
+    float half = 0.5f * fov;
+    float sy = k_sinf(half) / k_cosf(half);
+    float sx = sy * aspect;
+    float px = 2.0f * sx / (float)width;
+    v3 bl = ((pos - az) - ay * sy) - ax * sx;
+    for (int i = 0; i < 3; ++i) {
+        out->position[i] = comp(pos, i);
+        out->bottom_left[i] = comp(bl, i);
+        out->axis_x[i] = comp(ax, i);
+        out->axis_y[i] = comp(ay, i);
+    }
+    out->pixel_size = px;
+    return KHP_OK;
+}
+
+// CPU_Scene::flattenNode fiber -> Cylinder arguments (CPU_Scene.cpp:121-144).
+extern "C" khp_status khp_fibers_to_cones(uint32_t n_fibers, uint32_t verts, const float* positions,
+                                          const float* radii, float* out_base_r0, float* out_apex_r1) {
+    if (verts < 2 || !positions || !radii || !out_base_r0 || !out_apex_r1) return KHP_EINVAL;
+    size_t k = 0;
+    for (uint32_t f = 0; f < n_fibers; ++f) {
+        const float* P = positions + (size_t)f * verts * 3;
+        const float* R = radii + (size_t)f * verts;
+        for (uint32_t c = 0; c + 1 < verts; ++c, ++k) {
+            v3 basepos = ld3(P + 3 * c), apexpos = ld3(P + 3 * (c + 1));
+            float br = R[c];
+            basepos = basepos - (apexpos - basepos) * 0.008f;
+            br -= (c > 3) ? 0.1f * br : 0.05f * br;
+            float* ob = out_base_r0 + 4 * k;
+            float* oa = out_apex_r1 + 4 * k;
+            ob[0] = basepos.x; ob[1] = basepos.y; ob[2] = basepos.z; ob[3] = br;
+            oa[0] = apexpos.x; oa[1] = apexpos.y; oa[2] = apexpos.z; oa[3] = R[c + 1];
+        }
+    }
+    return KHP_OK;
+}
+
+// Seeded hairball: Mesh::addFurToFaces recurrence (Mesh.cpp:118-142) in each
+// root's tangent frame (local y = sphere normal, local z = random tangent).
+extern "C" khp_status khp_gen_hairball(uint32_t n, uint32_t verts, const float center[3], float ball_r,
+                                       float root_r, uint32_t seed, float* positions, float* radii) {
+    if (verts < 2 || verts > 64 || !center || !positions || !radii) return KHP_EINVAL;
+    // glm::log((float)i) for i = 0..64 (float-rounded natural logs)
+    static float lnt[65];
+    static bool init = false;
+    if (!init) {
+        for (int i = 1; i <= 64; ++i) lnt[i] = (float)log((double)i);
+        init = true;
+    }
+    v3 C = ld3(center);
+    uint32_t key0 = lowbias32(seed ^ 0x48414952u);
+    for (uint32_t s = 0; s < n; ++s) {
+        uint32_t key = lowbias32(key0 ^ s);
+        float u0 = draw_u01(key, 0), u1 = draw_u01(key, 1), u2 = draw_u01(key, 2);
+        float z = 1.0f - 2.0f * u0;
+        float rxy = sqrtf(gmax(0.0f, 1.0f - z * z));
+        float phi = 2.0f * PIF * u1;
+        v3 nrm = mk(rxy * k_cosf(phi), z, rxy * k_sinf(phi));
+        v3 ref = fabsf(nrm.y) < 0.9f ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+        v3 t0 = normalize(cross(nrm, ref));
+        v3 b0 = cross(nrm, t0);
+        float psi = 2.0f * PIF * u2;
+        v3 tan = t0 * k_cosf(psi) + b0 * k_sinf(psi);
+        float* P = positions + (size_t)s * verts * 3;
+        float* R = radii + (size_t)s * verts;
+        v3 pos = C + nrm * ball_r;
+        pos = pos - nrm * 0.003f;  // "move start position down" (Mesh.cpp:115)
+        float radius = root_r;
+        P[0] = pos.x; P[1] = pos.y; P[2] = pos.z;
+        R[0] = radius;
+        uint32_t k = 1;
+        for (int i = (int)verts; i > 1; --i, ++k) {
+            float off_y = lnt[i] / 90.0f;
+            v3 point = (pos + nrm * off_y) + tan * 0.06f;
+            radius -= radius / ((float)i + 5.0f);
+            P[3 * k] = point.x; P[3 * k + 1] = point.y; P[3 * k + 2] = point.z;
+            R[k] = radius;
+            pos = point;
+        }
+        R[verts - 1] = 0.001f;  // Mesh.cpp:142
+    }
+    return KHP_OK;
+}
+
+static void push_tri(std::vector<float>& v, std::vector<float>& n, v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc) {
+    v3 vs[3] = {a, b, c}, ns[3] = {na, nb, nc};
+    for (int i = 0; i < 3; ++i) {
+        v.push_back(vs[i].x); v.push_back(vs[i].y); v.push_back(vs[i].z);
+        n.push_back(ns[i].x); n.push_back(ns[i].y); n.push_back(ns[i].z);
+    }
+}
+
+extern "C" khp_status khp_gen_icosphere(uint32_t subdiv, const float center[3], float radius, float* tri_v,
+                                        float* tri_n) {
+    if (subdiv > 8 || !center || !tri_v || !tri_n) return KHP_EINVAL;
+    const float t = 1.61803398874989484820f;
+    std::vector<v3> P = {mk(-1, t, 0), mk(1, t, 0), mk(-1, -t, 0), mk(1, -t, 0), mk(0, -1, t), mk(0, 1, t),
+                         mk(0, -1, -t), mk(0, 1, -t), mk(t, 0, -1), mk(t, 0, 1), mk(-t, 0, -1), mk(-t, 0, 1)};
+    for (auto& p : P) p = normalize(p);
+    std::vector<uint32_t> F = {0, 11, 5, 0, 5, 1, 0, 1, 7, 0, 7, 10, 0, 10, 11, 1, 5, 9, 5, 11, 4, 11, 10, 2,
+                               10, 7, 6, 7, 1, 8, 3, 9, 4, 3, 4, 2, 3, 2, 6, 3, 6, 8, 3, 8, 9, 4, 9, 5, 2, 4, 11,
+                               6, 2, 10, 8, 6, 7, 9, 8, 1};
+    for (uint32_t s = 0; s < subdiv; ++s) {
+        std::vector<uint32_t> G;
+        G.reserve(F.size() * 4);
+        for (size_t i = 0; i < F.size(); i += 3) {
+            uint32_t a = F[i], b = F[i + 1], c = F[i + 2];
+            v3 ab = normalize((P[a] + P[b]) * 0.5f), bc = normalize((P[b] + P[c]) * 0.5f),
+               ca = normalize((P[c] + P[a]) * 0.5f);
+            uint32_t iab = (uint32_t)P.size(); P.push_back(ab);
+            uint32_t ibc = (uint32_t)P.size(); P.push_back(bc);
+            uint32_t ica = (uint32_t)P.size(); P.push_back(ca);
+            uint32_t q[12] = {a, iab, ica, b, ibc, iab, c, ica, ibc, iab, ibc, ica};
+            G.insert(G.end(), q, q + 12);
+        }
+        F.swap(G);
+    }
+    v3 C = ld3(center);
+    std::vector<float> vv, nn;
+    for (size_t i = 0; i < F.size(); i += 3) {
+        v3 a = P[F[i]], b = P[F[i + 1]], c = P[F[i + 2]];
+        push_tri(vv, nn, C + a * radius, C + b * radius, C + c * radius, a, b, c);
+    }
+    memcpy(tri_v, vv.data(), vv.size() * sizeof(float));
+    memcpy(tri_n, nn.data(), nn.size() * sizeof(float));
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_gen_torus(uint32_t nu, uint32_t nv, const float center[3], float R, float r,
+                                    float* tri_v, float* tri_n) {
+    if (nu < 3 || nv < 3 || !center || !tri_v || !tri_n) return KHP_EINVAL;
+    v3 C = ld3(center);
+    auto P = [&](uint32_t i, uint32_t j, v3& pos, v3& nrm) {
+        float a = 2.0f * PIF * (float)(i % nu) / (float)nu;
+        float b = 2.0f * PIF * (float)(j % nv) / (float)nv;
+        float ca = k_cosf(a), sa = k_sinf(a), cb = k_cosf(b), sb = k_sinf(b);
+        nrm = mk(ca * cb, sb, sa * cb);
+        pos = C + mk((R + r * cb) * ca, r * sb, (R + r * cb) * sa);
+    };
+    size_t k = 0;
+    for (uint32_t i = 0; i < nu; ++i)
+        for (uint32_t j = 0; j < nv; ++j) {
+            v3 p00, n00, p10, n10, p01, n01, p11, n11;
+            P(i, j, p00, n00); P(i + 1, j, p10, n10); P(i, j + 1, p01, n01); P(i + 1, j + 1, p11, n11);
+            v3 tv[6] = {p00, p01, p10, p10, p01, p11}, tn[6] = {n00, n01, n10, n10, n01, n11};
+            for (int q = 0; q < 6; ++q, ++k) {
+                tri_v[3 * k] = tv[q].x; tri_v[3 * k + 1] = tv[q].y; tri_v[3 * k + 2] = tv[q].z;
+                tri_n[3 * k] = tn[q].x; tri_n[3 * k + 1] = tn[q].y; tri_n[3 * k + 2] = tn[q].z;
+            }
+        }
+    return KHP_OK;
+}

@@ -1,0 +1,81 @@
+// scene.h -- host-side scene model of the core: the state KIRK's Triangle and
+// Cylinder constructors derive (flatten), the binned-SAH BVH, and the device
+// record layouts the kernels read.  Host only (g++), shared by render.hip.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/kirk_hip.h"
+#include "kmath.h"
+
+namespace khp {
+
+// ---- device record layouts (64 B per primitive, 64 B per interior node) ----
+// cone   : (base.xyz, r0) (u.xyz, slope) (v.xyz, min_d) (w.xyz, max_d)
+// triangle: (A.xyz, TRI_TAG) (ab.xyz, 0) (ac.xyz, 0) (0,0,0,0)
+constexpr uint32_t TRI_TAG = 0x7fc0deadu;
+// aux per slot: (base_d bits, material, object id, 1 if cone)
+struct Aux {
+    float base_d;
+    uint32_t mat;
+    uint32_t obj;
+    uint32_t is_cone;
+};
+// interior node: (L.min.xyz, L.max.x) (L.max.yz, R.min.xy) (R.min.z, R.max.xyz) (Lref, Rref, Lcnt, Rcnt)
+// child with cnt > 0 is a leaf covering slots [ref, ref+cnt); cnt == 0 -> interior node `ref`.
+struct DevNode {
+    float a[4], b[4], c[4];
+    int32_t ref[2], cnt[2];
+};
+static_assert(sizeof(DevNode) == 64, "node must be one 64 B record");
+
+// light state derived by the KIRK light ctors + Light::transform
+struct DevLight {
+    int32_t kind;
+    float color[3];
+    float position[3];
+    float direction[3];
+    float radius, c, l, q, inner, outer;
+    float vert[4][3];
+};
+
+struct BuildNode {
+    v3 mn, mx;
+    int32_t left, right, first, count;
+};
+
+struct HostScene {
+    uint32_t n_tris = 0, n_cones = 0, n_obj = 0;
+    // per object (object id order)
+    std::vector<float> rec;        // n_obj * 16
+    std::vector<Aux> aux;          // n_obj
+    std::vector<float> bounds;     // n_obj * 6
+    std::vector<float> centroid;   // n_obj * 3
+    std::vector<float> tri_nrm;    // n_tris * 9 (na, nb, nc after ctor reordering)
+    std::vector<float> cone_height;// n_cones
+    std::vector<khp_material> mats;
+    std::vector<DevLight> lights;
+    khp_environment env{};
+    khp_camera cam{};
+    // BVH
+    std::vector<BuildNode> nodes;  // DFS preorder
+    std::vector<uint32_t> ids;     // leaf-ordered object ids (slot -> object)
+    uint32_t depth = 0, max_leaf = 0;
+    // device layout
+    std::vector<DevNode> dnodes;   // interior nodes
+    std::vector<float> slot_rec;   // n_obj * 16, slot order
+    std::vector<Aux> slot_aux;     // slot order
+    int32_t root_ref = 0, root_cnt = 0;
+    float root_box[6] = {0, 0, 0, 0, 0, 0};
+};
+
+// Returns an error string (empty on success).
+std::string flatten_scene(const khp_scene* s, HostScene& hs);
+void build_bvh(HostScene& hs, int n_threads);
+void make_device_layout(HostScene& hs);
+void light_init(DevLight& L, const khp_light& in);
+
+}  // namespace khp

@@ -1,0 +1,153 @@
+"""ctypes view of the C-ABI in include/kirk_hip.h.
+
+The product path is libkirk_hip.so (HIP kernels for gfx950).  There is no CPU
+fallback: if the library is missing or no GPU is present, the calls fail
+loudly (RuntimeError), they never route anywhere else.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_uint8, c_uint32, c_uint64, c_double, c_void_p
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libkirk_hip.so")
+
+# enums (kirk_hip.h)
+KHP_OK, KHP_EINVAL, KHP_ENOMEM, KHP_EDEVICE, KHP_ENOTREADY, KHP_EUNSUPPORTED = range(6)
+STATUS_NAMES = {0: "KHP_OK", 1: "KHP_EINVAL", 2: "KHP_ENOMEM", 3: "KHP_EDEVICE", 4: "KHP_ENOTREADY",
+                5: "KHP_EUNSUPPORTED"}
+
+BSDF_NAMES = ["LambertianReflectionBSDF", "SpecularReflectionBSDF", "SpecularTransmissionBSDF", "GlossyBSDF",
+              "GlassBSDF", "MilkGlassBSDF", "LambertianTransmissionBSDF", "EmissionBSDF", "TransparentBSDF",
+              "MarschnerHairBSDF", "DEonHairBSDF"]
+SHADER_NAMES = ["SimpleShader", "MarschnerHairShader"]
+LIGHT_POINT, LIGHT_QUAD, LIGHT_SPOT, LIGHT_SUN = 0, 1, 2, 3
+
+RENDER_OUT_DEVICE = 1 << 0
+RENDER_NO_READBACK = 1 << 1
+CTX_STATS = 1 << 0
+
+F3 = c_float * 3
+
+
+class Material(ctypes.Structure):
+    _fields_ = [("bsdf", c_int32), ("shader", c_int32), ("diffuse", F3), ("specular", F3), ("volume", F3),
+                ("emission", F3), ("ior", c_float), ("roughness", c_float)]
+
+
+class Light(ctypes.Structure):
+    _fields_ = [("kind", c_int32), ("color", F3), ("position", F3), ("direction", F3), ("size", c_float * 2),
+                ("radius", c_float), ("att_const", c_float), ("att_lin", c_float), ("att_quad", c_float),
+                ("inner_angle", c_float), ("outer_angle", c_float)]
+
+
+class Environment(ctypes.Structure):
+    _fields_ = [("color", F3), ("ambient", F3)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("position", F3), ("bottom_left", F3), ("axis_x", F3), ("axis_y", F3), ("pixel_size", c_float)]
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [("n_tris", c_uint32), ("tri_v", POINTER(c_float)), ("tri_n", POINTER(c_float)),
+                ("tri_mat", POINTER(c_uint32)), ("n_cones", c_uint32), ("cone_base_r0", POINTER(c_float)),
+                ("cone_apex_r1", POINTER(c_float)), ("cone_mat", POINTER(c_uint32)), ("n_materials", c_uint32),
+                ("materials", POINTER(Material)), ("n_lights", c_uint32), ("lights", POINTER(Light)),
+                ("env", Environment), ("camera", Camera)]
+
+
+class RenderParams(ctypes.Structure):
+    _fields_ = [("width", c_uint32), ("height", c_uint32), ("spp", c_uint32), ("depth", c_uint32),
+                ("seed", c_uint32), ("first_sample", c_uint32), ("tile_size", c_uint32), ("tile_rank", c_uint32),
+                ("tile_nranks", c_uint32), ("flags", c_uint32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("n_objects", c_uint64), ("n_nodes", c_uint64), ("n_leaves", c_uint64), ("bvh_depth", c_uint32),
+                ("max_leaf_size", c_uint32), ("device_bytes", c_uint64), ("build_ms", c_double),
+                ("upload_ms", c_double), ("render_ms", c_double), ("extend_ms", c_double), ("shade_ms", c_double),
+                ("shadow_ms", c_double), ("other_ms", c_double), ("extend_rays", c_uint64),
+                ("shadow_rays", c_uint64), ("extend_launches", c_uint64), ("node_visits", c_uint64),
+                ("prim_tests", c_uint64), ("shadow_node_visits", c_uint64), ("shadow_prim_tests", c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# every symbol the header declares (checked by tests/test_abi.py)
+EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "khp_set_scene", "khp_build_accel",
+            "khp_render", "khp_read_framebuffer", "khp_trace_closest", "khp_trace_any", "khp_get_stats",
+            "khp_comm_unique_id", "khp_comm_init", "khp_gather_framebuffer", "khp_bsdf_kind_from_name",
+            "khp_bsdf_name", "khp_shader_kind_from_name", "khp_camera_setup", "khp_fibers_to_cones",
+            "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus"]
+
+_lib = None
+
+
+def fptr(a: np.ndarray):
+    return a.ctypes.data_as(POINTER(c_float))
+
+
+def uptr(a: np.ndarray):
+    return a.ctypes.data_as(POINTER(c_uint32))
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load libkirk_hip.so; raises RuntimeError if it was not built."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"HIP core not built: {p} missing (run __graft_entry__.build())")
+    lib = ctypes.CDLL(p)
+    P = POINTER
+    sig = {
+        "khp_create": (c_int, [P(c_void_p), c_int, c_uint32]),
+        "khp_destroy": (None, [c_void_p]),
+        "khp_last_error": (c_char_p, []),
+        "khp_abi_version": (c_int, []),
+        "khp_set_scene": (c_int, [c_void_p, P(SceneDesc)]),
+        "khp_build_accel": (c_int, [c_void_p]),
+        "khp_render": (c_int, [c_void_p, P(RenderParams), c_void_p]),
+        "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
+        "khp_trace_closest": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_int32),
+                                      P(c_float)]),
+        "khp_trace_any": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_uint8)]),
+        "khp_get_stats": (c_int, [c_void_p, P(Stats)]),
+        "khp_comm_unique_id": (c_int, [P(c_uint8)]),
+        "khp_comm_init": (c_int, [c_void_p, c_int, c_int, P(c_uint8)]),
+        "khp_gather_framebuffer": (c_int, [c_void_p, P(RenderParams), c_int]),
+        "khp_bsdf_kind_from_name": (c_int, [c_char_p]),
+        "khp_bsdf_name": (c_char_p, [c_int]),
+        "khp_shader_kind_from_name": (c_int, [c_char_p]),
+        "khp_camera_setup": (c_int, [P(c_float), P(c_float), P(c_float), c_float, c_float, c_float, c_uint32,
+                                     c_uint32, P(Camera)]),
+        "khp_fibers_to_cones": (c_int, [c_uint32, c_uint32, P(c_float), P(c_float), P(c_float), P(c_float)]),
+        "khp_gen_hairball": (c_int, [c_uint32, c_uint32, P(c_float), c_float, c_float, c_uint32, P(c_float),
+                                     P(c_float)]),
+        "khp_gen_icosphere": (c_int, [c_uint32, P(c_float), c_float, P(c_float), P(c_float)]),
+        "khp_gen_torus": (c_int, [c_uint32, c_uint32, P(c_float), c_float, c_float, P(c_float), P(c_float)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+class KhpError(RuntimeError):
+    def __init__(self, status: int, where: str, msg: str):
+        super().__init__(f"{where}: {STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+def check(lib, status: int, where: str):
+    if status != KHP_OK:
+        raise KhpError(status, where, (lib.khp_last_error() or b"").decode())

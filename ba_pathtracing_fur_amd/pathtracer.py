@@ -1,0 +1,200 @@
+"""KIRK-shaped host interface over the C-ABI.
+
+Mirrors the plugin surface the HIP core drops in behind:
+  * `PathTracer` ~ KIRK::CPU::PathTracer / CPU_Raytracer (CPU_PathTracer.h:33-166,
+    CPU_Raytracer.h:16-78): init(scene), set_sample_count, set_depth, render()
+    (one sample of every pixel, like one full pass of KIRK's segmented render),
+    render_to_texture(), get_current_sample_count(), reset();
+  * `BVH` ~ KIRK::CPU::CPU_DataStructure (CPU_DataStructure.h:25-28):
+    closest_intersection / is_intersection, batched over ray arrays;
+  * `BsdfFactory` / `ShaderFactory` ~ the name registries (BsdfFactory.cpp:28-55,
+    ShaderFactory.cpp:29-67): unknown names raise ValueError where KIRK throws
+    std::invalid_argument.
+Everything runs on the GPU through libkirk_hip.so; nothing here computes pixels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import native as N
+from .scenes import SceneData
+
+
+class BsdfFactory:
+    @staticmethod
+    def get_bsdf(name: str) -> int:
+        lib = N.load_library()
+        k = lib.khp_bsdf_kind_from_name(name.encode())
+        if k < 0:
+            raise ValueError(f"There is no BSDF registered with the name {name}")
+        return k
+
+    @staticmethod
+    def names() -> list[str]:
+        return list(N.BSDF_NAMES)
+
+
+class ShaderFactory:
+    @staticmethod
+    def get_shader(name: str) -> int:
+        lib = N.load_library()
+        k = lib.khp_shader_kind_from_name(name.encode())
+        if k < 0:
+            raise ValueError(f"There is no Shader registered with the name {name}")
+        return k
+
+
+class HipContext:
+    """One khp_ctx: one GPU, one stream (one process per GPU)."""
+
+    def __init__(self, device: int = 0, stats: bool = False):
+        self.lib = N.load_library()
+        self.ptr = ctypes.c_void_p()
+        N.check(self.lib, self.lib.khp_create(ctypes.byref(self.ptr), device, N.CTX_STATS if stats else 0),
+                "khp_create")
+        self._scene = None
+
+    def close(self):
+        if self.ptr:
+            self.lib.khp_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene(self, scene: SceneData):
+        d = scene.desc()
+        N.check(self.lib, self.lib.khp_set_scene(self.ptr, ctypes.byref(d)), "khp_set_scene")
+        self._scene = scene
+
+    def build_accel(self):
+        N.check(self.lib, self.lib.khp_build_accel(self.ptr), "khp_build_accel")
+
+    def render(self, width, height, spp, depth, seed=0x4B49524B, first_sample=0, tile_size=64, tile_rank=0,
+               tile_nranks=1, out: np.ndarray | None = None, readback=True) -> np.ndarray | None:
+        p = N.RenderParams(width, height, spp, depth, seed, first_sample, tile_size, tile_rank, tile_nranks,
+                           0 if readback else N.RENDER_NO_READBACK)
+        if readback and out is None:
+            out = np.zeros((height, width, 3), np.float32)
+        ptr = out.ctypes.data_as(ctypes.c_void_p) if (readback and out is not None) else None
+        N.check(self.lib, self.lib.khp_render(self.ptr, ctypes.byref(p), ptr), "khp_render")
+        return out
+
+    def read_framebuffer(self, width, height) -> np.ndarray:
+        out = np.zeros((height, width, 3), np.float32)
+        N.check(self.lib, self.lib.khp_read_framebuffer(self.ptr, N.fptr(out)), "khp_read_framebuffer")
+        return out
+
+    def trace_closest(self, orig, direction):
+        o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(direction, np.float32).reshape(-1, 3)
+        n = len(o)
+        t = np.empty(n, np.float32)
+        obj = np.empty(n, np.int32)
+        uv = np.empty((n, 2), np.float32)
+        N.check(self.lib, self.lib.khp_trace_closest(self.ptr, n, N.fptr(o), N.fptr(d), N.fptr(t),
+                                                     obj.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                     N.fptr(uv)), "khp_trace_closest")
+        return t, obj, uv
+
+    def trace_any(self, orig, direction, tmax):
+        o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(direction, np.float32).reshape(-1, 3)
+        tm = np.ascontiguousarray(tmax, np.float32).reshape(-1)
+        hit = np.empty(len(o), np.uint8)
+        N.check(self.lib, self.lib.khp_trace_any(self.ptr, len(o), N.fptr(o), N.fptr(d), N.fptr(tm),
+                                                 hit.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
+                "khp_trace_any")
+        return hit.astype(bool)
+
+    def stats(self) -> dict:
+        s = N.Stats()
+        N.check(self.lib, self.lib.khp_get_stats(self.ptr, ctypes.byref(s)), "khp_get_stats")
+        return s.as_dict()
+
+    # --- multi-GPU --------------------------------------------------------------
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        N.check(self.lib, self.lib.khp_comm_init(self.ptr, nranks, rank, buf), "khp_comm_init")
+
+    def gather_framebuffer(self, width, height, spp, depth, tile_size, nranks, rank, root=0):
+        p = N.RenderParams(width, height, spp, depth, 0, 0, tile_size, rank, nranks, 0)
+        N.check(self.lib, self.lib.khp_gather_framebuffer(self.ptr, ctypes.byref(p), root), "khp_gather_framebuffer")
+
+
+def comm_unique_id() -> bytes:
+    lib = N.load_library()
+    buf = (ctypes.c_uint8 * 128)()
+    N.check(lib, lib.khp_comm_unique_id(buf), "khp_comm_unique_id")
+    return bytes(buf)
+
+
+class BVH:
+    """CPU_DataStructure-shaped batched queries on the GPU BVH."""
+
+    def __init__(self, ctx: HipContext):
+        self.ctx = ctx
+
+    def closest_intersection(self, orig, direction):
+        return self.ctx.trace_closest(orig, direction)
+
+    def is_intersection(self, orig, direction, tmax):
+        return self.ctx.trace_any(orig, direction, tmax)
+
+
+class PathTracer:
+    """KIRK::CPU::PathTracer on the HIP core (progressive, seeded)."""
+
+    def __init__(self, scene: SceneData | None = None, depth: int = 8, device: int = 0, width: int = 256,
+                 height: int = 256, seed: int = 0x4B49524B):
+        self.ctx = HipContext(device)
+        self.m_depth = depth                # CPU_Raytracer.h:73-75 default 8
+        self.m_samples_per_pixel = 1        # PathTracer() default
+        self.c_sample = 0
+        self.width, self.height = width, height
+        self.seed = seed
+        if scene is not None:
+            self.init(scene)
+
+    def init(self, scene: SceneData):
+        self.ctx.set_scene(scene)
+        self.ctx.build_accel()
+        self.reset()
+
+    def set_depth(self, depth: int):
+        self.m_depth = int(depth)
+
+    def set_sample_count(self, samples: int):
+        self.m_samples_per_pixel = int(samples)
+
+    def get_current_sample_count(self) -> int:
+        return self.c_sample
+
+    def reset(self):
+        self.c_sample = 0
+
+    def render(self, n: int = 1):
+        """Add up to `n` samples (KIRK's render() adds one sample per full pass)."""
+        n = min(n, self.m_samples_per_pixel - self.c_sample)
+        if n <= 0:
+            return
+        self.ctx.render(self.width, self.height, n, self.m_depth, self.seed, first_sample=self.c_sample,
+                        readback=False)
+        self.c_sample += n
+
+    def render_to_texture(self) -> np.ndarray:
+        """Render every remaining sample; returns the float RGB framebuffer (H, W, 3), row 0 = bottom."""
+        self.render(self.m_samples_per_pixel - self.c_sample)
+        return self.ctx.read_framebuffer(self.width, self.height)
+
+    @staticmethod
+    def to_rgba8(fb: np.ndarray) -> np.ndarray:
+        """Texture::setPixel's 8-bit clamp (Texture.cpp:222-241), top row first."""
+        rgb = np.clip(fb, 0.0, 1.0) * 255.0
+        rgba = np.concatenate([rgb, np.full(fb.shape[:2] + (1,), 255.0, np.float32)], axis=-1)
+        return rgba.astype(np.uint8)[::-1]

@@ -1,0 +1,258 @@
+/*
+ * kirk_hip.h -- C-ABI of the MI355X-native fur path-tracing core.
+ *
+ * This is the drop-in boundary for the hot path of lucashilbig/BA_Pathtracing_Fur
+ * ("KIRK"): camera ray -> BVH closest hit over hair cone frusta and triangles ->
+ * shader/BSDF -> next-event shadow ray -> accumulate.  Every entry point below
+ * replaces one KIRK C++ interface; the replaced interface is cited (file:line,
+ * relative to the KIRK source tree src/libraries/KIRK/).
+ *
+ * Conventions
+ *  - plain C: no exceptions cross the ABI, no C++ or torch types in signatures;
+ *  - every call returns a khp_status; khp_last_error() returns a thread-local
+ *    message for the last failing call of this thread;
+ *  - all inputs are host pointers and are copied; outputs are caller-owned;
+ *  - one khp_ctx is single-threaded, like KIRK's non-re-entrant
+ *    CPU_Raytracer::render (KIRK/Utils/Threading.h:117);
+ *  - internally: one HIP device + one stream per context, optional RCCL comm.
+ *
+ * Coordinates/units are KIRK's: world space, right-handed, y up; images are
+ * stored row-major with row 0 at the BOTTOM of the frame (Camera::getRayFromPixel
+ * starts at m_bottom_left, KIRK/Common/Camera.cpp:59-66).
+ */
+#ifndef KIRK_HIP_H
+#define KIRK_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KHP_ABI_VERSION 1
+
+typedef struct khp_ctx khp_ctx;
+
+typedef enum {
+    KHP_OK = 0,
+    KHP_EINVAL = 1,       /* bad argument (KIRK: std::invalid_argument)          */
+    KHP_ENOMEM = 2,       /* host or device allocation failed                   */
+    KHP_EDEVICE = 3,      /* HIP / RCCL error, or no device                     */
+    KHP_ENOTREADY = 4,    /* call order violated (e.g. render before build)     */
+    KHP_EUNSUPPORTED = 5  /* feature outside the hot path (textures, env maps)  */
+} khp_status;
+
+/* ---------------------------------------------------------------------------
+ * BSDF and shader kinds.  KIRK registers BSDFs by name in a singleton factory
+ * (Bsdf.h:133-241, BsdfFactory.cpp:28-55) and binds std::function callbacks;
+ * callbacks cannot run on a GPU, so the GPU side is a closed enum keyed by the
+ * same names (khp_bsdf_kind_from_name).
+ * ------------------------------------------------------------------------- */
+typedef enum {
+    KHP_BSDF_LAMBERTIAN_REFLECTION = 0,   /* "LambertianReflectionBSDF"   Bsdf.cpp:186-202 */
+    KHP_BSDF_SPECULAR_REFLECTION = 1,     /* "SpecularReflectionBSDF"     Bsdf.cpp:210-219 */
+    KHP_BSDF_SPECULAR_TRANSMISSION = 2,   /* "SpecularTransmissionBSDF"   Bsdf.cpp:258-290 */
+    KHP_BSDF_GLOSSY = 3,                  /* "GlossyBSDF"                 Bsdf.cpp:227-250 */
+    KHP_BSDF_GLASS = 4,                   /* "GlassBSDF"                  Bsdf.cpp:326-359 */
+    KHP_BSDF_MILK_GLASS = 5,              /* "MilkGlassBSDF"              Bsdf.cpp:367-418 */
+    KHP_BSDF_LAMBERTIAN_TRANSMISSION = 6, /* "LambertianTransmissionBSDF" Bsdf.cpp:298-318 */
+    KHP_BSDF_EMISSION = 7,                /* "EmissionBSDF"               Bsdf.cpp:427-437 */
+    KHP_BSDF_TRANSPARENT = 8,             /* "TransparentBSDF"            Bsdf.cpp:445-456 */
+    KHP_BSDF_MARSCHNER_HAIR = 9,          /* "MarschnerHairBSDF"          Bsdf.cpp:465-776 */
+    KHP_BSDF_DEON_HAIR = 10,              /* "DEonHairBSDF"               Bsdf.cpp:784-1056 */
+    KHP_BSDF_COUNT = 11
+} khp_bsdf_kind;
+
+typedef enum {
+    KHP_SHADER_SIMPLE = 0,          /* "SimpleShader"        SimpleShader.h:31-152        */
+    KHP_SHADER_MARSCHNER_HAIR = 1,  /* "MarschnerHairShader" MarschnerHairShader.h:31-138 */
+    KHP_SHADER_COUNT = 2
+} khp_shader_kind;
+
+/* KIRK::Material (Material.h:53-152), untextured values only (a17 in SURVEY §8). */
+typedef struct {
+    int32_t bsdf;          /* khp_bsdf_kind   */
+    int32_t shader;        /* khp_shader_kind */
+    float diffuse[3];      /* m_diffuse   */
+    float specular[3];     /* m_specular  */
+    float volume[3];       /* m_volume    */
+    float emission[3];     /* m_emission  */
+    float ior;             /* m_ior (KIRK default 1.52, Material.h:83)    */
+    float roughness;       /* m_roughness (KIRK default 1.0)             */
+} khp_material;
+
+typedef enum {
+    KHP_LIGHT_POINT = 0,   /* PointLight Light.cpp:127-199 */
+    KHP_LIGHT_QUAD = 1,    /* QuadLight  Light.cpp:216-296 */
+    KHP_LIGHT_SPOT = 2,    /* SpotLight  Light.cpp:327-440 */
+    KHP_LIGHT_SUN = 3      /* SunLight   Light.cpp:463-511 */
+} khp_light_kind;
+
+/* Constructor arguments of the KIRK light classes (Light.h), identity node
+ * transform.  The library derives the same state KIRK derives in the ctor
+ * and in Light::transform (normalised direction, quad vertices). */
+typedef struct {
+    int32_t kind;          /* khp_light_kind */
+    float color[3];
+    float position[3];
+    float direction[3];    /* ctor argument; normalised by the library      */
+    float size[2];         /* QuadLight m_size                               */
+    float radius;          /* point/spot/sun m_radius                        */
+    float att_const, att_lin, att_quad;
+    float inner_angle, outer_angle;   /* SpotLight, degrees                  */
+} khp_light;
+
+/* KIRK::Environment (Environment.h), COLOR type: background + ambient. */
+typedef struct {
+    float color[3];
+    float ambient[3];
+} khp_environment;
+
+/* The state KIRK::Camera::applyParameters derives (Camera.cpp:6-37). */
+typedef struct {
+    float position[3];
+    float bottom_left[3];
+    float axis_x[3];
+    float axis_y[3];
+    float pixel_size;
+} khp_camera;
+
+/* Flattened scene = what KIRK::CPU::Scene::flattenNode produces
+ * (CPU_Scene.cpp:73-197), before the Triangle/Cylinder constructors run.
+ * Object order (it shapes the BVH): triangles [0,n_tris) then cones. */
+typedef struct {
+    uint32_t n_tris;
+    const float* tri_v;           /* [n_tris][3][3] vertices a,b,c (Triangle ctor args) */
+    const float* tri_n;           /* [n_tris][3][3] vertex normals na,nb,nc             */
+    const uint32_t* tri_mat;      /* [n_tris] material index                            */
+    uint32_t n_cones;
+    const float* cone_base_r0;    /* [n_cones][4] basePoint.xyz, baseRadius  (Cylinder ctor) */
+    const float* cone_apex_r1;    /* [n_cones][4] apexPoint.xyz, apexRadius                  */
+    const uint32_t* cone_mat;     /* [n_cones] material index                                */
+    uint32_t n_materials;
+    const khp_material* materials;
+    uint32_t n_lights;
+    const khp_light* lights;
+    khp_environment env;
+    khp_camera camera;
+} khp_scene;
+
+#define KHP_RENDER_OUT_DEVICE   (1u << 0)  /* out_rgb is a device pointer        */
+#define KHP_RENDER_NO_READBACK  (1u << 1)  /* keep framebuffer in HBM only       */
+
+/* One khp_render call = samples [first_sample, first_sample+spp) of
+ * PathTracer::render (CPU_PathTracer.cpp:17-52) for every pixel this rank
+ * owns; the framebuffer holds KIRK's running mean (drawTexture, :61-90). */
+typedef struct {
+    uint32_t width, height;
+    uint32_t spp;            /* samples in this call                               */
+    uint32_t depth;          /* max bounces, PathTracer m_depth (Demo uses 5)      */
+    uint32_t seed;           /* frame seed of the counter RNG                      */
+    uint32_t first_sample;   /* progressive resume: 0 starts a new frame           */
+    uint32_t tile_size;      /* square tiles; 0 -> 64                              */
+    uint32_t tile_rank;      /* this rank renders tiles with id % tile_nranks == tile_rank */
+    uint32_t tile_nranks;    /* 0 or 1 -> all tiles                                */
+    uint32_t flags;          /* KHP_RENDER_*                                       */
+} khp_render_params;
+
+typedef struct {
+    uint64_t n_objects, n_nodes, n_leaves;
+    uint32_t bvh_depth, max_leaf_size;
+    uint64_t device_bytes;           /* scene + BVH + queues resident in HBM  */
+    double build_ms;                 /* flatten + BVH build (host)            */
+    double upload_ms;
+    double render_ms;                /* last khp_render, device time          */
+    double extend_ms, shade_ms, shadow_ms, other_ms;  /* per-kernel device time, last render */
+    uint64_t extend_rays, shadow_rays, extend_launches;
+    uint64_t node_visits, prim_tests, shadow_node_visits, shadow_prim_tests; /* KHP_CTX_STATS only */
+} khp_stats;
+
+#define KHP_CTX_STATS  (1u << 0)   /* instrumented kernels: count node/prim visits */
+
+/* ---- context --------------------------------------------------------------- */
+/* device: HIP device ordinal (one process per GPU). */
+khp_status khp_create(khp_ctx** out, int device, uint32_t flags);
+void khp_destroy(khp_ctx* ctx);
+const char* khp_last_error(void);
+int khp_abi_version(void);
+
+/* Replaces CPU::Scene::setSceneGraph (CPU_Scene.cpp:25-43) + the Triangle and
+ * Cylinder constructors (Triangle.cpp:3-129, Cylinder.cpp:5-67). Copies. */
+khp_status khp_set_scene(khp_ctx* ctx, const khp_scene* scene);
+
+/* Replaces BVH::addBaseDataStructure (CPU_BVH.cpp:16-44): binned SAH, 16 bins,
+ * leaf threshold 1 (CPU_BVH.h:64); uploads scene + BVH to HBM. */
+khp_status khp_build_accel(khp_ctx* ctx);
+
+/* Replaces PathTracer::render (CPU_PathTracer.cpp:17-52).  out_rgb: W*H*3
+ * floats (host unless KHP_RENDER_OUT_DEVICE, ignored with NO_READBACK).
+ * Pixels of tiles not owned by this rank are left untouched. */
+khp_status khp_render(khp_ctx* ctx, const khp_render_params* p, float* out_rgb);
+
+/* Copy the device framebuffer (running mean, W*H*3) to host. */
+khp_status khp_read_framebuffer(khp_ctx* ctx, float* out_rgb);
+
+/* Batch forms of CPU_DataStructure::closestIntersection / isIntersection
+ * (CPU_DataStructure.h:25-28, BVH impl CPU_BVH.cpp:51-93), on the GPU.
+ * orig/dir: [n][3] host arrays; dir is normalised like KIRK::Ray (Ray.cpp:11-15).
+ * closest: t_out = lambda (FLT_MAX if none), obj_out = object id or -1,
+ *          uv_out (optional, [n][2]) = barycentric u,v (0 for cones).
+ * any:     hit_out[i] = 1 if an object is hit with t in [0, tmax[i]]. */
+khp_status khp_trace_closest(khp_ctx* ctx, uint32_t n, const float* orig, const float* dir,
+                             float* t_out, int32_t* obj_out, float* uv_out);
+khp_status khp_trace_any(khp_ctx* ctx, uint32_t n, const float* orig, const float* dir,
+                         const float* tmax, uint8_t* hit_out);
+
+khp_status khp_get_stats(khp_ctx* ctx, khp_stats* out);
+
+/* ---- multi-GPU: tile sharding + RCCL framebuffer gather -------------------- */
+/* RCCL unique id (128 bytes), created on rank 0 and broadcast by the caller. */
+khp_status khp_comm_unique_id(uint8_t out_id[128]);
+khp_status khp_comm_init(khp_ctx* ctx, int nranks, int rank, const uint8_t id[128]);
+/* Gather every rank's owned tiles (per p->tile_*) into rank root's device
+ * framebuffer over RCCL; root may then khp_read_framebuffer. Collective. */
+khp_status khp_gather_framebuffer(khp_ctx* ctx, const khp_render_params* p, int root);
+
+/* ---- registries / host helpers --------------------------------------------- */
+/* BsdfFactory::getBsdf / ShaderFactory::getShader by KIRK name; -1 if unknown
+ * (KIRK throws std::invalid_argument, BsdfFactory.cpp:39-45). */
+int khp_bsdf_kind_from_name(const char* name);
+const char* khp_bsdf_name(int kind);
+int khp_shader_kind_from_name(const char* name);
+
+/* Camera::applyParameters (Camera.cpp:6-37) for a camera at `position`
+ * looking along `look_at` (a direction, KIRK m_local_look_at) with `up`;
+ * sensor size and focal length in metres (KIRK defaults 0.036x0.024, 0.0415). */
+khp_status khp_camera_setup(const float position[3], const float look_at[3], const float up[3],
+                            float sensor_w, float sensor_h, float focal_length,
+                            uint32_t width, uint32_t height, khp_camera* out);
+
+/* Fur fibers -> cone frusta exactly as CPU_Scene::flattenNode does with
+ * m_fiberAsCylinder (CPU_Scene.cpp:121-144): base pulled back by 0.8 % of the
+ * segment, base radius shrunk 5 % (segment index <= 3) or 10 %.
+ * positions [n_fibers][verts][3], radii [n_fibers][verts];
+ * out arrays [n_fibers*(verts-1)][4]. */
+khp_status khp_fibers_to_cones(uint32_t n_fibers, uint32_t verts_per_fiber,
+                               const float* positions, const float* radii,
+                               float* out_base_r0, float* out_apex_r1);
+
+/* Seeded synthetic inputs (stand-ins for SceneGraph + Mesh::addFurToFaces,
+ * Mesh.cpp:82-148).  Bit-reproducible on any host.
+ * hairball: roots uniform on a sphere, strands of `verts` vertices following
+ * the addFurToFaces recurrence in the root's tangent frame.
+ * positions [n][verts][3], radii [n][verts]. */
+khp_status khp_gen_hairball(uint32_t n_strands, uint32_t verts, const float center[3],
+                            float ball_radius, float root_radius, uint32_t seed,
+                            float* positions, float* radii);
+/* icosphere with `subdiv` subdivisions: 20*4^subdiv triangles (tri_v/tri_n as khp_scene). */
+khp_status khp_gen_icosphere(uint32_t subdiv, const float center[3], float radius,
+                             float* tri_v, float* tri_n);
+/* torus grid nu x nv quads -> 2*nu*nv triangles. */
+khp_status khp_gen_torus(uint32_t nu, uint32_t nv, const float center[3], float major_r,
+                         float minor_r, float* tri_v, float* tri_n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KIRK_HIP_H */
