@@ -146,166 +146,7 @@ __device__ __forceinline__ bool cone_any(float4 c0, float4 c1, float4 c2, float4
     return d >= min_d && d <= max_d;
 }
 
-struct Hit {
-    float t;
-    int32_t slot;
-    float u, v;
-};
-
-struct TravStats {
-    uint32_t nodes, prims;
-};
-
-__device__ __forceinline__ v3 inv_dir(v3 d, bool sgn[3]) {
-    sgn[0] = d.x < 0.0f;
-    sgn[1] = d.y < 0.0f;
-    sgn[2] = d.z < 0.0f;
-    return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-}
-
-// BVH::closestIntersection + BVHNode::traverse(Intersection*) + Container::
-// closestIntersectionWithCandidates (CPU_BVH.cpp:51-69, 148-199; Container.cpp:13-25).
-// The recursion becomes an explicit stack of (ref, cnt, tmin, tmax); pushing
-// far-then-near and testing the prune condition at pop time visits nodes in
-// exactly KIRK's order, which matters because a leaf may accept a farther
-// root (Appendix A.8/A.9 of SURVEY.md).
-template <bool STATS>
-__device__ __forceinline__ void trace_closest(const DevScene& S, const Ray& r, Hit& h, TravStats& st) {
-    h.t = FLT_MAX_;
-    h.slot = -1;
-    h.u = 0.0f;
-    h.v = 0.0f;
-    bool sgn[3];
-    v3 inv = inv_dir(r.d, sgn);
-    float t0, t1;
-    if (!slab(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4], S.root_box[5], r, inv, sgn,
-              t0, t1))
-        return;
-    int4 stack[STACK_MAX];
-    int sp = 0;
-    stack[sp++] = make_int4(S.root_ref, S.root_cnt, (int)bits_from_f(t0), (int)bits_from_f(t1));
-    while (sp > 0) {
-        int4 e = stack[--sp];
-        float tmin = f_from_bits((uint32_t)e.z), tmax = f_from_bits((uint32_t)e.w);
-        if (tmax < 0.0f || tmin > h.t) continue;
-        if (STATS) st.nodes++;
-        if (e.y > 0) {
-            float tl = FLT_MAX_, lu = 0.0f, lv = 0.0f, tMax = tmax;
-            int32_t sl = -1;
-            for (int k = 0; k < e.y; ++k) {
-                int32_t slot = e.x + k;
-                const float4* p = S.prims + 4 * (size_t)slot;
-                float4 p0 = p[0], p1 = p[1], p2 = p[2];
-                if (STATS) st.prims++;
-                float t, u, v;
-                bool ok;
-                if (is_tri(p0)) {
-                    ok = tri_test(p0, p1, p2, r, 0.0f, tMax, t, u, v);
-                } else {
-                    float4 p3 = p[3];
-                    ok = cone_closest(p0, p1, p2, p3, r, 0.0f, tMax, t);
-                    u = 0.0f;
-                    v = 0.0f;
-                }
-                if (ok) {
-                    tl = t;
-                    sl = slot;
-                    lu = u;
-                    lv = v;
-                    tMax = t;
-                }
-            }
-            if (sl >= 0 && tl < h.t) {
-                h.t = tl;
-                h.slot = sl;
-                h.u = lu;
-                h.v = lv;
-            }
-        } else {
-            const float4* np = reinterpret_cast<const float4*>(S.nodes + e.x);
-            float4 a = np[0], b = np[1], c = np[2];
-            int4 rf = reinterpret_cast<const int4*>(np)[3];
-            float l0, l1, r0, r1;
-            bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, r, inv, sgn, l0, l1);
-            bool rh = slab(b.z, b.w, c.x, c.y, c.z, c.w, r, inv, sgn, r0, r1);
-            int4 L = make_int4(rf.x, rf.z, (int)bits_from_f(l0), (int)bits_from_f(l1));
-            int4 R = make_int4(rf.y, rf.w, (int)bits_from_f(r0), (int)bits_from_f(r1));
-            if (lh && rh) {
-                if (l0 < r0) {
-                    stack[sp++] = R;
-                    stack[sp++] = L;
-                } else {
-                    stack[sp++] = L;
-                    stack[sp++] = R;
-                }
-            } else if (lh) {
-                stack[sp++] = L;
-            } else if (rh) {
-                stack[sp++] = R;
-            }
-        }
-    }
-}
-
-// BVH::isIntersection + BVHNode::traverse(Ray*) + isIntersectionWithCandidates
-// (CPU_BVH.cpp:77-93, 211-265; Container.cpp:27-34).  Any-hit results do not
-// depend on visiting order; KIRK's near-first order is kept anyway.
-template <bool STATS>
-__device__ __forceinline__ bool trace_any(const DevScene& S, const Ray& r, float tMaxRay, TravStats& st) {
-    bool sgn[3];
-    v3 inv = inv_dir(r.d, sgn);
-    float t0, t1;
-    if (!slab(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4], S.root_box[5], r, inv, sgn,
-              t0, t1))
-        return false;
-    int4 stack[STACK_MAX];
-    int sp = 0;
-    stack[sp++] = make_int4(S.root_ref, S.root_cnt, (int)bits_from_f(t0), (int)bits_from_f(t1));
-    while (sp > 0) {
-        int4 e = stack[--sp];
-        float tmin = f_from_bits((uint32_t)e.z), tmax = f_from_bits((uint32_t)e.w);
-        if (tmax < 0.0f || tmin > tMaxRay) continue;
-        if (STATS) st.nodes++;
-        if (e.y > 0) {
-            for (int k = 0; k < e.y; ++k) {
-                const float4* p = S.prims + 4 * (size_t)(e.x + k);
-                float4 p0 = p[0], p1 = p[1], p2 = p[2];
-                if (STATS) st.prims++;
-                bool ok;
-                if (is_tri(p0)) {
-                    float t, u, v;
-                    ok = tri_test(p0, p1, p2, r, 0.0f, tMaxRay, t, u, v);
-                } else {
-                    ok = cone_any(p0, p1, p2, p[3], r, tMaxRay);
-                }
-                if (ok) return true;
-            }
-        } else {
-            const float4* np = reinterpret_cast<const float4*>(S.nodes + e.x);
-            float4 a = np[0], b = np[1], c = np[2];
-            int4 rf = reinterpret_cast<const int4*>(np)[3];
-            float l0, l1, r0, r1;
-            bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, r, inv, sgn, l0, l1);
-            bool rh = slab(b.z, b.w, c.x, c.y, c.z, c.w, r, inv, sgn, r0, r1);
-            int4 L = make_int4(rf.x, rf.z, (int)bits_from_f(l0), (int)bits_from_f(l1));
-            int4 R = make_int4(rf.y, rf.w, (int)bits_from_f(r0), (int)bits_from_f(r1));
-            if (lh && rh) {
-                if (l0 < r0) {
-                    stack[sp++] = R;
-                    stack[sp++] = L;
-                } else {
-                    stack[sp++] = L;
-                    stack[sp++] = R;
-                }
-            } else if (lh) {
-                stack[sp++] = L;
-            } else if (rh) {
-                stack[sp++] = R;
-            }
-        }
-    }
-    return false;
-}
+#include "traverse.h"
 
 // ---------------------------------------------------------------------------
 // lights (Common/Light.h, Common/Light.cpp)

@@ -115,27 +115,84 @@ __global__ void k_prep(Counters* c, int cur) {
     c->ext_rays += c->nq[cur];
 }
 
+// ---- persistent lane-refill traversal -------------------------------------------------------
+// Every lane owns one ray at a time.  When at least REFILL lanes of a wave are
+// idle, the wave claims that many new rays with a single atomic and the idle
+// lanes start them, so a wave never waits for its slowest ray to admit new
+// work (Aila & Laine's persistent "while-while" with speculative refill).
+constexpr int RING = 8;         // LDS ring entries per lane (3 x 4 B each)
+constexpr int REFILL = 16;      // refill when >= REFILL lanes are idle
+constexpr size_t LDS_BYTES = 3 * RING * 256 * sizeof(uint32_t);
+
+struct SpillArea {
+    int4* base;
+    uint32_t stride;   // lanes in the grid
+};
+
+__device__ __forceinline__ uint32_t claim(unsigned long long idle, uint32_t* fetch, uint32_t& slot_out) {
+    uint32_t lane = lane_id();
+    uint32_t k = (uint32_t)__popcll(idle);
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(fetch, k);
+    base = __shfl(base, 0);
+    slot_out = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+    return base;
+}
+
 // ---- extend: closest hit for every queued ray ------------------------------------------
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_extend(DevScene S, Wave Wv, int cur) {
+__global__ __launch_bounds__(256) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
+    extern __shared__ uint32_t lds[];
     const uint32_t n = Wv.cnt->nq[cur];
+    LdsStack<RING> stk;
+    stk.init(lds, threadIdx.x, spill.base, blockIdx.x * blockDim.x + threadIdx.x, spill.stride);
     TravStats st{0, 0};
+    TravRay tr;
+    Hit h;
+    bool has = false, exhausted = false;
+    uint32_t idx = 0;
     for (;;) {
-        uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(&Wv.cnt->fetch_ext, 64u);
-        base = __shfl(base, 0);
-        if (base >= n) break;
-        uint32_t i = base + lane_id();
-        if (i < n) {
-            Ray r;
-            r.o = mk(Wv.qo[cur][0][i], Wv.qo[cur][1][i], Wv.qo[cur][2][i]);
-            r.d = mk(Wv.qd[cur][0][i], Wv.qd[cur][1][i], Wv.qd[cur][2][i]);
-            Hit h;
-            trace_closest<STATS>(S, r, h, st);
-            Wv.ht[i] = h.t;
-            Wv.hslot[i] = h.slot;
-            Wv.hu[i] = h.u;
-            Wv.hv[i] = h.v;
+        unsigned long long idle = __ballot(!has);
+        if (!exhausted && __popcll(idle) >= REFILL) {
+            uint32_t my;
+            uint32_t base = claim(idle, &Wv.cnt->fetch_ext, my);
+            if (base + (uint32_t)__popcll(idle) >= n) exhausted = true;
+            if (!has && my < n) {
+                idx = my;
+                Ray r;
+                r.o = mk(Wv.qo[cur][0][idx], Wv.qo[cur][1][idx], Wv.qo[cur][2][idx]);
+                r.d = mk(Wv.qd[cur][0][idx], Wv.qd[cur][1][idx], Wv.qd[cur][2][idx]);
+                trav_setup(tr, r);
+                h.t = FLT_MAX_;
+                h.slot = -1;
+                h.u = h.v = 0.0f;
+                has = trav_begin(S, tr, stk);
+                if (!has) {  // missed the root box
+                    Wv.ht[idx] = h.t;
+                    Wv.hslot[idx] = -1;
+                    Wv.hu[idx] = 0.0f;
+                    Wv.hv[idx] = 0.0f;
+                }
+            }
+        }
+        unsigned long long act = __ballot(has);
+        if (act == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        for (;;) {
+            if (has) {
+                closest_step<STATS>(S, tr, h, stk, st);
+                if (stk.empty()) {
+                    Wv.ht[idx] = h.t;
+                    Wv.hslot[idx] = h.slot;
+                    Wv.hu[idx] = h.u;
+                    Wv.hv[idx] = h.v;
+                    has = false;
+                }
+            }
+            act = __ballot(has);
+            if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
     }
     if (STATS) {
@@ -205,7 +262,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                 ShadeCtx s;
                 s.m = &S.mats[ax.mat];
                 v3 nrm;
-                if (ax.is_cone) {  // Cylinder::calcNormal (Cylinder.cpp:230-237)
+                if (ax.flags & 1u) {  // Cylinder::calcNormal (Cylinder.cpp:230-237)
                     float4 c0 = pr[0], c1 = pr[1], c2 = pr[2], c3 = pr[3];
                     v3 base3 = mk(c0.x, c0.y, c0.z);
                     s.U = mk(c1.x, c1.y, c1.z);
@@ -328,44 +385,79 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
 }
 
 // ---- shadow: BVH::isIntersection + light occlusion loop, then colour += acc ------------
+// finish one shadow record: light occlusion loop + deferred colour add
+__device__ __forceinline__ void shadow_finish(const DevScene& S, const Wave& Wv, uint32_t i, const TravRay& tr,
+                                              float tmax, bool occ) {
+    const float4* rec = Wv.sh + 6 * (size_t)i;
+    float4 b = rec[1], c = rec[2], d = rec[3], e = rec[4];
+    uint32_t pid = bits_from_f(b.w);
+    const Ray& r = tr.r;
+    if (!occ) {
+        for (int li = 0; li < S.n_lights; ++li) {
+            float t;
+            if (light_isect(S.lights[li], r, t) && (t < tmax)) {
+                occ = true;
+                break;
+            }
+        }
+    }
+    v3 lc = mk(c.x, c.y, c.z) * (occ ? 0.0f : 1.0f);
+    v3 dl = mk(0, 0, 0) + lc;
+    v3 acc = (mk(0, 0, 0) + dl * mk(d.x, d.y, d.z)) + mk(e.x, e.y, e.z);
+    if (c.w != 0.0f) {
+        float4 f = rec[5];
+        acc = acc + mk(f.x, f.y, f.z);
+    }
+    Wv.C[0][pid] = Wv.C[0][pid] + acc.x;
+    Wv.C[1][pid] = Wv.C[1][pid] + acc.y;
+    Wv.C[2][pid] = Wv.C[2][pid] + acc.z;
+}
+
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_shadow(DevScene S, Wave Wv) {
+__global__ __launch_bounds__(256) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
+    extern __shared__ uint32_t lds[];
     const uint32_t n = Wv.cnt->nsh;
+    LdsStack<RING> stk;
+    stk.init(lds, threadIdx.x, spill.base, blockIdx.x * blockDim.x + threadIdx.x, spill.stride);
     TravStats st{0, 0};
+    TravRay tr;
+    float tmax = 0.0f;
+    bool has = false, exhausted = false;
+    uint32_t idx = 0;
     for (;;) {
-        uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(&Wv.cnt->fetch_sh, 64u);
-        base = __shfl(base, 0);
-        if (base >= n) break;
-        uint32_t i = base + lane_id();
-        if (i < n) {
-            const float4* rec = Wv.sh + 6 * (size_t)i;
-            float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3], e = rec[4];
-            Ray r;
-            r.o = mk(a.x, a.y, a.z);
-            r.d = mk(b.x, b.y, b.z);
-            float tmax = a.w;
-            uint32_t pid = bits_from_f(b.w);
-            bool occ = trace_any<STATS>(S, r, tmax, st);
-            if (!occ) {
-                for (int li = 0; li < S.n_lights; ++li) {
-                    float t;
-                    if (light_isect(S.lights[li], r, t) && (t < tmax)) {
-                        occ = true;
-                        break;
-                    }
+        unsigned long long idle = __ballot(!has);
+        if (!exhausted && __popcll(idle) >= REFILL) {
+            uint32_t my;
+            uint32_t base = claim(idle, &Wv.cnt->fetch_sh, my);
+            if (base + (uint32_t)__popcll(idle) >= n) exhausted = true;
+            if (!has && my < n) {
+                idx = my;
+                const float4* rec = Wv.sh + 6 * (size_t)idx;
+                float4 a = rec[0], b = rec[1];
+                Ray r;
+                r.o = mk(a.x, a.y, a.z);
+                r.d = mk(b.x, b.y, b.z);
+                tmax = a.w;
+                trav_setup(tr, r);
+                has = trav_begin(S, tr, stk);
+                if (!has) shadow_finish(S, Wv, idx, tr, tmax, false);
+            }
+        }
+        unsigned long long act = __ballot(has);
+        if (act == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        for (;;) {
+            if (has) {
+                bool found = any_step<STATS>(S, tr, tmax, stk, st);
+                if (found || stk.empty()) {
+                    shadow_finish(S, Wv, idx, tr, tmax, found);
+                    has = false;
                 }
             }
-            v3 lc = mk(c.x, c.y, c.z) * (occ ? 0.0f : 1.0f);
-            v3 dl = mk(0, 0, 0) + lc;
-            v3 acc = (mk(0, 0, 0) + dl * mk(d.x, d.y, d.z)) + mk(e.x, e.y, e.z);
-            if (c.w != 0.0f) {
-                float4 f = rec[5];
-                acc = acc + mk(f.x, f.y, f.z);
-            }
-            Wv.C[0][pid] = Wv.C[0][pid] + acc.x;
-            Wv.C[1][pid] = Wv.C[1][pid] + acc.y;
-            Wv.C[2][pid] = Wv.C[2][pid] + acc.z;
+            act = __ballot(has);
+            if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
     }
     if (STATS) {
@@ -415,7 +507,8 @@ __global__ __launch_bounds__(256) void k_trace_closest(DevScene S, uint32_t n, c
     if (i < n) {
         Ray r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
         Hit h;
-        trace_closest<STATS>(S, r, h, st);
+        PrivStack stk;
+        trace_closest<STATS>(S, r, h, stk, st);
         t_out[i] = h.t;
         obj_out[i] = h.slot >= 0 ? (int32_t)S.aux[h.slot].obj : -1;
         if (uv_out) {
@@ -438,7 +531,8 @@ __global__ __launch_bounds__(256) void k_trace_any(DevScene S, uint32_t n, const
     if (i >= n) return;
     Ray r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
     TravStats st{0, 0};
-    hit_out[i] = trace_any<false>(S, r, tmax[i], st) ? 1 : 0;
+    PrivStack stk;
+    hit_out[i] = trace_any<false>(S, r, tmax[i], stk, st) ? 1 : 0;
 }
 
 // ---- multi-GPU: pack owned pixels / scatter a rank's pixels ------------------------------
@@ -510,7 +604,7 @@ struct khp_ctx {
     DevScene S{};
     // wavefront
     size_t cap = 0;
-    DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb, cnt;
+    DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb, cnt, spill;
     // framebuffer + pixel list
     DevMem fb, pix, stage, stage2, stage_pix;
     uint32_t fbW = 0, fbH = 0;
@@ -600,6 +694,8 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     c->st.build_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (c->hs.depth + 1 > (uint32_t)STACK_MAX)
         return fail(KHP_EUNSUPPORTED, "BVH deeper than the traversal stack (" + std::to_string(c->hs.depth) + ")");
+    if (c->hs.n_obj >= MAX_SLOTS)
+        return fail(KHP_EUNSUPPORTED, "more than 2^24 objects do not fit the packed leaf reference");
     HostScene& hs = c->hs;
     HIPCHK(upload(c->prims, hs.slot_rec.data(), hs.slot_rec.size(), c->stream));
     HIPCHK(upload(c->aux, hs.slot_aux.data(), hs.slot_aux.size(), c->stream));
@@ -632,12 +728,12 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     // persistent grid sizes
     int nb = 0;
     if (c->flags & KHP_CTX_STATS)
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<true>, 256, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<true>, 256, LDS_BYTES));
     else
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, 256, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, 256, LDS_BYTES));
     c->grid_ext = std::max(1, nb) * c->n_cu;
     nb = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, 256, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, 256, LDS_BYTES));
     c->grid_sh = std::max(1, nb) * c->n_cu;
     nb = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade, 256, 0));
@@ -662,6 +758,9 @@ static khp_status ensure_wave(khp_ctx* c, size_t cap) {
     HIPCHK(c->keyb.ensure(cap * 4));
     HIPCHK(c->shb.ensure(cap * 6 * sizeof(float4)));
     HIPCHK(c->cnt.ensure(sizeof(Counters)));
+    // traversal-stack spill columns: one per resident lane, STACK_MAX entries deep
+    size_t lanes = (size_t)std::max(c->grid_ext, c->grid_sh) * 256;
+    HIPCHK(c->spill.ensure(lanes * STACK_MAX * sizeof(int4)));
     c->cap = cap;
     return KHP_OK;
 }
@@ -736,7 +835,7 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     s = ensure_wave(c, (size_t)P_chunk * S_chunk);
     if (s != KHP_OK) return s;
     HIPCHK(hipMemsetAsync(c->cnt.p, 0, sizeof(Counters), c->stream));
-    const bool stats = (c->flags & KHP_CTX_STATS) != 0;
+    const bool stats = (c->flags & KHP_CTX_STATS) != 0 || (p->flags & KHP_RENDER_STATS) != 0;
     c->launches.clear();
     c->ev_next = 0;
     Wave Wv{};
@@ -764,6 +863,8 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     Wv.H = p->height;
     Wv.seed = p->seed;
     Wv.depth = p->depth;
+    SpillArea sp_ext{c->spill.as<int4>(), (uint32_t)c->grid_ext * 256u};
+    SpillArea sp_sh{c->spill.as<int4>(), (uint32_t)c->grid_sh * 256u};
     hipEvent_t ev_start = next_event(c);
     (void)hipEventRecord(ev_start, c->stream);
     for (uint32_t p0 = 0; p0 < P_all; p0 += P_chunk) {
@@ -783,18 +884,18 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
                 hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, c->stream, Wv.cnt, cur);
                 timed(c, 0, true);
                 if (stats)
-                    hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(256), 0, c->stream, c->S, Wv, cur);
+                    hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(256), LDS_BYTES, c->stream, c->S, Wv, cur, sp_ext);
                 else
-                    hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(256), 0, c->stream, c->S, Wv, cur);
+                    hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(256), LDS_BYTES, c->stream, c->S, Wv, cur, sp_ext);
                 timed(c, 0, false);
                 timed(c, 1, true);
                 hipLaunchKernelGGL(k_shade, dim3(c->grid_shade), dim3(256), 0, c->stream, c->S, Wv, cur, b);
                 timed(c, 1, false);
                 timed(c, 2, true);
                 if (stats)
-                    hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), 0, c->stream, c->S, Wv);
+                    hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp_sh);
                 else
-                    hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), 0, c->stream, c->S, Wv);
+                    hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp_sh);
                 timed(c, 2, false);
             }
             hipLaunchKernelGGL(k_tail, dim3(1), dim3(1), 0, c->stream, Wv.cnt);

@@ -97,7 +97,7 @@ static void tri_ctor(HostScene& hs, uint32_t id, v3 a, v3 b, v3 c, v3 na, v3 nb,
     float* tn = &hs.tri_nrm[9 * (size_t)id];
     float nn[9] = {nA.x, nA.y, nA.z, nB.x, nB.y, nB.z, nC.x, nC.y, nC.z};
     memcpy(tn, nn, sizeof(nn));
-    hs.aux[id] = Aux{0.0f, mat, id, 0u};
+    hs.aux[id] = Aux{0.0f, mat, id, 0u};  // flags: triangle
 }
 
 // Cylinder::Cylinder + computeBounds (Common/Cylinder.cpp:5-67, 306-336).
@@ -140,7 +140,7 @@ static void cone_ctor(HostScene& hs, uint32_t id, uint32_t ci, v3 base, v3 apex,
     float* ce = &hs.centroid[3 * (size_t)id];
     ce[0] = cen.x; ce[1] = cen.y; ce[2] = cen.z;
     hs.cone_height[ci] = height;
-    hs.aux[id] = Aux{base_d, mat, id, 1u};
+    hs.aux[id] = Aux{base_d, mat, id, 1u};  // flags: cone
 }
 
 std::string flatten_scene(const khp_scene* s, HostScene& hs) {
@@ -397,8 +397,14 @@ void make_device_layout(HostScene& hs) {
     hs.dnodes.assign((size_t)ni, DevNode{});
     auto child_ref = [&](int32_t c, int32_t& ref, int32_t& cnt) {
         const BuildNode& n = hs.nodes[c];
-        if (n.count > 0) { ref = n.first; cnt = n.count; }
-        else { ref = inner[c]; cnt = 0; }
+        if (n.count > 0) {
+            uint32_t ce = (uint32_t)n.count < LEAF_CNT_ESC ? (uint32_t)n.count : LEAF_CNT_ESC;
+            ref = (int32_t)(LEAF_BIT | (ce << 24) | (uint32_t)n.first);
+            cnt = n.count;
+        } else {
+            ref = inner[c];
+            cnt = 0;
+        }
     };
     for (size_t i = 0; i < hs.nodes.size(); ++i) {
         const BuildNode& n = hs.nodes[i];
@@ -426,6 +432,8 @@ void make_device_layout(HostScene& hs) {
         memcpy(&hs.slot_rec[16 * (size_t)s], &hs.rec[16 * (size_t)o], 16 * sizeof(float));
         hs.slot_aux[s] = hs.aux[o];
     }
+    for (const BuildNode& n : hs.nodes)
+        if (n.count > 0) hs.slot_aux[n.first].flags |= (uint32_t)n.count << 8;
 }
 
 }  // namespace khp

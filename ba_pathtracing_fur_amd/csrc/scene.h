@@ -17,15 +17,21 @@ namespace khp {
 // cone   : (base.xyz, r0) (u.xyz, slope) (v.xyz, min_d) (w.xyz, max_d)
 // triangle: (A.xyz, TRI_TAG) (ab.xyz, 0) (ac.xyz, 0) (0,0,0,0)
 constexpr uint32_t TRI_TAG = 0x7fc0deadu;
-// aux per slot: (base_d bits, material, object id, 1 if cone)
+// aux per slot: (base_d, material, object id, flags); flags bit 0 = cone,
+// bits 8..31 = candidate count of the leaf that starts at this slot (0 otherwise).
 struct Aux {
     float base_d;
     uint32_t mat;
     uint32_t obj;
-    uint32_t is_cone;
+    uint32_t flags;
 };
+// packed child/stack reference: interior node index, or LEAF_BIT | count << 24 | first slot
+// (count 127 = escape: read the count from Aux::flags of the first slot).
+constexpr uint32_t LEAF_BIT = 0x80000000u;
+constexpr uint32_t LEAF_CNT_ESC = 127u;
+constexpr uint32_t MAX_SLOTS = 1u << 24;
 // interior node: (L.min.xyz, L.max.x) (L.max.yz, R.min.xy) (R.min.z, R.max.xyz) (Lref, Rref, Lcnt, Rcnt)
-// child with cnt > 0 is a leaf covering slots [ref, ref+cnt); cnt == 0 -> interior node `ref`.
+// ref = packed reference (LEAF_BIT ...); cnt = leaf candidate count or 0 for an interior child.
 struct DevNode {
     float a[4], b[4], c[4];
     int32_t ref[2], cnt[2];
@@ -68,7 +74,7 @@ struct HostScene {
     std::vector<DevNode> dnodes;   // interior nodes
     std::vector<float> slot_rec;   // n_obj * 16, slot order
     std::vector<Aux> slot_aux;     // slot order
-    int32_t root_ref = 0, root_cnt = 0;
+    int32_t root_ref = 0, root_cnt = 0;   // root_ref packed
     float root_box[6] = {0, 0, 0, 0, 0, 0};
 };
 

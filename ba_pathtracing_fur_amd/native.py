@@ -28,6 +28,7 @@ LIGHT_POINT, LIGHT_QUAD, LIGHT_SPOT, LIGHT_SUN = 0, 1, 2, 3
 
 RENDER_OUT_DEVICE = 1 << 0
 RENDER_NO_READBACK = 1 << 1
+RENDER_STATS = 1 << 2
 CTX_STATS = 1 << 0
 
 F3 = c_float * 3

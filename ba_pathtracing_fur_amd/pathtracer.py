@@ -76,9 +76,9 @@ class HipContext:
         N.check(self.lib, self.lib.khp_build_accel(self.ptr), "khp_build_accel")
 
     def render(self, width, height, spp, depth, seed=0x4B49524B, first_sample=0, tile_size=64, tile_rank=0,
-               tile_nranks=1, out: np.ndarray | None = None, readback=True) -> np.ndarray | None:
-        p = N.RenderParams(width, height, spp, depth, seed, first_sample, tile_size, tile_rank, tile_nranks,
-                           0 if readback else N.RENDER_NO_READBACK)
+               tile_nranks=1, out: np.ndarray | None = None, readback=True, stats=False) -> np.ndarray | None:
+        flags = (0 if readback else N.RENDER_NO_READBACK) | (N.RENDER_STATS if stats else 0)
+        p = N.RenderParams(width, height, spp, depth, seed, first_sample, tile_size, tile_rank, tile_nranks, flags)
         if readback and out is None:
             out = np.zeros((height, width, 3), np.float32)
         ptr = out.ctypes.data_as(ctypes.c_void_p) if (readback and out is not None) else None

@@ -1,0 +1,240 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Msamples/s at 1080p 8 spp on the 1M-strand hairball.
+
+BASELINE.json metric: "Msamples/s at 1080p 8spp, 1M-strand hairball; achieved
+HBM GB/s vs peak".  Workload = config 3's scene (1M strands -> 9M cone frusta
+on a 2-triangle plane, 2x2 quad light, sky environment) rendered at
+1920x1080, 8 spp, depth 5 (SURVEY §8(d) "Metric row").
+
+One step = one full frame (16.6M camera samples) through the HIP wavefront
+core, inputs (scene + BVH) resident in HBM, framebuffer left in HBM.  With
+--gpus N (torchrun, one process per GPU) the frame is tile-sharded
+(64x64 tiles, tile_id % N) and each step ends with the RCCL framebuffer
+gather to rank 0; total work is fixed, so scaling is "strong".
+
+The JSON line also carries:
+  roofline     -- the extend (closest-hit) kernel: algorithmic bytes per launch
+                  (28 B ray + 32 B per visited node + 32 B per
+                  primitive test + 16 B hit, visit counts from an instrumented
+                  frame) / its average launch time from HIP events in the
+                  timed region, against 8 TB/s HBM;
+  cpu_baseline -- the C restatement (oracle/) timed on this host's cores on a
+                  bounded sample of the same frame (1 spp, every k-th row).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--strands", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(sd, args, budget_s):
+    """Oracle timed on the host cores over a bounded sample (every k-th row, 1 spp)."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle_ffi  # test infrastructure: only bench's cpu_baseline leg uses it
+
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    t0 = time.time()
+    o = oracle_ffi.Oracle(sd)
+    build_s = time.time() - t0
+    W, H = args.width, args.height
+    # pilot: 8 rows spread over the frame, sample 0
+    step = max(1, H // 8)
+    t0 = time.time()
+    o.render(W, H, 1, args.depth, threads=threads, rows=(0, H, step))
+    pilot = time.time() - t0
+    rate = len(range(0, H, step)) * W / max(pilot, 1e-6)  # samples per second
+    frame = W * H
+    if rate * budget_s >= frame:
+        # whole frames, progressive samples 0..spp_cpu-1 (capped at the workload's spp)
+        spp_cpu = int(max(1, min(args.spp, rate * budget_s // frame)))
+        t0 = time.time()
+        o.render(W, H, spp_cpu, args.depth, threads=threads)
+        dt = time.time() - t0
+        samples = frame * spp_cpu
+        what = f"full {W}x{H} frame x {spp_cpu} of {args.spp} spp"
+    else:
+        n_rows = int(max(1, rate * budget_s // W))
+        step = max(1, H // n_rows)
+        rows = len(range(0, H, step))
+        t0 = time.time()
+        o.render(W, H, 1, args.depth, threads=threads, rows=(0, H, step))
+        dt = time.time() - t0
+        samples = rows * W
+        what = f"{rows} of {H} rows (every {step}th) x {W} px x 1 spp"
+    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{what} of the same frame = {samples} samples in {dt:.1f} s ({threads} threads, "
+                      f"CPU restatement oracle/, -O3 x86-64-v3, same seeds); throughput is spp-linear; "
+                      f"oracle BVH build {build_s:.1f} s excluded"}
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes of the extend kernel from the committed PMC profile, if any."""
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_extend_*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            return json.load(f).get("bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch  # noqa: F401  (load torch's HIP runtime before libkirk_hip.so)
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    sys.path.insert(0, HERE)
+    from ba_pathtracing_fur_amd import HipContext, comm_unique_id, scenes
+
+    W, H, spp, depth = args.width, args.height, args.spp, args.depth
+    t0 = time.time()
+    sd = scenes.config3(W, H, n_strands=args.strands)
+    gen_s = time.time() - t0
+    ctx = HipContext(device=local_rank)
+    t0 = time.time()
+    ctx.set_scene(sd)
+    ctx.build_accel()
+    build_s = time.time() - t0
+    st0 = ctx.stats()
+    if rank == 0:
+        log(f"scene: {sd.n_objects} objects, gen {gen_s:.1f}s, flatten+BVH+upload {build_s:.1f}s, "
+            f"depth {st0['bvh_depth']}, nodes {st0['n_nodes']}, HBM {st0['device_bytes'] / 1e9:.2f} GB")
+    if world > 1:
+        obj = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.comm_init(world, rank, obj[0])
+
+    def step(stats=False):
+        ctx.render(W, H, spp, depth, tile_size=args.tile, tile_rank=rank, tile_nranks=world, readback=False,
+                   stats=stats)
+        if world > 1:
+            ctx.gather_framebuffer(W, H, spp, depth, args.tile, world, rank, 0)
+
+    for _ in range(args.warmup):
+        step()
+    # one instrumented frame (outside the timed region): exact visit counts
+    step(stats=True)
+    cnt = ctx.stats()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    ext_ms = 0.0
+    ext_launches = 0
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        s = ctx.stats()
+        ext_ms += s["extend_ms"]
+        ext_launches += s["extend_launches"]
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    last = ctx.stats()
+    samples_per_step = W * H * spp
+    value = args.steps * samples_per_step / elapsed / 1e6
+    # roofline of the extend kernel (this rank's launches)
+    rays = cnt["extend_rays"]
+    alg_bytes_frame = 44 * rays + 32 * (cnt["node_visits"] + cnt["prim_tests"])
+    launches_frame = max(1, cnt["extend_launches"])
+    avg_launch_ms = ext_ms / max(1, ext_launches)
+    bytes_per_launch = alg_bytes_frame / launches_frame
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    traffic = pmc_traffic()
+    out = {
+        "metric": "Msamples/s at 1080p 8spp, 1M-strand hairball; achieved HBM GB/s vs peak",
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: seeded hairball (khp_gen_hairball, seed 0x4B49524B), scene built in-process",
+        "config": {
+            "workload": f"config3 scene at the metric row: {args.strands} strands ({sd.n_objects - 2} cone frusta) "
+                        f"on a 2-tri plane + 2x2 quad light, {W}x{H}, {spp} spp, depth {depth}",
+            "width": W, "height": H, "spp": spp, "depth": depth, "strands": args.strands,
+            "objects": sd.n_objects, "parallelism": f"tile-sharded {args.tile}px tiles x{world}, RCCL gather",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_extend (closest-hit BVH2 traversal)",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "bytes_per_launch": int(bytes_per_launch),
+            "avg_launch_ms": round(avg_launch_ms, 4),
+            "per_ray": {"nodes": round(cnt["node_visits"] / max(1, rays), 2),
+                        "prims": round(cnt["prim_tests"] / max(1, rays), 2)},
+        },
+        "frame": {
+            "extend_rays": rays, "shadow_rays": cnt["shadow_rays"],
+            "extend_ms": round(last["extend_ms"], 3), "shade_ms": round(last["shade_ms"], 3),
+            "shadow_ms": round(last["shadow_ms"], 3), "other_ms": round(last["other_ms"], 3),
+            "device_ms": round(last["render_ms"], 3),
+            "shadow_nodes_per_ray": round(cnt["shadow_node_visits"] / max(1, cnt["shadow_rays"]), 2),
+            "build_s": round(build_s, 2),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(sd, args, args.cpu_seconds)
+        except Exception as e:  # reported, never silently replaced
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -139,6 +139,7 @@ typedef struct {
 
 #define KHP_RENDER_OUT_DEVICE   (1u << 0)  /* out_rgb is a device pointer        */
 #define KHP_RENDER_NO_READBACK  (1u << 1)  /* keep framebuffer in HBM only       */
+#define KHP_RENDER_STATS        (1u << 2)  /* instrumented kernels for this call  */
 
 /* One khp_render call = samples [first_sample, first_sample+spp) of
  * PathTracer::render (CPU_PathTracer.cpp:17-52) for every pixel this rank

@@ -1407,14 +1407,14 @@ typedef struct {
     ko_ctx* c;
     const khp_render_params* p;
     float* out;
-    uint32_t y0, y1;
+    uint32_t y0, y1, ystep;
     int tid, nth;
 } job_t;
 
 static void* render_worker(void* arg) {
     job_t* j = (job_t*)arg;
     const khp_render_params* p = j->p;
-    for (uint32_t y = j->y0 + (uint32_t)j->tid; y < j->y1; y += (uint32_t)j->nth) {
+    for (uint32_t y = j->y0 + (uint32_t)j->tid * j->ystep; y < j->y1; y += (uint32_t)j->nth * j->ystep) {
         for (uint32_t x = 0; x < p->width; ++x) {
             if (!owns_pixel(p, x, y)) continue;
             float* o = j->out + 3 * ((size_t)y * p->width + x);
@@ -1436,14 +1436,19 @@ static void* render_worker(void* arg) {
 }
 
 int ko_render_rows(ko_ctx* c, const khp_render_params* p, int n_threads, uint32_t y0, uint32_t y1, float* out_rgb) {
-    if (!c || !p || !out_rgb || p->width == 0 || p->height == 0) return KHP_EINVAL;
+    return ko_render_rows_step(c, p, n_threads, y0, y1, 1, out_rgb);
+}
+
+int ko_render_rows_step(ko_ctx* c, const khp_render_params* p, int n_threads, uint32_t y0, uint32_t y1,
+                        uint32_t ystep, float* out_rgb) {
+    if (!c || !p || !out_rgb || p->width == 0 || p->height == 0 || ystep == 0) return KHP_EINVAL;
     if (y1 > p->height) y1 = p->height;
     if (n_threads < 1) n_threads = 1;
     if (n_threads > 256) n_threads = 256;
     pthread_t th[256];
     job_t jobs[256];
     for (int t = 0; t < n_threads; ++t) {
-        jobs[t].c = c; jobs[t].p = p; jobs[t].out = out_rgb; jobs[t].y0 = y0; jobs[t].y1 = y1;
+        jobs[t].c = c; jobs[t].p = p; jobs[t].out = out_rgb; jobs[t].y0 = y0; jobs[t].y1 = y1; jobs[t].ystep = ystep;
         jobs[t].tid = t; jobs[t].nth = n_threads;
         if (n_threads > 1) pthread_create(&th[t], NULL, render_worker, &jobs[t]);
     }

@@ -39,9 +39,11 @@ void ko_destroy(ko_ctx* c);
 /* PathTracer::render over `spp` samples; out_rgb running mean (W*H*3).
  * n_threads: row-parallel worker threads (ThreadManager::for_loop_double). */
 int ko_render(ko_ctx* c, const khp_render_params* p, int n_threads, float* out_rgb);
-/* Render only rows [y0,y1) (bounded CPU-baseline sample). */
+/* Render only rows [y0,y1) (bounded CPU-baseline sample); _step: every ystep-th row. */
 int ko_render_rows(ko_ctx* c, const khp_render_params* p, int n_threads, uint32_t y0, uint32_t y1,
                    float* out_rgb);
+int ko_render_rows_step(ko_ctx* c, const khp_render_params* p, int n_threads, uint32_t y0, uint32_t y1,
+                        uint32_t ystep, float* out_rgb);
 
 int ko_trace_closest(ko_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out,
                      int32_t* obj_out, float* uv_out, uint64_t* node_visits, uint64_t* prim_tests);

@@ -44,6 +44,7 @@ def load():
         "ko_destroy": (None, [c_void_p]),
         "ko_render": (c_int, [c_void_p, c_void_p, c_int, P(c_float)]),
         "ko_render_rows": (c_int, [c_void_p, c_void_p, c_int, c_uint32, c_uint32, P(c_float)]),
+        "ko_render_rows_step": (c_int, [c_void_p, c_void_p, c_int, c_uint32, c_uint32, c_uint32, P(c_float)]),
         "ko_trace_closest": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_int32),
                                      P(c_float), P(c_uint64), P(c_uint64)]),
         "ko_trace_any": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_uint8)]),
@@ -105,7 +106,8 @@ class Oracle:
         if rows is None:
             rc = self.lib.ko_render(self.ptr, ctypes.addressof(p), n, _fp(out))
         else:
-            rc = self.lib.ko_render_rows(self.ptr, ctypes.addressof(p), n, rows[0], rows[1], _fp(out))
+            step = rows[2] if len(rows) > 2 else 1
+            rc = self.lib.ko_render_rows_step(self.ptr, ctypes.addressof(p), n, rows[0], rows[1], step, _fp(out))
         if rc != 0:
             raise ValueError(f"ko_render failed ({rc})")
         return out
