@@ -46,7 +46,9 @@ __device__ __forceinline__ v3 follow(const Ray& r, float t) { return r.d * t + r
 
 // BoundingVolume::intersects (CPU_Datastructures/BoundingBox.cpp:142-194)
 __device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r,
-                                     v3 inv, const bool sgn[3], float& t0, float& t1) {
+                                     v3 inv, float& t0, float& t1) {
+    // dir_sign = dir < 0 (CPU_BVH.cpp:55-56); taken from the direction, not from inv (-0.0)
+    const bool sgn[3] = {r.d.x < 0.0f, r.d.y < 0.0f, r.d.z < 0.0f};
     float tmin = ((sgn[0] ? mxx : mnx) - r.o.x) * inv.x;
     float tmax = ((sgn[0] ? mnx : mxx) - r.o.x) * inv.x;
     float tymin = ((sgn[1] ? mxy : mny) - r.o.y) * inv.y;

@@ -34,7 +34,7 @@ struct Counters {
     uint32_t fetch_ext, fetch_sh;
     uint32_t pad[3];
     unsigned long long ext_rays, sh_rays;
-    unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests;
+    unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests, spills;
 };
 
 struct Wave {
@@ -87,7 +87,9 @@ __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
     uint32_t pid = blockIdx.x * blockDim.x + threadIdx.x;
     if (pid == 0) Wv.cnt->nq[0] = n;
     if (pid >= n) return;
-    uint32_t s_local = pid / Wv.P, p_local = pid - s_local * Wv.P;
+    // pixel-major: the samples of one pixel are adjacent paths, so a wave traces
+    // 64/n_samples neighbouring pixels x all their samples (cache reuse)
+    uint32_t p_local = pid / Wv.n_samples, s_local = pid - p_local * Wv.n_samples;
     uint32_t pixel = Wv.pix[Wv.p_off + p_local];
     uint32_t x = pixel % Wv.W, y = pixel / Wv.W;
     uint32_t key = path_key(Wv.seed, pixel, Wv.sample0 + s_local);
@@ -120,8 +122,17 @@ __global__ void k_prep(Counters* c, int cur) {
 // idle, the wave claims that many new rays with a single atomic and the idle
 // lanes start them, so a wave never waits for its slowest ray to admit new
 // work (Aila & Laine's persistent "while-while" with speculative refill).
-constexpr int RING = 8;         // LDS ring entries per lane (3 x 4 B each)
-constexpr int REFILL = 16;      // refill when >= REFILL lanes are idle
+#ifndef KHP_RING
+#define KHP_RING 8
+#endif
+#ifndef KHP_REFILL
+#define KHP_REFILL 16
+#endif
+#ifndef KHP_TRAV_WAVES
+#define KHP_TRAV_WAVES 5   // 96 VGPRs, no scratch; measured best (4: -9 %, 6: spills)
+#endif
+constexpr int RING = KHP_RING;      // LDS ring entries per lane (3 x 4 B each)
+constexpr int REFILL = KHP_REFILL;  // refill when >= REFILL lanes are idle
 constexpr size_t LDS_BYTES = 3 * RING * 256 * sizeof(uint32_t);
 
 struct SpillArea {
@@ -141,11 +152,11 @@ __device__ __forceinline__ uint32_t claim(unsigned long long idle, uint32_t* fet
 
 // ---- extend: closest hit for every queued ray ------------------------------------------
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
+__global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = Wv.cnt->nq[cur];
-    LdsStack<RING> stk;
-    stk.init(lds, threadIdx.x, spill.base, blockIdx.x * blockDim.x + threadIdx.x, spill.stride);
+    LdsStack<RING, STATS> stk;
+    stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0};
     TravRay tr;
     Hit h;
@@ -200,6 +211,10 @@ __global__ __launch_bounds__(256) void k_extend(DevScene S, Wave Wv, int cur, Sp
         if (lane_id() == 0) {
             atomicAdd(&Wv.cnt->node_visits, a);
             atomicAdd(&Wv.cnt->prim_tests, b);
+        }
+        unsigned long long sp_ = wave_sum((unsigned long long)stk.spills);
+        if (lane_id() == 0) {
+            atomicAdd(&Wv.cnt->spills, sp_);
         }
     }
 }
@@ -414,11 +429,11 @@ __device__ __forceinline__ void shadow_finish(const DevScene& S, const Wave& Wv,
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
+__global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = Wv.cnt->nsh;
-    LdsStack<RING> stk;
-    stk.init(lds, threadIdx.x, spill.base, blockIdx.x * blockDim.x + threadIdx.x, spill.stride);
+    LdsStack<RING, STATS> stk;
+    stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0};
     TravRay tr;
     float tmax = 0.0f;
@@ -466,6 +481,10 @@ __global__ __launch_bounds__(256) void k_shadow(DevScene S, Wave Wv, SpillArea s
             atomicAdd(&Wv.cnt->sh_node_visits, a);
             atomicAdd(&Wv.cnt->sh_prim_tests, b);
         }
+        unsigned long long sp_ = wave_sum((unsigned long long)stk.spills);
+        if (lane_id() == 0) {
+            atomicAdd(&Wv.cnt->spills, sp_);
+        }
     }
 }
 
@@ -482,7 +501,7 @@ __global__ __launch_bounds__(256) void k_accumulate(Wave Wv, float* fb) {
     float* o = fb + 3 * (size_t)pixel;
     float r = o[0], g = o[1], b = o[2];
     for (uint32_t s = 0; s < Wv.n_samples; ++s) {
-        uint32_t pid = s * Wv.P + p;
+        uint32_t pid = p * Wv.n_samples + s;
         float cr = Wv.C[0][pid], cg = Wv.C[1][pid], cb = Wv.C[2][pid];
         uint32_t k = Wv.sample0 + s;
         if (k == 0) {
@@ -934,6 +953,7 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     c->st.prim_tests = hc.prim_tests;
     c->st.shadow_node_visits = hc.sh_node_visits;
     c->st.shadow_prim_tests = hc.sh_prim_tests;
+    c->st.stack_spills = hc.spills;
     return KHP_OK;
 }
 

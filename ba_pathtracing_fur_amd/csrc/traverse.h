@@ -30,14 +30,10 @@ struct TravStats {
 struct TravRay {
     Ray r;
     v3 inv;
-    bool sgn[3];
 };
 
 __device__ __forceinline__ void trav_setup(TravRay& tr, const Ray& r) {
     tr.r = r;
-    tr.sgn[0] = r.d.x < 0.0f;
-    tr.sgn[1] = r.d.y < 0.0f;
-    tr.sgn[2] = r.d.z < 0.0f;
     tr.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
 }
 
@@ -63,47 +59,53 @@ struct PrivStack {
     }
 };
 
-template <int R>
+// The LDS image is three [R][256] arrays (ref, tmin bits, tmax bits) at the
+// start of the kernel's dynamic LDS; a lane's column starts at its threadIdx.x.
+// The spill area is [STACK_MAX][grid lanes] int4, addressed from blockIdx /
+// threadIdx only on the (rare) spill path, so it costs no registers.
+template <int R, bool COUNT>
 struct LdsStack {
     static_assert((R & (R - 1)) == 0, "ring size must be a power of two");
-    uint32_t* lref;   // this lane's column in LDS: entry k at lref[k * 256]
-    float* lt0;
-    float* lt1;
-    int4* g;          // this lane's spill column: entry k at g[k * gstride]
-    uint32_t gstride;
+    uint32_t* lds;
+    int4* spill;
+    uint32_t stride;
     int sp, lo;       // entries [0, lo) spilled to global, [lo, sp) in the LDS ring
-    __device__ __forceinline__ void init(uint32_t* lds, uint32_t lane_in_block, int4* spill, uint32_t gtid,
-                                         uint32_t stride) {
-        lref = lds + lane_in_block;
-        lt0 = reinterpret_cast<float*>(lds + R * 256) + lane_in_block;
-        lt1 = reinterpret_cast<float*>(lds + 2 * R * 256) + lane_in_block;
-        g = spill + gtid;
-        gstride = stride;
+    uint32_t spills;  // spill events (COUNT builds only)
+    __device__ __forceinline__ void init(uint32_t* lds_base, int4* spill_base, uint32_t grid_lanes) {
+        lds = lds_base;
+        spill = spill_base;
+        stride = grid_lanes;
         sp = lo = 0;
+        spills = 0;
     }
     __device__ __forceinline__ void clear() { sp = lo = 0; }
     __device__ __forceinline__ bool empty() const { return sp == 0; }
+    __device__ __forceinline__ uint32_t slot(int e) const { return (uint32_t)(e & (R - 1)) * 256u + threadIdx.x; }
+    __device__ __forceinline__ int4* gcell(int e) const {
+        return spill + (size_t)e * stride + blockIdx.x * blockDim.x + threadIdx.x;
+    }
     __device__ __forceinline__ void push(uint32_t r, float a, float b) {
         if (sp - lo == R) {  // ring full: move the oldest entry to the spill column
-            int k = (lo & (R - 1)) * 256;
-            g[(size_t)lo * gstride] = make_int4((int)lref[k], (int)bits_from_f(lt0[k]), (int)bits_from_f(lt1[k]), 0);
+            uint32_t k = slot(lo);
+            *gcell(lo) = make_int4((int)lds[k], (int)lds[k + R * 256], (int)lds[k + 2 * R * 256], 0);
             ++lo;
+            if (COUNT) ++spills;
         }
-        int k = (sp & (R - 1)) * 256;
-        lref[k] = r;
-        lt0[k] = a;
-        lt1[k] = b;
+        uint32_t k = slot(sp);
+        lds[k] = r;
+        lds[k + R * 256] = bits_from_f(a);
+        lds[k + 2 * R * 256] = bits_from_f(b);
         ++sp;
     }
     __device__ __forceinline__ void pop(uint32_t& r, float& a, float& b) {
         --sp;
         if (sp >= lo) {
-            int k = (sp & (R - 1)) * 256;
-            r = lref[k];
-            a = lt0[k];
-            b = lt1[k];
+            uint32_t k = slot(sp);
+            r = lds[k];
+            a = f_from_bits(lds[k + R * 256]);
+            b = f_from_bits(lds[k + 2 * R * 256]);
         } else {
-            int4 e = g[(size_t)sp * gstride];
+            int4 e = *gcell(sp);
             r = (uint32_t)e.x;
             a = f_from_bits((uint32_t)e.y);
             b = f_from_bits((uint32_t)e.z);
@@ -118,7 +120,7 @@ __device__ __forceinline__ bool trav_begin(const DevScene& S, const TravRay& tr,
     stk.clear();
     float t0, t1;
     if (!slab(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4], S.root_box[5], tr.r, tr.inv,
-              tr.sgn, t0, t1))
+              t0, t1))
         return false;
     stk.push((uint32_t)S.root_ref, t0, t1);
     return true;
@@ -137,8 +139,8 @@ __device__ __forceinline__ void visit_interior(const DevScene& S, const TravRay&
     float4 a = np[0], b = np[1], c = np[2];
     int4 rf = reinterpret_cast<const int4*>(np)[3];
     float l0, l1, r0, r1;
-    bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, tr.sgn, l0, l1);
-    bool rh = slab(b.z, b.w, c.x, c.y, c.z, c.w, tr.r, tr.inv, tr.sgn, r0, r1);
+    bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, l0, l1);
+    bool rh = slab(b.z, b.w, c.x, c.y, c.z, c.w, tr.r, tr.inv, r0, r1);
     if (lh && rh) {
         if (l0 < r0) {
             stk.push((uint32_t)rf.y, r0, r1);

@@ -73,7 +73,8 @@ class Stats(ctypes.Structure):
                 ("upload_ms", c_double), ("render_ms", c_double), ("extend_ms", c_double), ("shade_ms", c_double),
                 ("shadow_ms", c_double), ("other_ms", c_double), ("extend_rays", c_uint64),
                 ("shadow_rays", c_uint64), ("extend_launches", c_uint64), ("node_visits", c_uint64),
-                ("prim_tests", c_uint64), ("shadow_node_visits", c_uint64), ("shadow_prim_tests", c_uint64)]
+                ("prim_tests", c_uint64), ("shadow_node_visits", c_uint64), ("shadow_prim_tests", c_uint64),
+                ("stack_spills", c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -102,7 +103,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("KHP_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise RuntimeError(f"HIP core not built: {p} missing (run __graft_entry__.build())")
     lib = ctypes.CDLL(p)

@@ -220,6 +220,7 @@ def main():
             "shadow_ms": round(last["shadow_ms"], 3), "other_ms": round(last["other_ms"], 3),
             "device_ms": round(last["render_ms"], 3),
             "shadow_nodes_per_ray": round(cnt["shadow_node_visits"] / max(1, cnt["shadow_rays"]), 2),
+            "stack_spills_per_ray": round(cnt["stack_spills"] / max(1, rays + cnt["shadow_rays"]), 4),
             "build_s": round(build_s, 2),
         },
     }

@@ -166,6 +166,7 @@ typedef struct {
     double extend_ms, shade_ms, shadow_ms, other_ms;  /* per-kernel device time, last render */
     uint64_t extend_rays, shadow_rays, extend_launches;
     uint64_t node_visits, prim_tests, shadow_node_visits, shadow_prim_tests; /* KHP_CTX_STATS only */
+    uint64_t stack_spills;           /* traversal-stack entries spilled from LDS (stats only) */
 } khp_stats;
 
 #define KHP_CTX_STATS  (1u << 0)   /* instrumented kernels: count node/prim visits */
