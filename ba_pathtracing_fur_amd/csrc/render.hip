@@ -575,12 +575,7 @@ __global__ void k_unpack(float* fb, const uint32_t* pix, uint32_t P, const float
 // ============================================================================
 //  host side
 // ============================================================================
-static thread_local std::string g_err;
 
-static khp_status fail(khp_status s, const std::string& msg) {
-    g_err = msg;
-    return s;
-}
 
 #define HIPCHK(expr)                                                                                     \
     do {                                                                                                 \
@@ -625,7 +620,7 @@ struct khp_ctx {
     size_t cap = 0;
     DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb, cnt, spill;
     // framebuffer + pixel list
-    DevMem fb, pix, stage, stage2, stage_pix;
+    DevMem fb, pix, stage, stage_pix;
     uint32_t fbW = 0, fbH = 0;
     std::vector<uint32_t> pix_host;
     uint32_t pix_key[5] = {0, 0, 0, 0, 0};
@@ -635,7 +630,9 @@ struct khp_ctx {
     std::vector<TimedLaunch> launches;
     int grid_ext = 0, grid_sh = 0, grid_shade = 0;
     khp_stats st{};
-    // rccl
+    // rccl gather: pixel lists cached per (W, H, tile, nranks, rank, root)
+    uint32_t gather_key[6] = {0, 0, 0, 0, 0, 0};
+    std::vector<size_t> gather_counts;   // root: pixels per rank; sender: [own count]
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
 };
@@ -650,7 +647,7 @@ static hipEvent_t next_event(khp_ctx* c) {
 }
 
 extern "C" int khp_abi_version(void) { return KHP_ABI_VERSION; }
-extern "C" const char* khp_last_error(void) { return g_err.c_str(); }
+extern "C" const char* khp_last_error(void) { return last_error(); }
 
 extern "C" khp_status khp_create(khp_ctx** out, int device, uint32_t flags) {
     if (!out) return fail(KHP_EINVAL, "out is null");
@@ -1061,43 +1058,44 @@ extern "C" khp_status khp_gather_framebuffer(khp_ctx* c, const khp_render_params
     if (p->tile_nranks != (uint32_t)c->nranks) return fail(KHP_EINVAL, "tile_nranks must equal the comm size");
     HIPCHK(hipSetDevice(c->device));
     uint32_t T = p->tile_size ? p->tile_size : 64;
+    uint32_t key[6] = {p->width, p->height, T, (uint32_t)c->nranks, (uint32_t)c->rank, (uint32_t)root};
+    if (memcmp(key, c->gather_key, sizeof(key)) != 0) {
+        // the pixel lists depend only on the frame geometry: build + upload once, not per frame
+        std::vector<uint32_t> flat, one;
+        c->gather_counts.assign((size_t)c->nranks, 0);
+        for (int r = 0; r < c->nranks; ++r) {
+            if ((c->rank == root) == (r == root)) continue;  // root: every sender; sender: itself
+            owned_pixels(p->width, p->height, T, (uint32_t)r, (uint32_t)c->nranks, one);
+            c->gather_counts[r] = one.size();
+            flat.insert(flat.end(), one.begin(), one.end());
+        }
+        if (c->rank != root) c->gather_counts[root] = 0;
+        HIPCHK(upload(c->stage_pix, flat.data(), flat.size(), c->stream));
+        HIPCHK(c->stage.ensure(flat.size() * 3 * sizeof(float) + 16));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        memcpy(c->gather_key, key, sizeof(key));
+    }
     if (c->rank != root) {
-        std::vector<uint32_t> mine;
-        owned_pixels(p->width, p->height, T, (uint32_t)c->rank, (uint32_t)c->nranks, mine);
-        HIPCHK(upload(c->stage_pix, mine.data(), mine.size(), c->stream));
-        HIPCHK(c->stage.ensure(mine.size() * 3 * sizeof(float) + 16));
-        uint32_t P = (uint32_t)mine.size();
+        uint32_t P = (uint32_t)c->gather_counts[c->rank];
         if (P) hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
                                   c->stage_pix.as<uint32_t>(), P, c->stage.as<float>());
         NCCLCHK(ncclSend(c->stage.p, (size_t)P * 3, ncclFloat32, root, c->comm, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         return KHP_OK;
     }
-    // root: receive every other rank's pixels, then scatter them into the framebuffer
-    std::vector<std::vector<uint32_t>> lists((size_t)c->nranks);
+    // root: receive every other rank's pixels (one grouped recv), then scatter them into the framebuffer
     size_t total = 0;
-    for (int r = 0; r < c->nranks; ++r) {
-        if (r == root) continue;
-        owned_pixels(p->width, p->height, T, (uint32_t)r, (uint32_t)c->nranks, lists[r]);
-        total += lists[r].size();
-    }
-    HIPCHK(c->stage.ensure(total * 3 * sizeof(float) + 16));
-    HIPCHK(c->stage2.ensure(total * sizeof(uint32_t) + 16));
-    std::vector<uint32_t> flat;
-    flat.reserve(total);
-    for (int r = 0; r < c->nranks; ++r) flat.insert(flat.end(), lists[r].begin(), lists[r].end());
-    HIPCHK(hipMemcpyAsync(c->stage2.p, flat.data(), flat.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     NCCLCHK(ncclGroupStart());
-    size_t off = 0;
     for (int r = 0; r < c->nranks; ++r) {
         if (r == root) continue;
-        NCCLCHK(ncclRecv(c->stage.as<float>() + off * 3, lists[r].size() * 3, ncclFloat32, r, c->comm, c->stream));
-        off += lists[r].size();
+        NCCLCHK(ncclRecv(c->stage.as<float>() + total * 3, c->gather_counts[r] * 3, ncclFloat32, r, c->comm,
+                         c->stream));
+        total += c->gather_counts[r];
     }
     NCCLCHK(ncclGroupEnd());
     if (total)
         hipLaunchKernelGGL(k_unpack, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, c->stream,
-                           c->fb.as<float>(), c->stage2.as<uint32_t>(), (uint32_t)total, c->stage.as<float>());
+                           c->fb.as<float>(), c->stage_pix.as<uint32_t>(), (uint32_t)total, c->stage.as<float>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     return KHP_OK;

@@ -443,6 +443,44 @@ void make_device_layout(HostScene& hs) {
 // ============================================================================
 using namespace khp;
 
+static thread_local std::string g_err;
+khp_status khp::fail(khp_status s, const std::string& msg) {
+    g_err = msg;
+    return s;
+}
+const char* khp::last_error() { return g_err.c_str(); }
+
+extern "C" khp_status khp_host_build(const khp_scene* scene, uint32_t* n_nodes, uint32_t* depth, float* node_boxes,
+                                     int32_t* node_first, int32_t* node_count, int32_t* object_ids,
+                                     float* obj_bounds, float* records) {
+    if (!scene || !n_nodes) return fail(KHP_EINVAL, "scene or n_nodes is null");
+    HostScene hs;
+    std::string err = flatten_scene(scene, hs);
+    if (!err.empty()) return fail(KHP_EINVAL, err);
+    unsigned nt = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+    build_bvh(hs, (int)nt);
+    *n_nodes = (uint32_t)hs.nodes.size();
+    if (depth) *depth = hs.depth;
+    for (size_t i = 0; i < hs.nodes.size(); ++i) {
+        const BuildNode& n = hs.nodes[i];
+        if (node_boxes) {
+            float b[6] = {n.mn.x, n.mn.y, n.mn.z, n.mx.x, n.mx.y, n.mx.z};
+            memcpy(node_boxes + 6 * i, b, sizeof(b));
+        }
+        if (node_first) node_first[i] = n.count ? n.first : -1;
+        if (node_count) node_count[i] = n.count;
+    }
+    for (uint32_t i = 0; i < hs.n_obj; ++i) {
+        if (object_ids) object_ids[i] = (int32_t)hs.ids[i];
+        if (obj_bounds) {
+            memcpy(obj_bounds + 9 * (size_t)i, &hs.bounds[6 * (size_t)i], 6 * sizeof(float));
+            memcpy(obj_bounds + 9 * (size_t)i + 6, &hs.centroid[3 * (size_t)i], 3 * sizeof(float));
+        }
+        if (records) memcpy(records + 16 * (size_t)i, &hs.rec[16 * (size_t)i], 16 * sizeof(float));
+    }
+    return KHP_OK;
+}
+
 static const char* kBsdfNames[KHP_BSDF_COUNT] = {
     "LambertianReflectionBSDF", "SpecularReflectionBSDF", "SpecularTransmissionBSDF", "GlossyBSDF",
     "GlassBSDF", "MilkGlassBSDF", "LambertianTransmissionBSDF", "EmissionBSDF", "TransparentBSDF",
@@ -470,8 +508,12 @@ extern "C" khp_status khp_camera_setup(const float position[3], const float look
                                        float sensor_w, float sensor_h, float focal_length, uint32_t width,
                                        uint32_t height, khp_camera* out) {
     if (!position || !look_at || !up || !out || width == 0 || height == 0 || focal_length <= 0.0f)
-        return KHP_EINVAL;
+        return fail(KHP_EINVAL, "camera: null pointer, zero resolution or focal length <= 0");
     v3 pos = ld3(position), la = ld3(look_at), upv = ld3(up);
+    // KIRK would produce a NaN frame here (normalize of a zero vector); reject it instead
+    v3 side = cross(upv, la);
+    if (dot(la, la) == 0.0f || dot(side, side) == 0.0f)
+        return fail(KHP_EINVAL, "degenerate camera frame (look direction zero or parallel to up)");
     float aspect = (float)width / (float)height;
     v3 az = normalize(-la);
     v3 ax = normalize(cross(upv, az));

@@ -84,4 +84,8 @@ void build_bvh(HostScene& hs, int n_threads);
 void make_device_layout(HostScene& hs);
 void light_init(DevLight& L, const khp_light& in);
 
+// Per-thread message behind khp_last_error(); every failing entry point sets it.
+khp_status fail(khp_status s, const std::string& msg);
+const char* last_error();
+
 }  // namespace khp

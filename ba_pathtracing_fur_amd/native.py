@@ -85,7 +85,7 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_render", "khp_read_framebuffer", "khp_trace_closest", "khp_trace_any", "khp_get_stats",
             "khp_comm_unique_id", "khp_comm_init", "khp_gather_framebuffer", "khp_bsdf_kind_from_name",
             "khp_bsdf_name", "khp_shader_kind_from_name", "khp_camera_setup", "khp_fibers_to_cones",
-            "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus"]
+            "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus", "khp_host_build"]
 
 _lib = None
 
@@ -134,6 +134,8 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
                                      P(c_float)]),
         "khp_gen_icosphere": (c_int, [c_uint32, P(c_float), c_float, P(c_float), P(c_float)]),
         "khp_gen_torus": (c_int, [c_uint32, c_uint32, P(c_float), c_float, c_float, P(c_float), P(c_float)]),
+        "khp_host_build": (c_int, [P(SceneDesc), P(c_uint32), P(c_uint32), P(c_float), P(c_int32), P(c_int32),
+                                   P(c_int32), P(c_float), P(c_float)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -153,3 +155,24 @@ class KhpError(RuntimeError):
 def check(lib, status: int, where: str):
     if status != KHP_OK:
         raise KhpError(status, where, (lib.khp_last_error() or b"").decode())
+
+
+def host_build(scene) -> dict:
+    """Flatten + BVH build of the product, run on the host (no GPU): khp_host_build."""
+    lib = load_library()
+    d = scene.desc()
+    nn, dep = c_uint32(), c_uint32()
+    ip = lambda a: a.ctypes.data_as(POINTER(c_int32))
+    check(lib, lib.khp_host_build(ctypes.byref(d), ctypes.byref(nn), ctypes.byref(dep), None, None, None, None, None,
+                                  None), "khp_host_build")
+    n, m = nn.value, scene.n_objects
+    boxes = np.empty((n, 6), np.float32)
+    first = np.empty(n, np.int32)
+    count = np.empty(n, np.int32)
+    ids = np.empty(m, np.int32)
+    bounds = np.empty((m, 9), np.float32)
+    rec = np.empty((m, 16), np.float32)
+    check(lib, lib.khp_host_build(ctypes.byref(d), ctypes.byref(nn), ctypes.byref(dep), fptr(boxes), ip(first),
+                                  ip(count), ip(ids), fptr(bounds), fptr(rec)), "khp_host_build")
+    return {"boxes": boxes, "first": first, "count": count, "ids": ids, "bounds": bounds, "records": rec,
+            "depth": dep.value}

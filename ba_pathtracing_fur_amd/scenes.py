@@ -188,6 +188,33 @@ class SceneData:
         self._desc = d
         return d
 
+    # --- plain-data (de)serialisation: .npz of arrays + raw boundary structs -----------
+    def to_arrays(self) -> dict:
+        """Arrays for np.savez; materials/lights/camera are their khp_* struct bytes."""
+        raw = lambda objs, T: np.frombuffer(bytes((T * len(objs))(*objs)), np.uint8).copy()
+        return {"tri_v": self.tri_v, "tri_n": self.tri_n, "tri_mat": self.tri_mat,
+                "cone_base_r0": self.cone_base_r0, "cone_apex_r1": self.cone_apex_r1, "cone_mat": self.cone_mat,
+                "materials": raw(self.materials, N.Material), "lights": raw(self.lights, N.Light),
+                "env": np.float32([*self.env_color, *self.env_ambient]),
+                "camera": np.frombuffer(bytes(self.cam), np.uint8).copy(), "name": np.array(self.name)}
+
+    @classmethod
+    def from_arrays(cls, a) -> "SceneData":
+        def structs(buf, T):
+            buf = np.ascontiguousarray(buf, np.uint8).tobytes()
+            n = len(buf) // ctypes.sizeof(T)
+            return list((T * n).from_buffer_copy(buf)) if n else []
+        env = np.asarray(a["env"], np.float32)
+        return cls(tri_v=np.asarray(a["tri_v"], np.float32), tri_n=np.asarray(a["tri_n"], np.float32),
+                   tri_mat=np.asarray(a["tri_mat"], np.uint32),
+                   cone_base_r0=np.asarray(a["cone_base_r0"], np.float32),
+                   cone_apex_r1=np.asarray(a["cone_apex_r1"], np.float32),
+                   cone_mat=np.asarray(a["cone_mat"], np.uint32),
+                   materials=structs(a["materials"], N.Material), lights=structs(a["lights"], N.Light),
+                   env_color=tuple(float(x) for x in env[:3]), env_ambient=tuple(float(x) for x in env[3:]),
+                   cam=N.Camera.from_buffer_copy(np.ascontiguousarray(a["camera"], np.uint8).tobytes()),
+                   name=str(a["name"]))
+
 
 # ---- generators (libkirk_hip host code) -------------------------------------------
 def hairball(n_strands: int, center, ball_radius: float, root_radius: float = 0.004, verts: int = 10,
@@ -296,5 +323,43 @@ def config5(width=3840, height=2160, n_strands=1_000_000, torus_grid=500, glass_
     return sd
 
 
+def zoo(width=64, height=48, n_strands=400) -> SceneData:
+    """Every BSDF of the zoo (Bsdf.cpp) and every light kind (Light.cpp) in one frame.
+
+    Not a BASELINE config: a coverage scene for parity tests.  A row of small
+    icospheres carries the nine surface BSDFs, two hairballs carry the Marschner
+    and d'Eon fibers; point, quad, spot and sun lights all contribute.
+    """
+    sd = SceneData(name="zoo")
+    v, n = quad((-4, 0, -4), (-4, 0, 4), (4, 0, 4), (4, 0, -4), (0, 1, 0))
+    sd.add_triangles(v, n, sd.add_material(material(diffuse=(0.6, 0.6, 0.6))))
+    v, n = quad((-4, 0, -2.5), (4, 0, -2.5), (4, 3, -2.5), (-4, 3, -2.5), (0, 0, 1))
+    sd.add_triangles(v, n, sd.add_material(material(diffuse=(0.3, 0.5, 0.3))))
+    surf = [material("LambertianReflectionBSDF", diffuse=(0.8, 0.3, 0.2)),
+            material("SpecularReflectionBSDF", specular=(0.9, 0.9, 0.7)),
+            material("SpecularTransmissionBSDF", volume=(0.9, 1.0, 0.9), ior=1.33),
+            material("GlossyBSDF", diffuse=(0.2, 0.3, 0.8), specular=(0.8, 0.8, 0.8), roughness=0.3),
+            material("GlassBSDF", volume=(1.0, 0.95, 0.9), ior=1.52),
+            material("MilkGlassBSDF", diffuse=(0.9, 0.9, 0.9), volume=(0.9, 0.9, 1.0), ior=1.45, roughness=0.5),
+            material("LambertianTransmissionBSDF", diffuse=(0.7, 0.7, 0.2)),
+            material("EmissionBSDF", emission=(2.0, 1.0, 0.5)),
+            material("TransparentBSDF", volume=(0.5, 0.8, 1.0))]
+    for i, m in enumerate(surf):
+        gv, gn = icosphere(1, (-2.4 + 0.6 * i, 0.3, -0.6 + 0.35 * (i % 2)), 0.27)
+        sd.add_triangles(gv, gn, sd.add_material(m))
+    for k, bsdf in enumerate(("MarschnerHairBSDF", "DEonHairBSDF")):
+        pos, rad = hairball(n_strands, (-0.9 + 1.8 * k, 0.9, 0.8), 0.3, root_radius=0.006, seed=SEED + k)
+        sd.add_fibers(pos, rad, sd.add_material(fiber_material(bsdf)))
+    sd.lights += [point_light((1.5, 2.5, 1.5), (4.0, 3.5, 3.0), radius=0.2),
+                  quad_light((0.0, 2.8, 0.0), (0.0, -1.0, 0.0), (1.0, 1.0), (3.0, 3.0, 3.0), att_const=1.0),
+                  spot_light((-2.0, 2.5, 1.0), (0.5, -1.0, -0.3), (6.0, 5.0, 4.0), outer=30.0, inner=15.0,
+                             att_const=1.0),
+                  sun_light((0.3, -1.0, -0.4), (0.8, 0.8, 0.7))]
+    sd.env_color = (0.2, 0.25, 0.35)
+    sd.env_ambient = (0.05, 0.05, 0.05)
+    sd.cam = camera((0.0, 1.5, 4.2), (0.0, -0.25, -1.0), (0.0, 1.0, 0.0), width, height)
+    return sd
+
+
 def build_config(name: str, **kw) -> SceneData:
-    return {"config1": config1, "config2": config2, "config3": config3, "config5": config5}[name](**kw)
+    return {"config1": config1, "config2": config2, "config3": config3, "config5": config5, "zoo": zoo}[name](**kw)

@@ -108,17 +108,17 @@ def pmc_traffic():
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    sys.path.insert(0, HERE)
+    from ba_pathtracing_fur_amd.sharding import ShardedFrame, env_ranks
+
+    rank, local_rank, world = env_ranks()
     dist = None
     if world > 1:
         import torch  # noqa: F401  (load torch's HIP runtime before libkirk_hip.so)
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")
-    sys.path.insert(0, HERE)
-    from ba_pathtracing_fur_amd import HipContext, comm_unique_id, scenes
+        dist.init_process_group("gloo")   # bootstrap only: the framebuffer moves over RCCL
+    from ba_pathtracing_fur_amd import HipContext, scenes
 
     W, H, spp, depth = args.width, args.height, args.spp, args.depth
     t0 = time.time()
@@ -133,16 +133,10 @@ def main():
     if rank == 0:
         log(f"scene: {sd.n_objects} objects, gen {gen_s:.1f}s, flatten+BVH+upload {build_s:.1f}s, "
             f"depth {st0['bvh_depth']}, nodes {st0['n_nodes']}, HBM {st0['device_bytes'] / 1e9:.2f} GB")
-    if world > 1:
-        obj = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        ctx.comm_init(world, rank, obj[0])
+    frame = ShardedFrame(ctx, rank, world, dist, tile=args.tile)
 
     def step(stats=False):
-        ctx.render(W, H, spp, depth, tile_size=args.tile, tile_rank=rank, tile_nranks=world, readback=False,
-                   stats=stats)
-        if world > 1:
-            ctx.gather_framebuffer(W, H, spp, depth, args.tile, world, rank, 0)
+        frame.render(W, H, spp, depth, stats=stats)
 
     for _ in range(args.warmup):
         step()
@@ -150,27 +144,17 @@ def main():
     step(stats=True)
     cnt = ctx.stats()
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
     ext_ms = 0.0
     ext_launches = 0
-    barrier()
+    frame.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         s = ctx.stats()
         ext_ms += s["extend_ms"]
         ext_launches += s["extend_launches"]
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    frame.barrier()
+    elapsed = frame.max_over_ranks(time.perf_counter() - t0)
     last = ctx.stats()
     samples_per_step = W * H * spp
     value = args.steps * samples_per_step / elapsed / 1e6
@@ -232,7 +216,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
-        dist.barrier()
+        frame.barrier()
         dist.destroy_process_group()
     ctx.close()
 

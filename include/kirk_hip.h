@@ -215,6 +215,19 @@ khp_status khp_comm_init(khp_ctx* ctx, int nranks, int rank, const uint8_t id[12
  * framebuffer over RCCL; root may then khp_read_framebuffer. Collective. */
 khp_status khp_gather_framebuffer(khp_ctx* ctx, const khp_render_params* p, int root);
 
+/* ---- host-only introspection (no device needed) ---------------------------- */
+/* Runs exactly the flatten + BVH build of khp_set_scene/khp_build_accel on the
+ * host.  Call with null arrays first to get *n_nodes / *depth.  Nodes are in
+ * DFS preorder (node, left subtree, right subtree), like the recursion of
+ * BVHNode::split (CPU_BVH.cpp:95-138).
+ *   node_boxes [n_nodes][6] bmin.xyz bmax.xyz; node_first/node_count: leaf
+ *   candidate range into object_ids (count 0 = interior, first = -1);
+ *   object_ids [n_obj] leaf order; obj_bounds [n_obj][9] bmin bmax centroid;
+ *   records [n_obj][16] the 64-byte intersection record of every object. */
+khp_status khp_host_build(const khp_scene* scene, uint32_t* n_nodes, uint32_t* depth, float* node_boxes,
+                          int32_t* node_first, int32_t* node_count, int32_t* object_ids, float* obj_bounds,
+                          float* records);
+
 /* ---- registries / host helpers --------------------------------------------- */
 /* BsdfFactory::getBsdf / ShaderFactory::getShader by KIRK name; -1 if unknown
  * (KIRK throws std::invalid_argument, BsdfFactory.cpp:39-45). */

@@ -1,0 +1,43 @@
+"""Test configuration.
+
+Markers:
+  gpu -- needs an MI355X (runs through libkirk_hip.so's HIP kernels via the C-ABI).
+Everything else runs on the CPU: the oracle (oracle/, test infrastructure)
+against analytic known answers and committed golden fixtures, the product's
+host-side flatten/BVH/generators, ABI exports, and world_size-2 gloo runs.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: requires an AMD MI355X GPU (HIP kernels through the C-ABI)")
+
+
+def _built():
+    lib = os.path.join(ROOT, "ba_pathtracing_fur_amd", "lib", "libkirk_hip.so")
+    orc = os.path.join(ROOT, "oracle", "build", "libkirk_oracle.so")
+    if not os.path.exists(lib):
+        subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "ba_pathtracing_fur_amd", "csrc")])
+    if not os.path.exists(orc):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+_built()
+
+
+@pytest.fixture(scope="session")
+def hip_ctx():
+    """One khp_ctx on cuda:0 shared by the GPU tests (one process, one GPU)."""
+    from ba_pathtracing_fur_amd.pathtracer import HipContext
+    ctx = HipContext(0)
+    yield ctx
+    ctx.close()

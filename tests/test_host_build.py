@@ -1,0 +1,119 @@
+"""Product host side (scene.cpp: flatten, binned-SAH BVH, generators, camera) vs the oracle.
+
+The closest hit of KIRK's traversal depends on BVH child order,
+so the product must build the *same* tree as CPU_BVH.cpp; these tests compare
+khp_host_build's output node by node with the oracle's build.  CPU only.
+"""
+import numpy as np
+import pytest
+
+import oracle_ffi
+from ba_pathtracing_fur_amd import native as N
+from ba_pathtracing_fur_amd import scenes as S
+
+TRI_TAG = np.uint32(0x7FC0DEAD)
+
+
+def _same_bits(a, b):
+    return np.array_equal(np.ascontiguousarray(a, np.float32).view(np.uint32),
+                          np.ascontiguousarray(b, np.float32).view(np.uint32))
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("config1", dict(width=32, height=32)),
+    ("config2", dict(width=32, height=32, n_strands=2000)),
+    ("config3", dict(width=32, height=32, n_strands=3000)),
+    ("config5", dict(width=32, height=32, n_strands=1500, torus_grid=20, glass_subdiv=2)),
+])
+def test_bvh_matches_oracle(name, kw):
+    sd = S.build_config(name, **kw)
+    prod = N.host_build(sd)
+    o = oracle_ffi.Oracle(sd)
+    boxes, first, count, ids, depth = o.bvh()
+    assert prod["depth"] == depth
+    assert _same_bits(prod["boxes"], boxes)
+    assert np.array_equal(prod["first"], first) and np.array_equal(prod["count"], count)
+    assert np.array_equal(prod["ids"], ids)
+    assert _same_bits(prod["bounds"], o.object_bounds())
+
+
+def test_records_match_oracle():
+    sd = S.config5(32, 32, n_strands=800, torus_grid=12, glass_subdiv=1)
+    prod = N.host_build(sd)
+    o = oracle_ffi.Oracle(sd)
+    nt = len(sd.tri_v)
+    rec = prod["records"]
+    cr = o.cone_records()
+    assert _same_bits(rec[nt:], cr[:, :16])          # base,r0 | u,slope | v,min_d | w,max_d
+    tr, _ = o.tri_records()
+    assert _same_bits(rec[:nt, 0:3], tr[:, 0:3])     # A
+    assert np.all(rec[:nt, 3].view(np.uint32) == TRI_TAG)
+    assert _same_bits(rec[:nt, 4:7], tr[:, 9:12])    # ab
+    assert _same_bits(rec[:nt, 8:11], tr[:, 12:15])  # ac
+
+
+def test_build_is_deterministic():
+    sd = S.config2(16, 16, n_strands=5000)
+    a, b = N.host_build(sd), N.host_build(sd)
+    for k in ("boxes", "first", "count", "ids"):
+        assert np.array_equal(a[k], b[k])
+
+
+def test_degenerate_scene_coincident_centroids():
+    # all objects share one centroid: SAH finds no split; the builder must still terminate
+    sd = S.SceneData()
+    m = sd.add_material(S.material())
+    br = np.tile(np.float32([[0, 0, 0, 0.1]]), (9, 1))
+    ar = np.tile(np.float32([[0, 1, 0, 0.1]]), (9, 1))
+    sd.add_cones(br, ar, m)
+    sd.cam = S.camera((0, 0.5, 3), (0, 0, -1), width=8, height=8)
+    prod = N.host_build(sd)
+    boxes, first, count, ids, depth = oracle_ffi.Oracle(sd).bvh()
+    assert np.array_equal(prod["count"], count) and count.sum() == 9
+
+
+def test_empty_scene_rejected():
+    sd = S.SceneData()
+    sd.cam = S.camera((0, 0, 1), (0, 0, -1), width=8, height=8)
+    with pytest.raises(N.KhpError) as e:
+        N.host_build(sd)
+    assert e.value.status == N.KHP_EINVAL
+
+
+# ---- generators (deterministic synthetic stand-ins for the .obj/.hair assets) -------------
+def test_hairball_deterministic_and_shaped():
+    a = S.hairball(500, (0, 0, 0), 0.5, seed=7)
+    b = S.hairball(500, (0, 0, 0), 0.5, seed=7)
+    c = S.hairball(500, (0, 0, 0), 0.5, seed=8)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert not np.array_equal(a[0], c[0])
+    pos, rad = a
+    assert pos.shape == (500, 10, 3) and rad.shape == (500, 10)
+    assert np.all(np.isfinite(pos)) and np.all(rad > 0)
+    r = np.linalg.norm(pos[:, 0], axis=1)   # roots 0.003 below the ball surface (Mesh.cpp:115)
+    assert np.allclose(r, 0.5 - 0.003, atol=1e-5)
+    assert np.all(np.diff(rad, axis=1) <= 0)  # tapering
+
+
+def test_icosphere_and_torus_closed_meshes():
+    v, n = S.icosphere(2, (0, 0, 0), 1.0)
+    assert v.shape == (20 * 4 ** 2, 3, 3)
+    assert np.allclose(np.linalg.norm(v.reshape(-1, 3), axis=1), 1.0, atol=1e-5)
+    assert np.allclose(np.linalg.norm(n.reshape(-1, 3), axis=1), 1.0, atol=1e-5)
+    v, n = S.torus(8, 6, (0, 0, 0), 1.0, 0.25)
+    assert v.shape == (8 * 6 * 2, 3, 3)
+    d = np.linalg.norm(v.reshape(-1, 3)[:, [0, 2]], axis=1)
+    assert d.min() > 0.74 and d.max() < 1.26
+
+
+def test_camera_setup_validates():
+    lib = N.load_library()
+    cam = N.Camera()
+    p, up = np.float32([0, 0, 0]), np.float32([0, 1, 0])
+    # look direction zero, or parallel to up: no camera frame
+    for look in (np.float32([0, 0, 0]), np.float32([0, 2, 0])):
+        rc = lib.khp_camera_setup(N.fptr(p), N.fptr(look), N.fptr(up), 0.036, 0.024, 0.0415, 16, 16, cam)
+        assert rc == N.KHP_EINVAL
+    rc = lib.khp_camera_setup(N.fptr(p), N.fptr(np.float32([0, 0, -1])), N.fptr(up), 0.036, 0.024, 0.0415, 0, 16,
+                              cam)
+    assert rc == N.KHP_EINVAL

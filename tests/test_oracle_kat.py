@@ -1,0 +1,316 @@
+"""Known-answer tests that pin the oracle (the CPU restatement under oracle/).
+
+KIRK has no tests or golden vectors of its own, so the oracle is
+pinned here by analytic answers for the primitives and by invariants of the
+integrator; tests/test_golden.py then freezes its outputs as fixtures.
+"""
+import numpy as np
+import pytest
+
+import oracle_ffi
+from ba_pathtracing_fur_amd import native as N
+from ba_pathtracing_fur_amd import scenes as S
+
+FLT_MAX = np.float32(3.4028234663852886e38)
+
+
+def single_cone_scene(base, apex, r0, r1):
+    sd = S.SceneData(name="cone")
+    m = sd.add_material(S.material())
+    sd.add_cones(np.array([[*base, r0]], np.float32), np.array([[*apex, r1]], np.float32), m)
+    sd.cam = S.camera((0, 0, 5), (0, 0, -1), width=8, height=8)
+    return sd
+
+
+def single_tri_scene(a, b, c):
+    sd = S.SceneData(name="tri")
+    m = sd.add_material(S.material())
+    v = np.array([[a, b, c]], np.float32)
+    n = np.broadcast_to(np.float32([0, 0, 1]), (1, 3, 3)).copy()
+    sd.add_triangles(v, n, m)
+    sd.cam = S.camera((0, 0, 5), (0, 0, -1), width=8, height=8)
+    return sd
+
+
+# ---- ray / cone frustum (Cylinder.cpp:73-228) --------------------------------------
+def test_cylinder_front_hit():
+    o = oracle_ffi.Oracle(single_cone_scene((0, 0, 0), (0, 2, 0), 0.5, 0.5))
+    t, obj, uv, _, _ = o.trace_closest([[0, 1, -5]], [[0, 0, 1]])
+    assert obj[0] == 0 and abs(t[0] - 4.5) < 1e-5 and uv[0].tolist() == [0.0, 0.0]
+    assert o.trace_any([[0, 1, -5]], [[0, 0, 1]], [10.0])[0]
+    assert not o.trace_any([[0, 1, -5]], [[0, 0, 1]], [4.4])[0]
+
+
+def test_cone_open_caps_and_height():
+    o = oracle_ffi.Oracle(single_cone_scene((0, 0, 0), (0, 2, 0), 0.5, 0.5))
+    # along the axis: no caps (Cylinder.cpp "open frustum")
+    t, obj, *_ = o.trace_closest([[0, -5, 0]], [[0, 1, 0]])
+    assert obj[0] == -1 and t[0] == FLT_MAX
+    # above the apex plane: v.Q > max_d -> miss
+    t, obj, *_ = o.trace_closest([[0, 3, -5]], [[0, 0, 1]])
+    assert obj[0] == -1
+
+
+def test_cone_from_inside_takes_second_root():
+    o = oracle_ffi.Oracle(single_cone_scene((0, 0, 0), (0, 2, 0), 0.5, 0.5))
+    t, obj, *_ = o.trace_closest([[0, 1, 0]], [[0, 0, 1]])  # t1 = -0.5 < 1e-4 -> t2
+    assert obj[0] == 0 and abs(t[0] - 0.5) < 1e-6
+
+
+def test_cone_radius_interpolates():
+    o = oracle_ffi.Oracle(single_cone_scene((0, 0, 0), (0, 2, 0), 0.5, 0.0))
+    t, obj, *_ = o.trace_closest([[0, 1, -5]], [[0, 0, 1]])  # radius 0.25 at y=1
+    assert obj[0] == 0 and abs(t[0] - 4.75) < 1e-5
+
+
+def test_tilted_cone_matches_analytic():
+    base, apex, r = np.float64([0.1, -0.2, 0.3]), np.float64([0.8, 1.1, -0.4]), 0.2
+    o = oracle_ffi.Oracle(single_cone_scene(base, apex, r, r))
+    rng = np.random.default_rng(3)
+    axis = (apex - base) / np.linalg.norm(apex - base)
+    hits = 0
+    for _ in range(200):
+        orig = rng.uniform(-3, 3, 3)
+        target = base + rng.uniform(0.2, 0.8) * (apex - base) + rng.normal(scale=0.1, size=3)
+        d = target - orig
+        d /= np.linalg.norm(d)
+        t, obj, *_ = o.trace_closest([orig], [d])
+        # analytic infinite cylinder intersection in float64
+        w = orig - base
+        dp = d - np.dot(d, axis) * axis
+        wp = w - np.dot(w, axis) * axis
+        a, b, c = dp @ dp, 2 * dp @ wp, wp @ wp - r * r
+        disc = b * b - 4 * a * c
+        if disc < 0:
+            assert obj[0] == -1
+            continue
+        roots = sorted([(-b - np.sqrt(disc)) / (2 * a), (-b + np.sqrt(disc)) / (2 * a)])
+        good = [x for x in roots if x > 1e-4 and 0 <= np.dot(orig + x * d - base, axis) <= np.linalg.norm(apex - base)]
+        if not good:
+            assert obj[0] == -1
+            continue
+        hits += 1
+        # float32 quadratic (KIRK solves in float) vs float64: ill-conditioned near grazing roots
+        assert obj[0] == 0 and abs(t[0] - good[0]) < 1e-3 * max(1.0, good[0])
+    assert hits > 50
+
+
+# ---- ray / triangle (Triangle.cpp:152-242) -------------------------------------------
+def test_triangle_hit_and_barycentrics():
+    o = oracle_ffi.Oracle(single_tri_scene((0, 0, 0), (1, 0, 0), (0, 1, 0)))
+    t, obj, uv, *_ = o.trace_closest([[0.25, 0.25, 2.0]], [[0, 0, -1]])
+    assert obj[0] == 0 and abs(t[0] - 2.0) < 1e-6
+    # barycentrics refer to the ctor-reordered vertices (longest axis ordering)
+    assert abs(uv[0].sum() - 0.5) < 1e-6 or abs(1 - uv[0].sum() - 0.25) < 1e-6
+
+
+def test_triangle_parallel_and_outside():
+    o = oracle_ffi.Oracle(single_tri_scene((0, 0, 0), (1, 0, 0), (0, 1, 0)))
+    t, obj, *_ = o.trace_closest([[0.2, 0.2, 1.0]], [[1, 0, 0]])   # in-plane: |det| < 1e-7
+    assert obj[0] == -1
+    t, obj, *_ = o.trace_closest([[0.9, 0.9, 1.0]], [[0, 0, -1]])  # u + v > 1
+    assert obj[0] == -1
+    t, obj, *_ = o.trace_closest([[0.2, 0.2, -1.0]], [[0, 0, -1]])  # behind: t < 0
+    assert obj[0] == -1
+
+
+# ---- BVH closest == brute force for triangle soups (CPU_BVH.cpp:51-199) ---------------
+def test_bvh_closest_equals_bruteforce():
+    rng = np.random.default_rng(5)
+    n = 400
+    c = rng.uniform(-1, 1, (n, 1, 3))
+    v = (c + rng.normal(scale=0.15, size=(n, 3, 3))).astype(np.float32)
+    nrm = np.broadcast_to(np.float32([0, 0, 1]), (n, 3, 3)).copy()
+    sd = S.SceneData()
+    sd.add_triangles(v, nrm, sd.add_material(S.material()))
+    sd.cam = S.camera((0, 0, 5), (0, 0, -1), width=8, height=8)
+    o = oracle_ffi.Oracle(sd)
+    orig = rng.uniform(-2, 2, (500, 3)).astype(np.float32)
+    d = rng.normal(size=(500, 3)).astype(np.float32)
+    t, obj, *_ = o.trace_closest(orig, d)
+    dn = d / np.linalg.norm(d, axis=1, keepdims=True)
+    # brute force Moller-Trumbore in float64
+    A, B, C = v[:, 0].astype(np.float64), v[:, 1].astype(np.float64), v[:, 2].astype(np.float64)
+    e1, e2 = B - A, C - A
+    for i in range(len(orig)):
+        p = np.cross(dn[i], e2)
+        det = np.einsum("ij,ij->i", e1, p)
+        ok = np.abs(det) > 1e-9
+        inv = np.where(ok, 1 / np.where(ok, det, 1), 0)
+        s = orig[i] - A
+        u = np.einsum("ij,ij->i", s, p) * inv
+        q = np.cross(s, e1)
+        vv = (q @ dn[i]) * inv
+        tt = np.einsum("ij,ij->i", e2, q) * inv
+        hit = ok & (u >= 0) & (vv >= 0) & (u + vv <= 1) & (tt >= 0)
+        if not hit.any():
+            assert obj[i] == -1
+        else:
+            assert obj[i] >= 0 and abs(t[i] - tt[hit].min()) < 1e-4
+
+
+def test_bvh_structure_invariants():
+    sd = S.config2(32, 24, n_strands=500)
+    boxes, first, count, ids, depth = oracle_ffi.Oracle(sd).bvh()
+    assert sorted(ids.tolist()) == list(range(sd.n_objects))
+    leaves = count > 0
+    assert count[leaves].sum() == sd.n_objects
+    # SAH leaf threshold 1 (CPU_BVH.cpp): leaves of 1 or 2 objects unless centroids coincide
+    assert 1 <= count[leaves].min() and count.max() <= 2
+    assert depth >= int(np.log2(sd.n_objects))
+
+
+# ---- lights (Light.cpp) ---------------------------------------------------------------
+def test_quad_light_vertices_and_hit():
+    sd = S.config1(16, 16)
+    o = oracle_ffi.Oracle(sd)
+    # a camera ray straight up into the ceiling light centre sees the light (t ~= 0.999-0.5)
+    img = o.render(16, 16, 1, 1, threads=1)
+    assert np.isfinite(img).all()
+
+
+def test_environment_only_frame():
+    sd = S.SceneData()
+    sd.add_triangles(*S.quad((100, 100, 100), (101, 100, 100), (101, 101, 100), (100, 101, 100), (0, 0, 1)),
+                     sd.add_material(S.material()))
+    sd.env_color = (0.25, 0.5, 0.75)
+    sd.cam = S.camera((0, 0, 0), (0, 0, -1), width=8, height=8)
+    img = oracle_ffi.Oracle(sd).render(8, 8, 3, 5, threads=1)
+    assert np.array_equal(img, np.broadcast_to(np.float32([0.25, 0.5, 0.75]), img.shape))
+
+
+def test_light_seen_directly_emits_color_over_pi():
+    sd = S.SceneData()
+    sd.add_triangles(*S.quad((-9, -9, -20), (9, -9, -20), (9, 9, -20), (-9, 9, -20), (0, 0, 1)),
+                     sd.add_material(S.material(diffuse=(0, 0, 0))))
+    sd.lights.append(S.quad_light((0, 0, -5), (0, 0, 1), (4, 4), (3.0, 2.0, 1.0), att_const=2.0))
+    sd.env_color = (0, 0, 0)
+    sd.env_ambient = (0, 0, 0)
+    sd.cam = S.camera((0, 0, 0), (0, 0, -1), width=8, height=8)
+    img = oracle_ffi.Oracle(sd).render(8, 8, 1, 1, threads=1)
+    want = np.float32([3, 2, 1]) * np.float32(1 / np.pi) / 2.0   # sampleLightSource: color/pi/const
+    assert np.allclose(img[4, 4], want, rtol=1e-6)
+
+
+# ---- BSDFs (Bsdf.cpp) ---------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def hair_oracle():
+    return oracle_ffi.Oracle(single_cone_scene((0, 0, 0), (0, 1, 0), 0.1, 0.1))
+
+
+def test_lambert_sample(hair_oracle):
+    m = S.material(diffuse=(0.5, 0.25, 1.0))
+    r = hair_oracle.bsdf_sample(0, m, [0, 0, 1], [0, 0, 1], [0.3, 0.7], [0, 0])
+    out = r["out"]
+    assert out[2] > 0 and abs(np.linalg.norm(out) - 1) < 1e-5
+    assert abs(r["pdf"] - abs(out[2]) / np.pi) < 1e-6
+    assert np.allclose(r["f"], np.float32([0.5, 0.25, 1.0]) / np.pi, rtol=1e-6) and r["flags"] == 0
+
+
+def test_specular_reflection(hair_oracle):
+    m = S.material("SpecularReflectionBSDF", specular=(1, 1, 1))
+    i = np.float32([0.6, 0, 0.8])
+    r = hair_oracle.bsdf_sample(0, m, i, [0, 0, 1], [0.5, 0.5], [0, 0])
+    assert np.allclose(r["out"], [-0.6, 0, 0.8], atol=1e-6) and r["pdf"] == 1.0 and r["flags"] & 2
+
+
+def test_glass_normal_incidence(hair_oracle):
+    m = S.material("GlassBSDF", ior=1.5)
+    F = ((1 - 1.5) / (1 + 1.5)) ** 2
+    r = hair_oracle.bsdf_sample(0, m, [0, 0, 1], [0, 0, 1], [0.5, 0.9], [0, 0])   # sample.y > F -> refract
+    assert np.allclose(r["out"], [0, 0, -1], atol=1e-6)
+    assert abs(r["pdf"] - (1 - F)) < 1e-6 and r["flags"] == 3
+    assert np.allclose(r["f"], (1 - F) / 1.5 ** 2, rtol=1e-5)
+    r = hair_oracle.bsdf_sample(0, m, [0, 0, 1], [0, 0, 1], [0.5, 0.01], [0, 0])  # sample.y < F -> reflect
+    assert np.allclose(r["out"], [0, 0, 1], atol=1e-6) and abs(r["pdf"] - F) < 1e-6
+
+
+def test_emission_and_transparent(hair_oracle):
+    r = hair_oracle.bsdf_sample(0, S.material("EmissionBSDF"), [0, 0, 1], [0, 0, 1], [0.5, 0.5], [0, 0])
+    assert r["flags"] == 4 and r["out"].tolist() == [0, 0, 0] and r["f"].tolist() == [1, 1, 1]
+    r = hair_oracle.bsdf_sample(0, S.material("TransparentBSDF"), [0.6, 0, 0.8], [0, 0, 1], [0.5, 0.5], [0, 0])
+    assert np.allclose(r["out"], [-0.6, 0, -0.8]) and r["flags"] == 3
+
+
+def test_grazing_early_exit(hair_oracle):
+    r = hair_oracle.bsdf_sample(0, S.material(), [1, 0, 0], [0, 0, 1], [0.5, 0.5], [0, 0])  # dot == 0
+    assert r["f"].tolist() == [0, 0, 0]
+
+
+def test_marschner_r_lobe(hair_oracle):
+    m = S.fiber_material()
+    i = np.float32([0.3, 0.2, 0.932738])
+    i = i / np.linalg.norm(i)
+    n = np.float32([0, 0, 1])
+    r = hair_oracle.bsdf_sample(0, m, i, n, [0, 0], [0.25, 0.5])
+    assert r["flags"] == 2 and r["pdf"] > 0 and np.all(r["f"] == r["f"][0])
+    # cone frame of an upright cone: v = +y, u = x (cross(v, z)), w = cross(u, v) = z
+    U, Vv, W = np.float64([1, 0, 0]), np.float64([0, 1, 0]), np.float64([0, 0, 1])
+    ic = np.array([i @ Vv, i @ U, i @ W])
+    assert abs(r["sample"][0] - np.arctan2(np.hypot(ic[0], ic[2]), ic[1])) < 1e-6   # sample.x = theta_i
+    # out = R^T reflect(-i, n) with R = rotate(alpha, V), alpha = -(5 + 5*0.25) raw radians
+    a = -(5 + 5 * 0.25)
+    refl = -i + 2 * (i @ n) * n
+    c, s = np.cos(a), np.sin(a)
+    R = np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])   # glm::rotate(alpha, +y)
+    # KIRK writes vec4(d) * M (row vector times matrix) == M^T d  (Bsdf.cpp MarschnerHairBSDF::sample)
+    assert np.allclose(r["out"], R.T @ refl, atol=1e-5)
+    assert not np.allclose(r["out"], R @ refl, atol=1e-3)
+
+
+def test_deon_r_lobe_keeps_sample(hair_oracle):
+    m = S.fiber_material("DEonHairBSDF")
+    r = hair_oracle.bsdf_sample(0, m, [0, 0.6, 0.8], [0, 0, 1], [0.125, 0.5], [0.5, 0.5])
+    assert r["flags"] == 2 and r["sample"][0] == np.float32(0.125)
+
+
+# ---- integrator invariants (CPU_PathTracer.cpp) -----------------------------------------
+def test_progressive_equals_one_shot():
+    sd = S.config2(24, 16, n_strands=300)
+    o = oracle_ffi.Oracle(sd)
+    full = o.render(24, 16, 4, 5, threads=2)
+    part = o.render(24, 16, 2, 5, threads=2)
+    part = o.render(24, 16, 2, 5, first_sample=2, threads=2, out=part)
+    assert np.array_equal(full.view(np.uint32), part.view(np.uint32))
+
+
+def test_tiles_partition_the_frame():
+    sd = S.config1(40, 24)
+    o = oracle_ffi.Oracle(sd)
+    full = o.render(40, 24, 2, 3, threads=2)
+    acc = np.zeros_like(full)
+    for r in range(3):
+        acc = o.render(40, 24, 2, 3, threads=2, tile_size=8, tile_rank=r, tile_nranks=3, out=acc)
+    assert np.array_equal(full.view(np.uint32), acc.view(np.uint32))
+
+
+def test_thread_count_invariance():
+    sd = S.config2(24, 16, n_strands=300)
+    o = oracle_ffi.Oracle(sd)
+    a = o.render(24, 16, 2, 5, threads=1)
+    b = o.render(24, 16, 2, 5, threads=7)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+# ---- host helpers (Camera.cpp, CPU_Scene.cpp) ------------------------------------------------
+def test_camera_apply_parameters():
+    cam = S.camera((0, 0.5, 1.85), (0, 0, -1), (0, 1, 0), 320, 200)
+    pos = np.float64([0, 0.5, 1.85])
+    az = np.float64([0, 0, 1])
+    ax = np.cross([0, 1, 0], az)
+    ay = np.cross(az, ax)
+    fov = 2 * np.arctan(np.hypot(0.036, 0.024) / (2 * 0.0415))
+    sy = np.tan(fov / 2)
+    sx = sy * 320 / 200
+    assert abs(cam.pixel_size - 2 * sx / 320) < 1e-7
+    assert np.allclose(list(cam.bottom_left), pos - az - sy * ay - sx * ax, atol=1e-6)
+
+
+def test_fibers_to_cones_flatten_rule():
+    pos = np.float32([[[0, 0, 0], [0, 1, 0], [0, 2, 0], [0, 3, 0], [0, 4, 0], [0, 5, 0]]])
+    rad = np.float32([[1.0, 0.9, 0.8, 0.7, 0.6, 0.5]])
+    sd = S.SceneData()
+    sd.add_fibers(pos, rad, sd.add_material(S.fiber_material()))
+    b, a = sd.cone_base_r0, sd.cone_apex_r1
+    assert np.allclose(b[0, :3], [0, -0.008, 0]) and np.isclose(b[0, 3], 0.95)      # c <= 3: -5 %
+    assert np.isclose(b[4, 3], 0.6 * 0.9) and np.allclose(a[:, 3], rad[0, 1:])      # c > 3: -10 %
