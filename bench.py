@@ -19,7 +19,8 @@ The JSON line also carries:
                   frame) / its average launch time from HIP events in the
                   timed region, against 8 TB/s HBM;
   cpu_baseline -- the C restatement (oracle/) timed on this host's cores on a
-                  bounded sample of the same frame (1 spp, every k-th row).
+                  bounded sample of the same frame: progressive full-frame
+                  samples 0, 1, ... until --cpu-seconds or the workload's spp.
 """
 from __future__ import annotations
 
@@ -55,7 +56,7 @@ def log(*a):
 
 
 def cpu_baseline(sd, args, budget_s):
-    """Oracle timed on the host cores over a bounded sample (every k-th row, 1 spp)."""
+    """Oracle timed on the host cores over a bounded sample of the same frame."""
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle_ffi  # test infrastructure: only bench's cpu_baseline leg uses it
 
@@ -64,23 +65,26 @@ def cpu_baseline(sd, args, budget_s):
     o = oracle_ffi.Oracle(sd)
     build_s = time.time() - t0
     W, H = args.width, args.height
-    # pilot: 8 rows spread over the frame, sample 0
+    frame = W * H
+    # progressive full frames (sample k of the same seeds) until the budget is spent or the
+    # workload's spp is reached; if one frame alone would blow the budget, every k-th row instead
     step = max(1, H // 8)
     t0 = time.time()
     o.render(W, H, 1, args.depth, threads=threads, rows=(0, H, step))
     pilot = time.time() - t0
-    rate = len(range(0, H, step)) * W / max(pilot, 1e-6)  # samples per second
-    frame = W * H
-    if rate * budget_s >= frame:
-        # whole frames, progressive samples 0..spp_cpu-1 (capped at the workload's spp)
-        spp_cpu = int(max(1, min(args.spp, rate * budget_s // frame)))
+    est_frame_s = pilot * H / len(range(0, H, step))
+    if est_frame_s <= budget_s:
+        out = None
+        spp_cpu = 0
         t0 = time.time()
-        o.render(W, H, spp_cpu, args.depth, threads=threads)
+        while spp_cpu < args.spp and time.time() - t0 < budget_s:
+            out = o.render(W, H, 1, args.depth, first_sample=spp_cpu, threads=threads, out=out)
+            spp_cpu += 1
         dt = time.time() - t0
         samples = frame * spp_cpu
         what = f"full {W}x{H} frame x {spp_cpu} of {args.spp} spp"
     else:
-        n_rows = int(max(1, rate * budget_s // W))
+        n_rows = int(max(1, budget_s / est_frame_s * H))
         step = max(1, H // n_rows)
         rows = len(range(0, H, step))
         t0 = time.time()

@@ -196,3 +196,19 @@ def test_native_library_is_loaded():
     """The frames above came from libkirk_hip.so (no fallback exists); it must be mapped in-process."""
     maps = open("/proc/self/maps").read()
     assert "libkirk_hip.so" in maps
+
+
+def test_cpp_host_program_matches(hip_ctx, tmp_path):
+    """examples/render_hairball (C++ on the C-ABI, no Python) renders the same config-3 frame."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "render_hairball")
+    out = tmp_path / "f.pfm"
+    subprocess.run([exe, "3000", "64", "40", "2", "5", "1", str(out)], check=True, timeout=300)
+    raw = out.read_bytes()
+    hdr_end = raw.index(b"-1.0\n") + 5
+    img = np.frombuffer(raw[hdr_end:], np.float32).reshape(40, 64, 3)
+    sd = S.config3(64, 40, n_strands=3000)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    want = hip_ctx.render(64, 40, 2, 5)
+    assert np.array_equal(img.view(np.uint32), want.view(np.uint32))

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 passes for bench.py (run on the GPU box via gpurun, from the repo root).
-# usage: tools/profile.sh <tag> [pass...]   passes: trace fetch write sq list
+# usage: tools/profile.sh <tag> [pass...]   passes: trace fetch write sq lat ea tcc list
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}; shift || true
@@ -15,8 +15,10 @@ for p in $PASSES; do
     trace) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B --steps 3 --warmup 1 > $OUT/trace_bench.json 2> $OUT/trace_bench.log ;;
     fetch) timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/fetch -o run -- $B --steps 1 --warmup 0 > $OUT/fetch_bench.json 2> $OUT/fetch_bench.log ;;
     write) timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/write -o run -- $B --steps 1 --warmup 0 > $OUT/write_bench.json 2> $OUT/write_bench.log ;;
-    sq)    timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_SALU --kernel-include-regex 'k_extend' --output-format csv -d $OUT/sq -o run -- $B --steps 1 --warmup 0 > $OUT/sq_bench.json 2> $OUT/sq_bench.log ;;
-    tcc)   timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex 'k_extend' --output-format csv -d $OUT/tcc -o run -- $B --steps 1 --warmup 0 > $OUT/tcc_bench.json 2> $OUT/tcc_bench.log ;;
+    sq)    timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_SALU --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/sq -o run -- $B --steps 1 --warmup 0 > $OUT/sq_bench.json 2> $OUT/sq_bench.log ;;
+    lat)   timeout -k 10 600 rocprofv3 --pmc VmemLatency --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/lat -o run -- $B --steps 1 --warmup 0 > $OUT/lat_bench.json 2> $OUT/lat_bench.log ;;
+    ea)    timeout -k 10 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/ea -o run -- $B --steps 1 --warmup 0 > $OUT/ea_bench.json 2> $OUT/ea_bench.log ;;
+    tcc)   timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tcc -o run -- $B --steps 1 --warmup 0 > $OUT/tcc_bench.json 2> $OUT/tcc_bench.log ;;
   esac
 done
 echo "profile passes done: $PASSES"
