@@ -49,6 +49,7 @@ struct Wave {
     float* C[3];
     int32_t* flags;
     uint32_t* key;
+    uint8_t* vis;        // shadow-ray occlusion flag per shadow record
     float4* sh;          // 6 float4 per shadow record
     Counters* cnt;
     const uint32_t* pix;  // owned pixel ids (y*W+x)
@@ -131,6 +132,9 @@ __global__ void k_prep(Counters* c, int cur) {
 #ifndef KHP_TRAV_WAVES
 #define KHP_TRAV_WAVES 5   // 96 VGPRs, no scratch; measured best (4: -9 %, 6: spills)
 #endif
+#ifndef KHP_SH_WAVES
+#define KHP_SH_WAVES KHP_TRAV_WAVES
+#endif
 constexpr int RING = KHP_RING;      // LDS ring entries per lane (3 x 4 B each)
 constexpr int REFILL = KHP_REFILL;  // refill when >= REFILL lanes are idle
 constexpr size_t LDS_BYTES = 3 * RING * 256 * sizeof(uint32_t);
@@ -151,6 +155,41 @@ __device__ __forceinline__ uint32_t claim(unsigned long long idle, uint32_t* fet
 }
 
 // ---- extend: closest hit for every queued ray ------------------------------------------
+#ifndef KHP_WW
+#define KHP_WW 0   // 1: while-while phases (measured 35 % slower: waves wait for the longest interior run); 0: if-if
+#endif
+#ifndef KHP_ONEFETCH
+#define KHP_ONEFETCH 1   // one record fetch per lane per iteration (nodes and candidates alike)
+#endif
+#ifndef KHP_WW_EXT
+#define KHP_WW_EXT KHP_WW
+#endif
+#ifndef KHP_WW_SH
+#define KHP_WW_SH KHP_WW
+#endif
+
+// One traversal round of a wave.  KHP_WW: every lane with an interior entry
+// keeps descending until its entry is a leaf (or it runs out), then all lanes
+// holding a leaf test it together.  A lane never moves past its own leaf
+// before testing it, so each ray's visit order -- and therefore its result --
+// is exactly KIRK's; only the interleaving of lanes changes.
+template <bool STATS, bool WW, class LeafFn, class Stack>
+__device__ __forceinline__ void trav_round(const DevScene& S, const TravRay& tr, float tlimit_in, bool has, Stack& stk,
+                                           Cur& c, TravStats& st, LeafFn leaf, const float* tlimit_live) {
+    if (!has) return;
+    if (WW) {
+        // per-lane loop: the wave keeps issuing interior steps until every lane
+        // holds a leaf (or is done).  NB: a ballot-controlled form of this loop
+        // (exit when __ballot(interior) == 0) was measured to corrupt other
+        // lanes' traversal state on gfx950 / ROCm 7.2; keep the plain while.
+        while (cur_interior(c)) interior_step<STATS>(S, tr, *tlimit_live, stk, c, st);
+        if (cur_leaf(c)) leaf();
+    } else if (c.valid) {
+        if (ref_leaf(c.ref)) leaf();
+        else interior_step<STATS>(S, tr, *tlimit_live, stk, c, st);
+    }
+}
+
 template <bool STATS>
 __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
@@ -160,6 +199,8 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
     TravStats st{0, 0};
     TravRay tr;
     Hit h;
+    Cur c{0u, 0.0f, 0.0f, false};
+    LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
     bool has = false, exhausted = false;
     uint32_t idx = 0;
     for (;;) {
@@ -177,7 +218,8 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
                 h.t = FLT_MAX_;
                 h.slot = -1;
                 h.u = h.v = 0.0f;
-                has = trav_begin(S, tr, stk);
+                lf.left = 0;
+                has = trav_begin(S, tr, stk, c);
                 if (!has) {  // missed the root box
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = -1;
@@ -192,16 +234,27 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
             continue;
         }
         for (;;) {
-            if (has) {
-                closest_step<STATS>(S, tr, h, stk, st);
-                if (stk.empty()) {
-                    Wv.ht[idx] = h.t;
-                    Wv.hslot[idx] = h.slot;
-                    Wv.hu[idx] = h.u;
-                    Wv.hv[idx] = h.v;
-                    has = false;
-                }
+#if KHP_ONEFETCH
+            const bool work = has && resolve<STATS>(S, h.t, stk, c, lf, st);
+            if (has && !work) {
+                Wv.ht[idx] = h.t;
+                Wv.hslot[idx] = h.slot;
+                Wv.hu[idx] = h.u;
+                Wv.hv[idx] = h.v;
+                has = false;
             }
+            if (work) step1_closest<STATS>(S, tr, h, stk, c, lf, st);
+#else
+            trav_round<STATS, KHP_WW_EXT>(S, tr, h.t, has, stk, c, st,
+                              [&] { leaf_step_closest<STATS>(S, tr, h, stk, c, st); }, &h.t);
+            if (has && !c.valid) {
+                Wv.ht[idx] = h.t;
+                Wv.hslot[idx] = h.slot;
+                Wv.hu[idx] = h.u;
+                Wv.hv[idx] = h.v;
+                has = false;
+            }
+#endif
             act = __ballot(has);
             if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
@@ -399,45 +452,55 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
     }
 }
 
-// ---- shadow: BVH::isIntersection + light occlusion loop, then colour += acc ------------
-// finish one shadow record: light occlusion loop + deferred colour add
-__device__ __forceinline__ void shadow_finish(const DevScene& S, const Wave& Wv, uint32_t i, const TravRay& tr,
-                                              float tmax, bool occ) {
-    const float4* rec = Wv.sh + 6 * (size_t)i;
-    float4 b = rec[1], c = rec[2], d = rec[3], e = rec[4];
-    uint32_t pid = bits_from_f(b.w);
-    const Ray& r = tr.r;
-    if (!occ) {
-        for (int li = 0; li < S.n_lights; ++li) {
-            float t;
-            if (light_isect(S.lights[li], r, t) && (t < tmax)) {
-                occ = true;
-                break;
+// ---- shadow: BVH::isIntersection (k_shadow), then the light occlusion loop and
+//      the deferred colour add (k_shadow_finish, SimpleShader.h:131-148) ---------------
+// k_shadow_finish: one shadow record per lane, streaming; kept out of the
+// traversal kernel so k_shadow's registers go to traversal only.
+__global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
+    const uint32_t n = Wv.cnt->nsh;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4* rec = Wv.sh + 6 * (size_t)i;
+        float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3], e = rec[4];
+        uint32_t pid = bits_from_f(b.w);
+        Ray r;
+        r.o = mk(a.x, a.y, a.z);
+        r.d = mk(b.x, b.y, b.z);
+        const float tmax = a.w;
+        bool occ = Wv.vis[i] != 0;
+        if (!occ) {
+            for (int li = 0; li < S.n_lights; ++li) {
+                float t;
+                if (light_isect(S.lights[li], r, t) && (t < tmax)) {
+                    occ = true;
+                    break;
+                }
             }
         }
+        v3 lc = mk(c.x, c.y, c.z) * (occ ? 0.0f : 1.0f);
+        v3 dl = mk(0, 0, 0) + lc;
+        v3 acc = (mk(0, 0, 0) + dl * mk(d.x, d.y, d.z)) + mk(e.x, e.y, e.z);
+        if (c.w != 0.0f) {
+            float4 f = rec[5];
+            acc = acc + mk(f.x, f.y, f.z);
+        }
+        Wv.C[0][pid] = Wv.C[0][pid] + acc.x;
+        Wv.C[1][pid] = Wv.C[1][pid] + acc.y;
+        Wv.C[2][pid] = Wv.C[2][pid] + acc.z;
     }
-    v3 lc = mk(c.x, c.y, c.z) * (occ ? 0.0f : 1.0f);
-    v3 dl = mk(0, 0, 0) + lc;
-    v3 acc = (mk(0, 0, 0) + dl * mk(d.x, d.y, d.z)) + mk(e.x, e.y, e.z);
-    if (c.w != 0.0f) {
-        float4 f = rec[5];
-        acc = acc + mk(f.x, f.y, f.z);
-    }
-    Wv.C[0][pid] = Wv.C[0][pid] + acc.x;
-    Wv.C[1][pid] = Wv.C[1][pid] + acc.y;
-    Wv.C[2][pid] = Wv.C[2][pid] + acc.z;
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
+__global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = Wv.cnt->nsh;
     LdsStack<RING, STATS> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0};
     TravRay tr;
+    Cur c{0u, 0.0f, 0.0f, false};
+    LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
     float tmax = 0.0f;
-    bool has = false, exhausted = false;
+    bool has = false, exhausted = false, found = false;
     uint32_t idx = 0;
     for (;;) {
         unsigned long long idle = __ballot(!has);
@@ -454,8 +517,10 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_shadow(DevScene S, Wave
                 r.d = mk(b.x, b.y, b.z);
                 tmax = a.w;
                 trav_setup(tr, r);
-                has = trav_begin(S, tr, stk);
-                if (!has) shadow_finish(S, Wv, idx, tr, tmax, false);
+                found = false;
+                lf.left = 0;
+                has = trav_begin(S, tr, stk, c);
+                if (!has) Wv.vis[idx] = 0;
             }
         }
         unsigned long long act = __ballot(has);
@@ -464,13 +529,24 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_shadow(DevScene S, Wave
             continue;
         }
         for (;;) {
-            if (has) {
-                bool found = any_step<STATS>(S, tr, tmax, stk, st);
-                if (found || stk.empty()) {
-                    shadow_finish(S, Wv, idx, tr, tmax, found);
-                    has = false;
-                }
+#if KHP_ONEFETCH
+            const bool work = has && resolve<STATS>(S, tmax, stk, c, lf, st);
+            if (has && !work) {
+                Wv.vis[idx] = 0;
+                has = false;
             }
+            if (work && step1_any<STATS>(S, tr, tmax, stk, c, lf, st)) {
+                Wv.vis[idx] = 1;
+                has = false;
+            }
+#else
+            trav_round<STATS, KHP_WW_SH>(S, tr, tmax, has, stk, c, st,
+                              [&] { found = leaf_step_any<STATS>(S, tr, tmax, stk, c, st); }, &tmax);
+            if (has && (found || !c.valid)) {
+                Wv.vis[idx] = found ? 1 : 0;
+                has = false;
+            }
+#endif
             act = __ballot(has);
             if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
@@ -618,7 +694,7 @@ struct khp_ctx {
     DevScene S{};
     // wavefront
     size_t cap = 0;
-    DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb, cnt, spill;
+    DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb, visb, cnt, spill;
     // framebuffer + pixel list
     DevMem fb, pix, stage, stage_pix;
     uint32_t fbW = 0, fbH = 0;
@@ -710,8 +786,8 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     c->st.build_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (c->hs.depth + 1 > (uint32_t)STACK_MAX)
         return fail(KHP_EUNSUPPORTED, "BVH deeper than the traversal stack (" + std::to_string(c->hs.depth) + ")");
-    if (c->hs.n_obj >= MAX_SLOTS)
-        return fail(KHP_EUNSUPPORTED, "more than 2^24 objects do not fit the packed leaf reference");
+    if (c->hs.n_slots >= MAX_SLOTS)
+        return fail(KHP_EUNSUPPORTED, "more than 2^24 primitive slots do not fit the packed leaf reference");
     HostScene& hs = c->hs;
     HIPCHK(upload(c->prims, hs.slot_rec.data(), hs.slot_rec.size(), c->stream));
     HIPCHK(upload(c->aux, hs.slot_aux.data(), hs.slot_aux.size(), c->stream));
@@ -772,6 +848,7 @@ static khp_status ensure_wave(khp_ctx* c, size_t cap) {
     }
     HIPCHK(c->flagsb.ensure(cap * 4));
     HIPCHK(c->keyb.ensure(cap * 4));
+    HIPCHK(c->visb.ensure(cap));
     HIPCHK(c->shb.ensure(cap * 6 * sizeof(float4)));
     HIPCHK(c->cnt.ensure(sizeof(Counters)));
     // traversal-stack spill columns: one per resident lane, STACK_MAX entries deep
@@ -779,6 +856,32 @@ static khp_status ensure_wave(khp_ctx* c, size_t cap) {
     HIPCHK(c->spill.ensure(lanes * STACK_MAX * sizeof(int4)));
     c->cap = cap;
     return KHP_OK;
+}
+
+// Device pointers of the wavefront state (sized by ensure_wave).
+static Wave wave_view(khp_ctx* c) {
+    Wave Wv{};
+    for (int q = 0; q < 2; ++q) {
+        for (int k = 0; k < 3; ++k) {
+            Wv.qo[q][k] = c->qbuf[q][k].as<float>();
+            Wv.qd[q][k] = c->qbuf[q][3 + k].as<float>();
+        }
+        Wv.qpid[q] = c->qbuf[q][6].as<uint32_t>();
+    }
+    Wv.ht = c->ht.as<float>();
+    Wv.hslot = c->hslot.as<int32_t>();
+    Wv.hu = c->hu.as<float>();
+    Wv.hv = c->hv.as<float>();
+    for (int k = 0; k < 3; ++k) {
+        Wv.T[k] = c->Tb[k].as<float>();
+        Wv.C[k] = c->Cb[k].as<float>();
+    }
+    Wv.flags = c->flagsb.as<int32_t>();
+    Wv.key = c->keyb.as<uint32_t>();
+    Wv.vis = c->visb.as<uint8_t>();
+    Wv.sh = c->shb.as<float4>();
+    Wv.cnt = c->cnt.as<Counters>();
+    return Wv;
 }
 
 static void owned_pixels(uint32_t W, uint32_t H, uint32_t T, uint32_t rank, uint32_t nranks,
@@ -854,26 +957,7 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     const bool stats = (c->flags & KHP_CTX_STATS) != 0 || (p->flags & KHP_RENDER_STATS) != 0;
     c->launches.clear();
     c->ev_next = 0;
-    Wave Wv{};
-    for (int q = 0; q < 2; ++q) {
-        for (int k = 0; k < 3; ++k) {
-            Wv.qo[q][k] = c->qbuf[q][k].as<float>();
-            Wv.qd[q][k] = c->qbuf[q][3 + k].as<float>();
-        }
-        Wv.qpid[q] = c->qbuf[q][6].as<uint32_t>();
-    }
-    Wv.ht = c->ht.as<float>();
-    Wv.hslot = c->hslot.as<int32_t>();
-    Wv.hu = c->hu.as<float>();
-    Wv.hv = c->hv.as<float>();
-    for (int k = 0; k < 3; ++k) {
-        Wv.T[k] = c->Tb[k].as<float>();
-        Wv.C[k] = c->Cb[k].as<float>();
-    }
-    Wv.flags = c->flagsb.as<int32_t>();
-    Wv.key = c->keyb.as<uint32_t>();
-    Wv.sh = c->shb.as<float4>();
-    Wv.cnt = c->cnt.as<Counters>();
+    Wave Wv = wave_view(c);
     Wv.pix = c->pix.as<uint32_t>();
     Wv.W = p->width;
     Wv.H = p->height;
@@ -912,6 +996,9 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
                     hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp_sh);
                 else
                     hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp_sh);
+                timed(c, 2, false);
+                timed(c, 2, true);   // shadow stage = any-hit traversal + finish
+                hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, c->stream, c->S, Wv);
                 timed(c, 2, false);
             }
             hipLaunchKernelGGL(k_tail, dim3(1), dim3(1), 0, c->stream, Wv.cnt);
@@ -964,12 +1051,96 @@ extern "C" khp_status khp_read_framebuffer(khp_ctx* c, float* out_rgb) {
     return KHP_OK;
 }
 
+// ---- batch queries through the persistent wavefront kernels (test hook) -------------
+// KHP_TRACE_PERSISTENT=1 routes khp_trace_closest / khp_trace_any through k_extend /
+// k_shadow -- the kernels the renderer uses -- instead of the one-ray-per-thread
+// kernels, so tests can check the production traversal ray by ray.
+__global__ void k_load_rays(uint32_t n, const float* orig, const float* dir, Wave Wv, int as_shadow,
+                            const float* tmax) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        Wv.cnt->nq[0] = as_shadow ? 0u : n;
+        Wv.cnt->nsh = as_shadow ? n : 0u;
+    }
+    if (i >= n) return;
+    Ray r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
+    if (as_shadow) {
+        Wv.sh[6 * (size_t)i] = make_float4(r.o.x, r.o.y, r.o.z, tmax[i]);
+        Wv.sh[6 * (size_t)i + 1] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
+    } else {
+        Wv.qo[0][0][i] = r.o.x; Wv.qo[0][1][i] = r.o.y; Wv.qo[0][2][i] = r.o.z;
+        Wv.qd[0][0][i] = r.d.x; Wv.qd[0][1][i] = r.d.y; Wv.qd[0][2][i] = r.d.z;
+    }
+}
+
+__global__ void k_store_hits(DevScene S, uint32_t n, Wave Wv, float* t, int32_t* obj, float* uv) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t sl = Wv.hslot[i];
+    t[i] = Wv.ht[i];
+    obj[i] = sl >= 0 ? (int32_t)S.aux[sl].obj : -1;
+    uv[2 * i] = Wv.hu[i];
+    uv[2 * i + 1] = Wv.hv[i];
+}
+
+// 0: one-ray-per-thread kernels; 1: instrumented persistent kernels (KIRK's
+// plain BVH2 steps, visit counts); 2: production persistent kernels (paired).
+static int trace_persistent() {
+    const char* e = getenv("KHP_TRACE_PERSISTENT");
+    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+}
+
+static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig, const float* dir,
+                                       const float* tmax_h, float* t_out, int32_t* obj_out, float* uv_out,
+                                       uint8_t* hit_out) {
+    const bool shadow = hit_out != nullptr;
+    khp_status s = ensure_wave(c, n);
+    if (s != KHP_OK) return s;
+    DevMem o, d, tm, t, ob, uv;
+    HIPCHK(upload(o, orig, 3 * (size_t)n, c->stream));
+    HIPCHK(upload(d, dir, 3 * (size_t)n, c->stream));
+    if (shadow) HIPCHK(upload(tm, tmax_h, (size_t)n, c->stream));
+    HIPCHK(hipMemsetAsync(c->cnt.p, 0, sizeof(Counters), c->stream));
+    Wave Wv = wave_view(c);
+    hipLaunchKernelGGL(k_load_rays, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, o.as<float>(), d.as<float>(),
+                       Wv, shadow ? 1 : 0, tm.as<float>());
+    const bool prod = trace_persistent() == 2;
+    if (shadow) {
+        SpillArea sp{c->spill.as<int4>(), (uint32_t)c->grid_sh * 256u};
+        if (prod) hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp);
+        else hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(hit_out, Wv.vis, n, hipMemcpyDeviceToHost, c->stream));
+    } else {
+        SpillArea sp{c->spill.as<int4>(), (uint32_t)c->grid_ext * 256u};
+        if (prod) hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(256), LDS_BYTES, c->stream, c->S, Wv, 0, sp);
+        else hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(256), LDS_BYTES, c->stream, c->S, Wv, 0, sp);
+        HIPCHK(t.ensure(4 * (size_t)n));
+        HIPCHK(ob.ensure(4 * (size_t)n));
+        HIPCHK(uv.ensure(8 * (size_t)n));
+        hipLaunchKernelGGL(k_store_hits, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->S, n, Wv, t.as<float>(),
+                           ob.as<int32_t>(), uv.as<float>());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(t_out, t.p, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(obj_out, ob.p, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        if (uv_out) HIPCHK(hipMemcpyAsync(uv_out, uv.p, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    }
+    Counters hc;
+    HIPCHK(hipMemcpyAsync(&hc, c->cnt.p, sizeof(hc), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->st.node_visits = shadow ? hc.sh_node_visits : hc.node_visits;
+    c->st.prim_tests = shadow ? hc.sh_prim_tests : hc.prim_tests;
+    c->st.stack_spills = hc.spills;
+    return KHP_OK;
+}
+
 extern "C" khp_status khp_trace_closest(khp_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out,
                                         int32_t* obj_out, float* uv_out) {
     if (!c || (n && (!orig || !dir || !t_out || !obj_out))) return fail(KHP_EINVAL, "null argument");
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
     if (n == 0) return KHP_OK;
     HIPCHK(hipSetDevice(c->device));
+    if (trace_persistent()) return trace_persistent_run(c, n, orig, dir, nullptr, t_out, obj_out, uv_out, nullptr);
     DevMem o, d, t, ob, uv, stb;
     HIPCHK(upload(o, orig, 3 * (size_t)n, c->stream));
     HIPCHK(upload(d, dir, 3 * (size_t)n, c->stream));
@@ -999,6 +1170,7 @@ extern "C" khp_status khp_trace_any(khp_ctx* c, uint32_t n, const float* orig, c
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
     if (n == 0) return KHP_OK;
     HIPCHK(hipSetDevice(c->device));
+    if (trace_persistent()) return trace_persistent_run(c, n, orig, dir, tmax, nullptr, nullptr, nullptr, hit_out);
     DevMem o, d, tm, h;
     HIPCHK(upload(o, orig, 3 * (size_t)n, c->stream));
     HIPCHK(upload(d, dir, 3 * (size_t)n, c->stream));

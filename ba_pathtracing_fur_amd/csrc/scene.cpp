@@ -389,27 +389,57 @@ void build_bvh(HostScene& hs, int n_threads) {
 }
 
 void make_device_layout(HostScene& hs) {
-    // interior index per preorder node
-    std::vector<int32_t> inner(hs.nodes.size(), -1);
-    int32_t ni = 0;
-    for (size_t i = 0; i < hs.nodes.size(); ++i)
-        if (hs.nodes[i].count == 0) inner[i] = ni++;
-    hs.dnodes.assign((size_t)ni, DevNode{});
+    // Interior records: the two children of a node, when both are interior, get
+    // the records (2k, 2k+1) of one 128-B line, so the traversal can expand a
+    // far sibling from the line it fetched for the near one.  A lone interior
+    // child takes a whole pair (even index).  The root sits alone in pair 0.
+    const size_t nn = hs.nodes.size();
+    std::vector<int32_t> rec_of(nn, -1);
+    int32_t next = 0;
+    if (hs.nodes[0].count == 0) {
+        rec_of[0] = 0;
+        next = 2;
+        std::vector<int32_t> st{0};
+        while (!st.empty()) {
+            int32_t i = st.back();
+            st.pop_back();
+            const BuildNode& n = hs.nodes[i];
+            const bool li = hs.nodes[n.left].count == 0, ri = hs.nodes[n.right].count == 0;
+            if (li) rec_of[n.left] = next;
+            if (ri) rec_of[n.right] = li ? next + 1 : next;
+            if (li || ri) next += 2;
+            if (ri) st.push_back(n.right);
+            if (li) st.push_back(n.left);  // left subtree first: DFS preorder of pairs
+        }
+    }
+    hs.dnodes.assign((size_t)next, DevNode{});
+    // Leaf slots: a leaf with >= 2 candidates starts at an even slot so its
+    // first two 64-B records share one line (pad slots are never referenced).
+    std::vector<uint32_t> slot_of_first(hs.n_obj + 1, 0);
+    uint32_t ns = 0;
+    for (size_t i = 0; i < nn; ++i) {  // preorder visits leaves in ids order
+        const BuildNode& n = hs.nodes[i];
+        if (n.count == 0) continue;
+        if (n.count >= 2 && (ns & 1u)) ++ns;
+        slot_of_first[n.first] = ns;
+        ns += (uint32_t)n.count;
+    }
+    hs.n_slots = ns;
     auto child_ref = [&](int32_t c, int32_t& ref, int32_t& cnt) {
         const BuildNode& n = hs.nodes[c];
         if (n.count > 0) {
             uint32_t ce = (uint32_t)n.count < LEAF_CNT_ESC ? (uint32_t)n.count : LEAF_CNT_ESC;
-            ref = (int32_t)(LEAF_BIT | (ce << 24) | (uint32_t)n.first);
+            ref = (int32_t)(LEAF_BIT | (ce << 24) | slot_of_first[n.first]);
             cnt = n.count;
         } else {
-            ref = inner[c];
+            ref = rec_of[c];
             cnt = 0;
         }
     };
-    for (size_t i = 0; i < hs.nodes.size(); ++i) {
+    for (size_t i = 0; i < nn; ++i) {
         const BuildNode& n = hs.nodes[i];
         if (n.count != 0) continue;
-        DevNode& d = hs.dnodes[inner[i]];
+        DevNode& d = hs.dnodes[rec_of[i]];
         const BuildNode& L = hs.nodes[n.left];
         const BuildNode& R = hs.nodes[n.right];
         float a[4] = {L.mn.x, L.mn.y, L.mn.z, L.mx.x};
@@ -425,15 +455,19 @@ void make_device_layout(HostScene& hs) {
     const BuildNode& r = hs.nodes[0];
     float rb[6] = {r.mn.x, r.mn.y, r.mn.z, r.mx.x, r.mx.y, r.mx.z};
     memcpy(hs.root_box, rb, sizeof(rb));
-    hs.slot_rec.resize(16 * (size_t)hs.n_obj);
-    hs.slot_aux.resize(hs.n_obj);
-    for (uint32_t s = 0; s < hs.n_obj; ++s) {
-        uint32_t o = hs.ids[s];
-        memcpy(&hs.slot_rec[16 * (size_t)s], &hs.rec[16 * (size_t)o], 16 * sizeof(float));
-        hs.slot_aux[s] = hs.aux[o];
+    hs.slot_rec.assign(16 * (size_t)ns, 0.0f);
+    hs.slot_aux.assign(ns, Aux{0.0f, 0u, 0u, 0u});
+    for (size_t i = 0; i < nn; ++i) {
+        const BuildNode& n = hs.nodes[i];
+        if (n.count == 0) continue;
+        const uint32_t s0 = slot_of_first[n.first];
+        for (int32_t k = 0; k < n.count; ++k) {
+            const uint32_t o = hs.ids[(size_t)n.first + k], sl = s0 + (uint32_t)k;
+            memcpy(&hs.slot_rec[16 * (size_t)sl], &hs.rec[16 * (size_t)o], 16 * sizeof(float));
+            hs.slot_aux[sl] = hs.aux[o];
+        }
+        hs.slot_aux[s0].flags |= (uint32_t)n.count << 8;
     }
-    for (const BuildNode& n : hs.nodes)
-        if (n.count > 0) hs.slot_aux[n.first].flags |= (uint32_t)n.count << 8;
 }
 
 }  // namespace khp

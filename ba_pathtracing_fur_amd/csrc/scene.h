@@ -74,6 +74,7 @@ struct HostScene {
     std::vector<DevNode> dnodes;   // interior nodes
     std::vector<float> slot_rec;   // n_obj * 16, slot order
     std::vector<Aux> slot_aux;     // slot order
+    uint32_t n_slots = 0;          // >= n_obj: 2-candidate leaves start at even slots
     int32_t root_ref = 0, root_cnt = 0;   // root_ref packed
     float root_box[6] = {0, 0, 0, 0, 0, 0};
 };

@@ -114,16 +114,64 @@ struct LdsStack {
     }
 };
 
-// Root box test (BVH::closestIntersection / isIntersection pre-test) and push.
+#ifndef KHP_PIN
+#define KHP_PIN 0   // 1: force whole-record loads (measured 10 % slower: the split lets lanes that fail an early-out skip the late fields)
+#endif
+// Materialise a fetched record in registers at this point.  Without it the
+// compiler splits a 64-B record fetch and sinks the loads of the fields a test
+// needs late (z planes, the cone's W / max_d) below the test's early-out
+// branches, which turns one memory round trip per record into two or three
+// dependent ones (seen in the gfx950 ISA).
+__device__ __forceinline__ void pin(float4& v) {
+#if KHP_PIN
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+#endif
+}
+__device__ __forceinline__ void pin(int4& v) {
+#if KHP_PIN
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+#endif
+}
+
+#ifndef KHP_LEAF_PAIR
+#define KHP_LEAF_PAIR 0   // 1: fetch a leaf's first two records together (spills at 96 VGPRs)
+#endif
+
+// The entry a lane processes next lives in registers (Cur); the stack holds
+// only the deferred far children.  When both children of a node are hit,
+// KIRK's recursion descends into the nearer one first: here it becomes `cur`
+// directly and the farther one is pushed -- the same visit order as
+// push(far), push(near), pop() without the LDS round trip.
+struct Cur {
+    uint32_t ref;
+    float t0, t1;
+    bool valid;
+};
+
 template <class Stack>
-__device__ __forceinline__ bool trav_begin(const DevScene& S, const TravRay& tr, Stack& stk) {
+__device__ __forceinline__ void cur_next(Stack& stk, Cur& c) {
+    if (stk.empty()) {
+        c.valid = false;
+    } else {
+        stk.pop(c.ref, c.t0, c.t1);
+        c.valid = true;
+    }
+}
+
+__device__ __forceinline__ bool cur_interior(const Cur& c) { return c.valid && !ref_leaf(c.ref); }
+__device__ __forceinline__ bool cur_leaf(const Cur& c) { return c.valid && ref_leaf(c.ref); }
+
+// Root box test (BVH::closestIntersection / isIntersection pre-test).
+template <class Stack>
+__device__ __forceinline__ bool trav_begin(const DevScene& S, const TravRay& tr, Stack& stk, Cur& c) {
     stk.clear();
     float t0, t1;
-    if (!slab(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4], S.root_box[5], tr.r, tr.inv,
-              t0, t1))
-        return false;
-    stk.push((uint32_t)S.root_ref, t0, t1);
-    return true;
+    c.valid = slab(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4], S.root_box[5], tr.r,
+                   tr.inv, t0, t1);
+    c.ref = (uint32_t)S.root_ref;
+    c.t0 = t0;
+    c.t1 = t1;
+    return c.valid;
 }
 
 __device__ __forceinline__ uint32_t leaf_count(const DevScene& S, uint32_t ref) {
@@ -132,15 +180,17 @@ __device__ __forceinline__ uint32_t leaf_count(const DevScene& S, uint32_t ref) 
     return c;
 }
 
-// Push the children of an interior node in KIRK's order (near child popped first).
+#ifndef KHP_PAIR
+#define KHP_PAIR 0   // 1: expand an interior far sibling from the near child's 128-B line (exact; measured 10 % slower)
+#endif
+// Cursor-only flag: the entry on top of the stack is this node's interior
+// sibling, whose record shares this node's 128-B line (records 2k, 2k+1).
+constexpr uint32_t SIB_BIT = 0x40000000u;
+
+// Push the two children of one record in KIRK's order (near popped first).
 template <class Stack>
-__device__ __forceinline__ void visit_interior(const DevScene& S, const TravRay& tr, uint32_t ref, Stack& stk) {
-    const float4* np = reinterpret_cast<const float4*>(S.nodes + ref);
-    float4 a = np[0], b = np[1], c = np[2];
-    int4 rf = reinterpret_cast<const int4*>(np)[3];
-    float l0, l1, r0, r1;
-    bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, l0, l1);
-    bool rh = slab(b.z, b.w, c.x, c.y, c.z, c.w, tr.r, tr.inv, r0, r1);
+__device__ __forceinline__ void push_children(Stack& stk, bool lh, bool rh, float l0, float l1, float r0, float r1,
+                                              int4 rf) {
     if (lh && rh) {
         if (l0 < r0) {
             stk.push((uint32_t)rf.y, r0, r1);
@@ -156,35 +206,124 @@ __device__ __forceinline__ void visit_interior(const DevScene& S, const TravRay&
     }
 }
 
-// One closest-hit step: pop one entry and process it.
+// Interior entry: prune test (BVHNode::traverse, CPU_BVH.cpp:151-153) at the
+// moment KIRK would pop it, then both child boxes, near child first.
+// tlimit = current closest t (closest hit) or the ray's tMax (any hit).
+//
+// PAIR: if the cursor carries SIB_BIT, the sibling's record is read from the
+// same line and the sibling's stack entry is replaced by the sibling's two
+// children (far, then near).  KIRK would pop the sibling later, test its
+// prune condition, and continue with its near child: popping the near child
+// at that same moment tests the near child's own interval instead, which
+// prunes whenever the sibling's would -- a child box lies inside its parent
+// box (boxes are unions), and the slab entry/exit distances are monotone in
+// the box under IEEE rounding.  So the visit order and every result are
+// unchanged; only the sibling's own pop and its line fetch disappear.
+// The instrumented kernels (STATS) keep plain BVH2 steps so node-visit counts
+// stay KIRK's.
 template <bool STATS, class Stack>
-__device__ __forceinline__ void closest_step(const DevScene& S, const TravRay& tr, Hit& h, Stack& stk,
-                                             TravStats& st) {
-    uint32_t ref;
-    float tmin, tmax;
-    stk.pop(ref, tmin, tmax);
-    if (tmax < 0.0f || tmin > h.t) return;
+__device__ __forceinline__ void interior_step(const DevScene& S, const TravRay& tr, float tlimit, Stack& stk, Cur& c,
+                                              TravStats& st) {
+    if (c.t1 < 0.0f || c.t0 > tlimit) {
+        cur_next(stk, c);
+        return;
+    }
     if (STATS) st.nodes++;
-    if (ref_leaf(ref)) {
-        const uint32_t first = ref & 0x00FFFFFFu, cnt = leaf_count(S, ref);
-        float tl = FLT_MAX_, lu = 0.0f, lv = 0.0f, tMax = tmax;
+    const uint32_t idx = c.ref & ~SIB_BIT;
+    const float4* np = reinterpret_cast<const float4*>(S.nodes + idx);
+    float4 a = np[0], b = np[1], cc = np[2];
+    int4 rf = reinterpret_cast<const int4*>(np)[3];
+    pin(a);
+    pin(b);
+    pin(cc);
+    pin(rf);
+    if (!STATS && KHP_PAIR && (c.ref & SIB_BIT)) {
+        const float4* sp = reinterpret_cast<const float4*>(S.nodes + (idx ^ 1u));
+        float4 sa = sp[0], sb = sp[1], sc = sp[2];
+        int4 srf = reinterpret_cast<const int4*>(sp)[3];
+        float sl0, sl1, sr0, sr1;
+        bool slh = slab(sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, tr.r, tr.inv, sl0, sl1);
+        bool srh = slab(sb.z, sb.w, sc.x, sc.y, sc.z, sc.w, tr.r, tr.inv, sr0, sr1);
+        uint32_t dref;
+        float d0, d1;
+        stk.pop(dref, d0, d1);  // the sibling's own entry
+        push_children(stk, slh, srh, sl0, sl1, sr0, sr1, srf);
+    }
+    float l0, l1, r0, r1;
+    bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, l0, l1);
+    bool rh = slab(b.z, b.w, cc.x, cc.y, cc.z, cc.w, tr.r, tr.inv, r0, r1);
+    if (lh && rh) {
+        // both children interior -> they are a record pair; flag the near one
+        const uint32_t sib = (!STATS && KHP_PAIR && !ref_leaf((uint32_t)rf.x) && !ref_leaf((uint32_t)rf.y)) ? SIB_BIT : 0u;
+        if (l0 < r0) {
+            stk.push((uint32_t)rf.y, r0, r1);
+            c = Cur{(uint32_t)rf.x | sib, l0, l1, true};
+        } else {
+            stk.push((uint32_t)rf.x, l0, l1);
+            c = Cur{(uint32_t)rf.y | sib, r0, r1, true};
+        }
+    } else if (lh) {
+        c = Cur{(uint32_t)rf.x, l0, l1, true};
+    } else if (rh) {
+        c = Cur{(uint32_t)rf.y, r0, r1, true};
+    } else {
+        cur_next(stk, c);
+    }
+}
+
+// One candidate of a leaf (Container::closestIntersectionWithCandidates,
+// Container.cpp:13-25): window [0, tMax], later equal-t candidates overwrite.
+__device__ __forceinline__ void leaf_candidate(float4 p0, float4 p1, float4 p2, float4 p3, int32_t slot,
+                                               const Ray& r, float& tMax, float& tl, int32_t& sl, float& lu,
+                                               float& lv) {
+    float t, u = 0.0f, v = 0.0f;
+    bool ok;
+    if (is_tri(p0)) ok = tri_test(p0, p1, p2, r, 0.0f, tMax, t, u, v);
+    else ok = cone_closest(p0, p1, p2, p3, r, 0.0f, tMax, t);
+    if (ok) {
+        tl = t;
+        sl = slot;
+        lu = u;
+        lv = v;
+        tMax = t;
+    }
+}
+
+// Leaf entry, closest hit: prune test, then every candidate with tMin = 0 and
+// tMax = the leaf's exit distance (CPU_BVH.cpp:155-167).  The first two
+// records are fetched together, so a two-candidate leaf costs one round trip.
+template <bool STATS, class Stack>
+__device__ __forceinline__ void leaf_step_closest(const DevScene& S, const TravRay& tr, Hit& h, Stack& stk, Cur& c,
+                                                  TravStats& st) {
+    if (!(c.t1 < 0.0f || c.t0 > h.t)) {
+        if (STATS) st.nodes++;
+        const uint32_t first = c.ref & 0x00FFFFFFu, cnt = leaf_count(S, c.ref);
+        const float4* p = S.prims + 4 * (size_t)first;
+        float tl = FLT_MAX_, lu = 0.0f, lv = 0.0f, tMax = c.t1;
         int32_t sl = -1;
+        if (STATS) st.prims += cnt;
+#if KHP_LEAF_PAIR
+        float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+        float4 b0, b1, b2, b3;
+        if (cnt > 1) {
+            b0 = p[4];
+            b1 = p[5];
+            b2 = p[6];
+            b3 = p[7];
+        }
+        leaf_candidate(a0, a1, a2, a3, (int32_t)first, tr.r, tMax, tl, sl, lu, lv);
+        if (cnt > 1) leaf_candidate(b0, b1, b2, b3, (int32_t)first + 1, tr.r, tMax, tl, sl, lu, lv);
+        for (uint32_t k = 2; k < cnt; ++k) {
+#else
         for (uint32_t k = 0; k < cnt; ++k) {
-            const int32_t slot = (int32_t)(first + k);
-            const float4* p = S.prims + 4 * (size_t)slot;
-            float4 p0 = p[0], p1 = p[1], p2 = p[2];
-            if (STATS) st.prims++;
-            float t, u = 0.0f, v = 0.0f;
-            bool ok;
-            if (is_tri(p0)) ok = tri_test(p0, p1, p2, tr.r, 0.0f, tMax, t, u, v);
-            else ok = cone_closest(p0, p1, p2, p[3], tr.r, 0.0f, tMax, t);
-            if (ok) {
-                tl = t;
-                sl = slot;
-                lu = u;
-                lv = v;
-                tMax = t;
-            }
+#endif
+            const float4* q = p + 4 * k;
+            float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+            pin(q0);
+            pin(q1);
+            pin(q2);
+            pin(q3);
+            leaf_candidate(q0, q1, q2, q3, (int32_t)(first + k), tr.r, tMax, tl, sl, lu, lv);
         }
         if (sl >= 0 && tl < h.t) {
             h.t = tl;
@@ -192,38 +331,180 @@ __device__ __forceinline__ void closest_step(const DevScene& S, const TravRay& t
             h.u = lu;
             h.v = lv;
         }
+    }
+    cur_next(stk, c);
+}
+
+__device__ __forceinline__ bool any_candidate(float4 p0, float4 p1, float4 p2, float4 p3, const Ray& r,
+                                              float tMaxRay) {
+    if (is_tri(p0)) {
+        float t, u, v;
+        return tri_test(p0, p1, p2, r, 0.0f, tMaxRay, t, u, v);
+    }
+    return cone_any(p0, p1, p2, p3, r, tMaxRay);
+}
+
+// Leaf entry, any hit (BVHNode::traverse(ray), CPU_BVH.cpp:211-265; Container.cpp:27-34).
+// Returns true when an occluder is found (traversal ends).
+template <bool STATS, class Stack>
+__device__ __forceinline__ bool leaf_step_any(const DevScene& S, const TravRay& tr, float tMaxRay, Stack& stk, Cur& c,
+                                              TravStats& st) {
+    if (!(c.t1 < 0.0f || c.t0 > tMaxRay)) {
+        if (STATS) st.nodes++;
+        const uint32_t first = c.ref & 0x00FFFFFFu, cnt = leaf_count(S, c.ref);
+        const float4* p = S.prims + 4 * (size_t)first;
+#if KHP_LEAF_PAIR
+        float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+        float4 b0, b1, b2, b3;
+        if (cnt > 1) {
+            b0 = p[4];
+            b1 = p[5];
+            b2 = p[6];
+            b3 = p[7];
+        }
+        if (STATS) st.prims++;
+        if (any_candidate(a0, a1, a2, a3, tr.r, tMaxRay)) return true;
+        if (cnt > 1) {
+            if (STATS) st.prims++;
+            if (any_candidate(b0, b1, b2, b3, tr.r, tMaxRay)) return true;
+        }
+        for (uint32_t k = 2; k < cnt; ++k) {
+#else
+        for (uint32_t k = 0; k < cnt; ++k) {
+#endif
+            const float4* q = p + 4 * k;
+            float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+            pin(q0);
+            pin(q1);
+            pin(q2);
+            pin(q3);
+            if (STATS) st.prims++;
+            if (any_candidate(q0, q1, q2, q3, tr.r, tMaxRay)) return true;
+        }
+    }
+    cur_next(stk, c);
+    return false;
+}
+
+// ---- one-fetch-per-iteration traversal (the production kernels) -------------------------
+// A lane holds either an interior entry (cursor) or a partly tested leaf
+// (LeafCur).  Each wave iteration resolves the lane's next unit of work
+// (popping pruned entries, opening leaves), then fetches exactly ONE 64-B
+// record -- a node or a candidate primitive, from the same instruction
+// stream -- and then runs the slab pair or the one candidate test.  Every
+// iteration thus costs one memory round trip, whatever mix of interior and
+// leaf work its lanes carry.  Visit order and arithmetic are those of
+// interior_step / leaf_step_*: candidates of a leaf are tested in order with
+// the leaf's window, and entries are prune-tested when they are popped.
+struct LeafCur {
+    uint32_t slot, left;  // next candidate slot, candidates still to test (0: not in a leaf)
+    float tmax;           // closest: the leaf window (shrinks on hits); any: unused
+    float tl, lu, lv;     // closest: best candidate of this leaf so far
+    int32_t sl;
+};
+
+// Open the leaf in the cursor: KIRK's leaf prologue (CPU_BVH.cpp:155-159).
+template <bool STATS>
+__device__ __forceinline__ void leaf_open(const DevScene& S, const Cur& c, LeafCur& lf, TravStats& st) {
+    if (STATS) st.nodes++;
+    lf.slot = c.ref & 0x00FFFFFFu;
+    lf.left = leaf_count(S, c.ref);
+    lf.tmax = c.t1;
+    lf.tl = FLT_MAX_;
+    lf.lu = lf.lv = 0.0f;
+    lf.sl = -1;
+}
+
+// Resolve the lane's next unit of work against `tlimit` (closest: current hit
+// t; any: the ray's tMax).  Returns false when the ray is finished.
+template <bool STATS, class Stack>
+__device__ __forceinline__ bool resolve(const DevScene& S, float tlimit, Stack& stk, Cur& c, LeafCur& lf,
+                                        TravStats& st) {
+    if (lf.left > 0) return true;
+    while (c.valid) {
+        if (c.t1 < 0.0f || c.t0 > tlimit) {  // pruned at pop time
+            cur_next(stk, c);
+            continue;
+        }
+        if (ref_leaf(c.ref)) {
+            leaf_open<STATS>(S, c, lf, st);
+            return true;
+        }
+        return true;  // interior: fetched this iteration
+    }
+    return false;
+}
+
+// The record this lane needs this iteration.
+__device__ __forceinline__ const float4* work_record(const DevScene& S, const Cur& c, const LeafCur& lf) {
+    return lf.left > 0 ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
+}
+
+// Interior work on a fetched record (prune test already done in resolve).
+template <bool STATS, class Stack>
+__device__ __forceinline__ void interior_apply(const TravRay& tr, float4 a, float4 b, float4 cc, int4 rf, Stack& stk,
+                                               Cur& c, TravStats& st) {
+    if (STATS) st.nodes++;
+    float l0, l1, r0, r1;
+    bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, l0, l1);
+    bool rh = slab(b.z, b.w, cc.x, cc.y, cc.z, cc.w, tr.r, tr.inv, r0, r1);
+    if (lh && rh) {
+        if (l0 < r0) {
+            stk.push((uint32_t)rf.y, r0, r1);
+            c = Cur{(uint32_t)rf.x, l0, l1, true};
+        } else {
+            stk.push((uint32_t)rf.x, l0, l1);
+            c = Cur{(uint32_t)rf.y, r0, r1, true};
+        }
+    } else if (lh) {
+        c = Cur{(uint32_t)rf.x, l0, l1, true};
+    } else if (rh) {
+        c = Cur{(uint32_t)rf.y, r0, r1, true};
     } else {
-        visit_interior(S, tr, ref, stk);
+        cur_next(stk, c);
     }
 }
 
-// One any-hit step; returns true when an occluder is found.
+// One closest-hit iteration for a lane that resolved to work.
 template <bool STATS, class Stack>
-__device__ __forceinline__ bool any_step(const DevScene& S, const TravRay& tr, float tMaxRay, Stack& stk,
-                                         TravStats& st) {
-    uint32_t ref;
-    float tmin, tmax;
-    stk.pop(ref, tmin, tmax);
-    if (tmax < 0.0f || tmin > tMaxRay) return false;
-    if (STATS) st.nodes++;
-    if (ref_leaf(ref)) {
-        const uint32_t first = ref & 0x00FFFFFFu, cnt = leaf_count(S, ref);
-        for (uint32_t k = 0; k < cnt; ++k) {
-            const float4* p = S.prims + 4 * (size_t)(first + k);
-            float4 p0 = p[0], p1 = p[1], p2 = p[2];
-            if (STATS) st.prims++;
-            bool ok;
-            if (is_tri(p0)) {
-                float t, u, v;
-                ok = tri_test(p0, p1, p2, tr.r, 0.0f, tMaxRay, t, u, v);
-            } else {
-                ok = cone_any(p0, p1, p2, p[3], tr.r, tMaxRay);
+__device__ __forceinline__ void step1_closest(const DevScene& S, const TravRay& tr, Hit& h, Stack& stk, Cur& c,
+                                              LeafCur& lf, TravStats& st) {
+    const float4* p = work_record(S, c, lf);
+    float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    if (lf.left > 0) {
+        if (STATS) st.prims++;
+        leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);
+        ++lf.slot;
+        if (--lf.left == 0) {
+            if (lf.sl >= 0 && lf.tl < h.t) {
+                h.t = lf.tl;
+                h.slot = lf.sl;
+                h.u = lf.lu;
+                h.v = lf.lv;
             }
-            if (ok) return true;
+            cur_next(stk, c);
         }
-        return false;
+    } else {
+        int4 rf = make_int4(__float_as_int(q3.x), __float_as_int(q3.y), __float_as_int(q3.z), __float_as_int(q3.w));
+        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st);
     }
-    visit_interior(S, tr, ref, stk);
+}
+
+// One any-hit iteration; returns true when an occluder is found.
+template <bool STATS, class Stack>
+__device__ __forceinline__ bool step1_any(const DevScene& S, const TravRay& tr, float tMaxRay, Stack& stk, Cur& c,
+                                          LeafCur& lf, TravStats& st) {
+    const float4* p = work_record(S, c, lf);
+    float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    if (lf.left > 0) {
+        if (STATS) st.prims++;
+        if (any_candidate(q0, q1, q2, q3, tr.r, tMaxRay)) return true;
+        ++lf.slot;
+        if (--lf.left == 0) cur_next(stk, c);
+    } else {
+        int4 rf = make_int4(__float_as_int(q3.x), __float_as_int(q3.y), __float_as_int(q3.z), __float_as_int(q3.w));
+        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st);
+    }
     return false;
 }
 
@@ -235,16 +516,26 @@ __device__ __forceinline__ void trace_closest(const DevScene& S, const Ray& r, H
     h.u = h.v = 0.0f;
     TravRay tr;
     trav_setup(tr, r);
-    if (!trav_begin(S, tr, stk)) return;
-    while (!stk.empty()) closest_step<STATS>(S, tr, h, stk, st);
+    Cur c;
+    if (!trav_begin(S, tr, stk, c)) return;
+    while (c.valid) {
+        if (ref_leaf(c.ref)) leaf_step_closest<STATS>(S, tr, h, stk, c, st);
+        else interior_step<STATS>(S, tr, h.t, stk, c, st);
+    }
 }
 
 template <bool STATS, class Stack>
 __device__ __forceinline__ bool trace_any(const DevScene& S, const Ray& r, float tMaxRay, Stack& stk, TravStats& st) {
     TravRay tr;
     trav_setup(tr, r);
-    if (!trav_begin(S, tr, stk)) return false;
-    while (!stk.empty())
-        if (any_step<STATS>(S, tr, tMaxRay, stk, st)) return true;
+    Cur c;
+    if (!trav_begin(S, tr, stk, c)) return false;
+    while (c.valid) {
+        if (ref_leaf(c.ref)) {
+            if (leaf_step_any<STATS>(S, tr, tMaxRay, stk, c, st)) return true;
+        } else {
+            interior_step<STATS>(S, tr, tMaxRay, stk, c, st);
+        }
+    }
     return false;
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 passes for bench.py (run on the GPU box via gpurun, from the repo root).
-# usage: tools/profile.sh <tag> [pass...]   passes: trace fetch write sq lat ea tcc list
+# usage: tools/profile.sh <tag> [pass...]   passes: trace fetch write sq lat ea tcc ta tas tcp tcpa list
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}; shift || true
@@ -12,13 +12,17 @@ B="python3 $R/bench.py --no-cpu-baseline"
 for p in $PASSES; do
   case $p in
     list)  timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true ;;
-    trace) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B --steps 3 --warmup 1 > $OUT/trace_bench.json 2> $OUT/trace_bench.log ;;
-    fetch) timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/fetch -o run -- $B --steps 1 --warmup 0 > $OUT/fetch_bench.json 2> $OUT/fetch_bench.log ;;
-    write) timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/write -o run -- $B --steps 1 --warmup 0 > $OUT/write_bench.json 2> $OUT/write_bench.log ;;
-    sq)    timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_SALU --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/sq -o run -- $B --steps 1 --warmup 0 > $OUT/sq_bench.json 2> $OUT/sq_bench.log ;;
-    lat)   timeout -k 10 600 rocprofv3 --pmc VmemLatency --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/lat -o run -- $B --steps 1 --warmup 0 > $OUT/lat_bench.json 2> $OUT/lat_bench.log ;;
-    ea)    timeout -k 10 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/ea -o run -- $B --steps 1 --warmup 0 > $OUT/ea_bench.json 2> $OUT/ea_bench.log ;;
-    tcc)   timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tcc -o run -- $B --steps 1 --warmup 0 > $OUT/tcc_bench.json 2> $OUT/tcc_bench.log ;;
+    trace) timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B --steps 3 --warmup 1 > $OUT/trace_bench.json 2> $OUT/trace_bench.log ;;
+    fetch) timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/fetch -o run -- $B --steps 1 --warmup 0 > $OUT/fetch_bench.json 2> $OUT/fetch_bench.log ;;
+    write) timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/write -o run -- $B --steps 1 --warmup 0 > $OUT/write_bench.json 2> $OUT/write_bench.log ;;
+    sq)    timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_SALU --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/sq -o run -- $B --steps 1 --warmup 0 > $OUT/sq_bench.json 2> $OUT/sq_bench.log ;;
+    lat)   timeout -k 10 240 rocprofv3 --pmc VmemLatency --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/lat -o run -- $B --steps 1 --warmup 0 > $OUT/lat_bench.json 2> $OUT/lat_bench.log ;;
+    ea)    timeout -k 10 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/ea -o run -- $B --steps 1 --warmup 0 > $OUT/ea_bench.json 2> $OUT/ea_bench.log ;;
+    ta)    timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_BUSY_avr --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/ta -o run -- $B --steps 1 --warmup 0 > $OUT/ta_bench.json 2> $OUT/ta_bench.log ;;
+    tas)   timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_ADDR_STALLED_BY_TC_CYCLES_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tas -o run -- $B --steps 1 --warmup 0 > $OUT/tas_bench.json 2> $OUT/tas_bench.log ;;
+    tcp)   timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TCP_PENDING_STALL_CYCLES_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tcp -o run -- $B --steps 1 --warmup 0 > $OUT/tcp_bench.json 2> $OUT/tcp_bench.log ;;
+    tcpa)  timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TCP_TOTAL_CACHE_ACCESSES_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tcpa -o run -- $B --steps 1 --warmup 0 > $OUT/tcpa_bench.json 2> $OUT/tcpa_bench.log ;;
+    tcc)   timeout -k 10 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tcc -o run -- $B --steps 1 --warmup 0 > $OUT/tcc_bench.json 2> $OUT/tcc_bench.log ;;
   esac
 done
 echo "profile passes done: $PASSES"
