@@ -31,10 +31,11 @@ using namespace khp;
 struct Counters {
     uint32_t nq[2];        // ray queue sizes
     uint32_t nsh;          // shadow queue size
-    uint32_t fetch_ext, fetch_sh;
+    uint32_t fetch_ext[8], fetch_sh[8];   // queue-segment claim cursors (one per XCD group)
     uint32_t pad[3];
     unsigned long long ext_rays, sh_rays;
     unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests, spills;
+    unsigned long long iters, lanes_busy, sh_iters, sh_lanes_busy;  // wave iterations, lanes with work
 };
 
 struct Wave {
@@ -113,8 +114,10 @@ __global__ void k_prep(Counters* c, int cur) {
     c->sh_rays += c->nsh;   // shadow rays of the previous bounce
     c->nq[nxt] = 0;
     c->nsh = 0;
-    c->fetch_ext = 0;
-    c->fetch_sh = 0;
+    for (int g = 0; g < 8; ++g) {
+        c->fetch_ext[g] = 0;
+        c->fetch_sh[g] = 0;
+    }
     c->ext_rays += c->nq[cur];
 }
 
@@ -144,15 +147,49 @@ struct SpillArea {
     uint32_t stride;   // lanes in the grid
 };
 
-__device__ __forceinline__ uint32_t claim(unsigned long long idle, uint32_t* fetch, uint32_t& slot_out) {
-    uint32_t lane = lane_id();
-    uint32_t k = (uint32_t)__popcll(idle);
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(fetch, k);
-    base = __shfl(base, 0);
-    slot_out = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-    return base;
-}
+// Work claiming with L2 affinity.  Blocks b and b+8 run on the same XCD
+// (round-robin placement -- used for speed only, never for correctness), and
+// each XCD has its own 4 MiB L2.  The queue is cut into NSEG contiguous
+// segments; the waves of block group g = blockIdx.x % 8 drain segment g first,
+// so each L2 serves one band of the frame (primary rays: a band of tiles;
+// secondary and shadow rays: the matching region of the scene), then move on
+// to the next segments so no XCD idles at the end of the launch.
+#ifndef KHP_XCD_SPLIT
+#define KHP_XCD_SPLIT 1
+#endif
+constexpr uint32_t NSEG = KHP_XCD_SPLIT ? 8u : 1u;
+
+struct Claimer {
+    uint32_t* fetch;  // NSEG cursors
+    uint32_t n;       // queue length
+    uint32_t sg;      // segment this wave is draining (wave-uniform)
+    uint32_t tried;   // segments found exhausted
+    __device__ __forceinline__ void init(uint32_t* f, uint32_t len) {
+        fetch = f;
+        n = len;
+        sg = NSEG > 1 ? blockIdx.x % NSEG : 0u;
+        tried = 0;
+    }
+    __device__ __forceinline__ uint32_t lo(uint32_t g) const { return (uint32_t)((uint64_t)n * g / NSEG); }
+    // Claims popc(idle) indices for the idle lanes; returns true for this lane
+    // if it received one (my).  Sets done when every segment is drained.
+    __device__ __forceinline__ bool claim(unsigned long long idle, uint32_t& my, bool& done) {
+        const uint32_t lane = lane_id();
+        const uint32_t k = (uint32_t)__popcll(idle);
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&fetch[sg], k);
+        base = __shfl(base, 0);
+        const uint32_t s0 = lo(sg), len = lo(sg + 1) - s0;
+        const uint32_t off = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+        my = s0 + off;
+        const bool got = off < len;
+        if (base + k >= len) {
+            sg = (sg + 1) % NSEG;
+            if (++tried == NSEG) done = true;
+        }
+        return got;
+    }
+};
 
 // ---- extend: closest hit for every queued ray ------------------------------------------
 #ifndef KHP_WW
@@ -203,13 +240,15 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
     bool has = false, exhausted = false;
     uint32_t idx = 0;
+    unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
+    Claimer cl;
+    cl.init(Wv.cnt->fetch_ext, n);
     for (;;) {
         unsigned long long idle = __ballot(!has);
         if (!exhausted && __popcll(idle) >= REFILL) {
             uint32_t my;
-            uint32_t base = claim(idle, &Wv.cnt->fetch_ext, my);
-            if (base + (uint32_t)__popcll(idle) >= n) exhausted = true;
-            if (!has && my < n) {
+            const bool got = cl.claim(idle, my, exhausted);
+            if (!has && got) {
                 idx = my;
                 Ray r;
                 r.o = mk(Wv.qo[cur][0][idx], Wv.qo[cur][1][idx], Wv.qo[cur][2][idx]);
@@ -243,6 +282,11 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
                 Wv.hv[idx] = h.v;
                 has = false;
             }
+            if (STATS) {
+                unsigned long long wm = __ballot(work);
+                ++wit;
+                wbusy += (uint32_t)__popcll(wm);
+            }
             if (work) step1_closest<STATS>(S, tr, h, stk, c, lf, st);
 #else
             trav_round<STATS, KHP_WW_EXT>(S, tr, h.t, has, stk, c, st,
@@ -268,6 +312,8 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
         unsigned long long sp_ = wave_sum((unsigned long long)stk.spills);
         if (lane_id() == 0) {
             atomicAdd(&Wv.cnt->spills, sp_);
+            atomicAdd(&Wv.cnt->iters, wit);
+            atomicAdd(&Wv.cnt->lanes_busy, wbusy);
         }
     }
 }
@@ -499,16 +545,21 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
     TravRay tr;
     Cur c{0u, 0.0f, 0.0f, false};
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
+    unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
     float tmax = 0.0f;
-    bool has = false, exhausted = false, found = false;
+    bool has = false, exhausted = false;
+#if !KHP_ONEFETCH
+    bool found = false;
+#endif
+    Claimer cl;
+    cl.init(Wv.cnt->fetch_sh, n);
     uint32_t idx = 0;
     for (;;) {
         unsigned long long idle = __ballot(!has);
         if (!exhausted && __popcll(idle) >= REFILL) {
             uint32_t my;
-            uint32_t base = claim(idle, &Wv.cnt->fetch_sh, my);
-            if (base + (uint32_t)__popcll(idle) >= n) exhausted = true;
-            if (!has && my < n) {
+            const bool got = cl.claim(idle, my, exhausted);
+            if (!has && got) {
                 idx = my;
                 const float4* rec = Wv.sh + 6 * (size_t)idx;
                 float4 a = rec[0], b = rec[1];
@@ -517,7 +568,9 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
                 r.d = mk(b.x, b.y, b.z);
                 tmax = a.w;
                 trav_setup(tr, r);
+#if !KHP_ONEFETCH
                 found = false;
+#endif
                 lf.left = 0;
                 has = trav_begin(S, tr, stk, c);
                 if (!has) Wv.vis[idx] = 0;
@@ -534,6 +587,11 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
             if (has && !work) {
                 Wv.vis[idx] = 0;
                 has = false;
+            }
+            if (STATS) {
+                unsigned long long wm = __ballot(work);
+                ++wit;
+                wbusy += (uint32_t)__popcll(wm);
             }
             if (work && step1_any<STATS>(S, tr, tmax, stk, c, lf, st)) {
                 Wv.vis[idx] = 1;
@@ -559,6 +617,8 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
         }
         unsigned long long sp_ = wave_sum((unsigned long long)stk.spills);
         if (lane_id() == 0) {
+            atomicAdd(&Wv.cnt->sh_iters, wit);
+            atomicAdd(&Wv.cnt->sh_lanes_busy, wbusy);
             atomicAdd(&Wv.cnt->spills, sp_);
         }
     }
@@ -680,6 +740,7 @@ struct DevMem {
 
 struct TimedLaunch {
     int kind;  // 0 extend, 1 shade, 2 shadow, 3 other
+    int bounce;
     hipEvent_t a, b;
 };
 
@@ -696,7 +757,8 @@ struct khp_ctx {
     size_t cap = 0;
     DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb, visb, cnt, spill;
     // framebuffer + pixel list
-    DevMem fb, pix, stage, stage_pix;
+    DevMem fb, pix, stage, stage_pix, snap;   // snap: per-bounce Counters snapshots (stats renders)
+    int cur_bounce = -1;
     uint32_t fbW = 0, fbH = 0;
     std::vector<uint32_t> pix_host;
     uint32_t pix_key[5] = {0, 0, 0, 0, 0};
@@ -929,7 +991,7 @@ static void timed(khp_ctx* c, int kind, bool begin) {
     hipEvent_t e = next_event(c);
     if (!e) return;
     (void)hipEventRecord(e, c->stream);
-    if (begin) c->launches.push_back(TimedLaunch{kind, e, nullptr});
+    if (begin) c->launches.push_back(TimedLaunch{kind, c->cur_bounce, e, nullptr});
     else c->launches.back().b = e;
 }
 
@@ -965,6 +1027,13 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     Wv.depth = p->depth;
     SpillArea sp_ext{c->spill.as<int4>(), (uint32_t)c->grid_ext * 256u};
     SpillArea sp_sh{c->spill.as<int4>(), (uint32_t)c->grid_sh * 256u};
+    size_t n_snap = 0;
+    std::vector<uint32_t> snap_bounce;
+    if (stats) {
+        size_t chunks = (size_t)((P_all + P_chunk - 1) / P_chunk) * ((p->spp + S_chunk - 1) / S_chunk);
+        HIPCHK(c->snap.ensure(chunks * p->depth * sizeof(Counters)));
+    }
+    c->cur_bounce = -1;
     hipEvent_t ev_start = next_event(c);
     (void)hipEventRecord(ev_start, c->stream);
     for (uint32_t p0 = 0; p0 < P_all; p0 += P_chunk) {
@@ -981,6 +1050,7 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
             timed(c, 3, false);
             for (uint32_t b = 0; b < p->depth; ++b) {
                 int cur = b & 1;
+                c->cur_bounce = (int)b;
                 hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, c->stream, Wv.cnt, cur);
                 timed(c, 0, true);
                 if (stats)
@@ -1000,7 +1070,14 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
                 timed(c, 2, true);   // shadow stage = any-hit traversal + finish
                 hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, c->stream, c->S, Wv);
                 timed(c, 2, false);
+                if (stats) {
+                    HIPCHK(hipMemcpyAsync(c->snap.as<Counters>() + n_snap, c->cnt.p, sizeof(Counters),
+                                          hipMemcpyDeviceToDevice, c->stream));
+                    snap_bounce.push_back(b);
+                    ++n_snap;
+                }
             }
+            c->cur_bounce = -1;
             hipLaunchKernelGGL(k_tail, dim3(1), dim3(1), 0, c->stream, Wv.cnt);
             timed(c, 3, true);
             hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, c->stream, Wv, c->fb.as<float>());
@@ -1020,6 +1097,13 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     c->st.render_ms = ms;
     c->st.extend_ms = c->st.shade_ms = c->st.shadow_ms = c->st.other_ms = 0.0;
     c->st.extend_launches = 0;
+    for (int k = 0; k < KHP_MAX_BOUNCE_STATS; ++k) {
+        c->st.bounce_extend_ms[k] = c->st.bounce_shadow_ms[k] = 0.0;
+        c->st.bounce_rays[k] = c->st.bounce_nodes[k] = c->st.bounce_prims[k] = 0;
+        c->st.bounce_shadow_rays[k] = c->st.bounce_shadow_nodes[k] = c->st.bounce_shadow_prims[k] = 0;
+        c->st.bounce_wave_iters[k] = c->st.bounce_lanes_busy[k] = 0;
+        c->st.bounce_shadow_wave_iters[k] = c->st.bounce_shadow_lanes_busy[k] = 0;
+    }
     for (auto& l : c->launches) {
         float t = 0.0f;
         if (l.b && hipEventElapsedTime(&t, l.a, l.b) == hipSuccess) {
@@ -1027,6 +1111,10 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
             else if (l.kind == 1) c->st.shade_ms += t;
             else if (l.kind == 2) c->st.shadow_ms += t;
             else c->st.other_ms += t;
+            if (l.bounce >= 0 && l.bounce < KHP_MAX_BOUNCE_STATS) {
+                if (l.kind == 0) c->st.bounce_extend_ms[l.bounce] += t;
+                if (l.kind == 2) c->st.bounce_shadow_ms[l.bounce] += t;
+            }
         }
     }
     Counters hc;
@@ -1038,6 +1126,27 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     c->st.shadow_node_visits = hc.sh_node_visits;
     c->st.shadow_prim_tests = hc.sh_prim_tests;
     c->st.stack_spills = hc.spills;
+    if (n_snap) {
+        std::vector<Counters> sn(n_snap);
+        HIPCHK(hipMemcpy(sn.data(), c->snap.p, n_snap * sizeof(Counters), hipMemcpyDeviceToHost));
+        Counters prev{};
+        for (size_t k = 0; k < n_snap; ++k) {
+            const uint32_t b = snap_bounce[k];
+            if (b < KHP_MAX_BOUNCE_STATS) {
+                c->st.bounce_rays[b] += sn[k].ext_rays - prev.ext_rays;
+                c->st.bounce_nodes[b] += sn[k].node_visits - prev.node_visits;
+                c->st.bounce_prims[b] += sn[k].prim_tests - prev.prim_tests;
+                c->st.bounce_shadow_rays[b] += sn[k].nsh;
+                c->st.bounce_shadow_nodes[b] += sn[k].sh_node_visits - prev.sh_node_visits;
+                c->st.bounce_shadow_prims[b] += sn[k].sh_prim_tests - prev.sh_prim_tests;
+                c->st.bounce_wave_iters[b] += sn[k].iters - prev.iters;
+                c->st.bounce_lanes_busy[b] += sn[k].lanes_busy - prev.lanes_busy;
+                c->st.bounce_shadow_wave_iters[b] += sn[k].sh_iters - prev.sh_iters;
+                c->st.bounce_shadow_lanes_busy[b] += sn[k].sh_lanes_busy - prev.sh_lanes_busy;
+            }
+            prev = sn[k];
+        }
+    }
     return KHP_OK;
 }
 

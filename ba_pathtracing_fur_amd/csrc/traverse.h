@@ -122,13 +122,16 @@ struct LdsStack {
 // needs late (z planes, the cone's W / max_d) below the test's early-out
 // branches, which turns one memory round trip per record into two or three
 // dependent ones (seen in the gfx950 ISA).
+#ifndef KHP_PIN1
+#define KHP_PIN1 1   // pin the one-fetch record (same speed, no scratch in k_extend)
+#endif
 __device__ __forceinline__ void pin(float4& v) {
-#if KHP_PIN
+#if KHP_PIN || KHP_PIN1
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 #endif
 }
 __device__ __forceinline__ void pin(int4& v) {
-#if KHP_PIN
+#if KHP_PIN || KHP_PIN1
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 #endif
 }
@@ -471,6 +474,9 @@ __device__ __forceinline__ void step1_closest(const DevScene& S, const TravRay& 
                                               LeafCur& lf, TravStats& st) {
     const float4* p = work_record(S, c, lf);
     float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+#if KHP_PIN1
+    pin(q0); pin(q1); pin(q2); pin(q3);
+#endif
     if (lf.left > 0) {
         if (STATS) st.prims++;
         leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);
@@ -496,6 +502,9 @@ __device__ __forceinline__ bool step1_any(const DevScene& S, const TravRay& tr, 
                                           LeafCur& lf, TravStats& st) {
     const float4* p = work_record(S, c, lf);
     float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+#if KHP_PIN1
+    pin(q0); pin(q1); pin(q2); pin(q3);
+#endif
     if (lf.left > 0) {
         if (STATS) st.prims++;
         if (any_candidate(q0, q1, q2, q3, tr.r, tMaxRay)) return true;

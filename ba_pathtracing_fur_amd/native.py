@@ -74,10 +74,16 @@ class Stats(ctypes.Structure):
                 ("shadow_ms", c_double), ("other_ms", c_double), ("extend_rays", c_uint64),
                 ("shadow_rays", c_uint64), ("extend_launches", c_uint64), ("node_visits", c_uint64),
                 ("prim_tests", c_uint64), ("shadow_node_visits", c_uint64), ("shadow_prim_tests", c_uint64),
-                ("stack_spills", c_uint64)]
+                ("stack_spills", c_uint64), ("bounce_rays", c_uint64 * 16), ("bounce_nodes", c_uint64 * 16),
+                ("bounce_prims", c_uint64 * 16), ("bounce_shadow_rays", c_uint64 * 16),
+                ("bounce_shadow_nodes", c_uint64 * 16), ("bounce_shadow_prims", c_uint64 * 16),
+                ("bounce_extend_ms", c_double * 16), ("bounce_shadow_ms", c_double * 16),
+                ("bounce_wave_iters", c_uint64 * 16), ("bounce_lanes_busy", c_uint64 * 16),
+                ("bounce_shadow_wave_iters", c_uint64 * 16), ("bounce_shadow_lanes_busy", c_uint64 * 16)]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: (list(getattr(self, k)) if not isinstance(getattr(self, k), (int, float)) else getattr(self, k))
+                for k, _ in self._fields_}
 
 
 # every symbol the header declares (checked by tests/test_abi.py)

@@ -210,6 +210,18 @@ def main():
             "shadow_nodes_per_ray": round(cnt["shadow_node_visits"] / max(1, cnt["shadow_rays"]), 2),
             "stack_spills_per_ray": round(cnt["stack_spills"] / max(1, rays + cnt["shadow_rays"]), 4),
             "build_s": round(build_s, 2),
+            "per_bounce": [
+                {"bounce": b, "rays": cnt["bounce_rays"][b],
+                 "nodes_per_ray": round(cnt["bounce_nodes"][b] / max(1, cnt["bounce_rays"][b]), 2),
+                 "prims_per_ray": round(cnt["bounce_prims"][b] / max(1, cnt["bounce_rays"][b]), 2),
+                 "extend_ms": round(last["bounce_extend_ms"][b], 3),
+                 "shadow_rays": cnt["bounce_shadow_rays"][b],
+                 "shadow_nodes_per_ray": round(cnt["bounce_shadow_nodes"][b] / max(1, cnt["bounce_shadow_rays"][b]), 2),
+                 "shadow_ms": round(last["bounce_shadow_ms"][b], 3),
+                 "wave_iters": cnt["bounce_wave_iters"][b],
+                 "lane_use": round(cnt["bounce_lanes_busy"][b] / max(1, 64 * cnt["bounce_wave_iters"][b]), 3),
+                 "shadow_lane_use": round(cnt["bounce_shadow_lanes_busy"][b] / max(1, 64 * cnt["bounce_shadow_wave_iters"][b]), 3)}
+                for b in range(min(depth, 16))],
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 1
+#define KHP_ABI_VERSION 2
 
 typedef struct khp_ctx khp_ctx;
 
@@ -167,7 +167,16 @@ typedef struct {
     uint64_t extend_rays, shadow_rays, extend_launches;
     uint64_t node_visits, prim_tests, shadow_node_visits, shadow_prim_tests; /* KHP_CTX_STATS only */
     uint64_t stack_spills;           /* traversal-stack entries spilled from LDS (stats only) */
+    /* per bounce (index = bounce, up to KHP_MAX_BOUNCE_STATS), instrumented renders only */
+    uint64_t bounce_rays[16], bounce_nodes[16], bounce_prims[16];
+    uint64_t bounce_shadow_rays[16], bounce_shadow_nodes[16], bounce_shadow_prims[16];
+    double bounce_extend_ms[16], bounce_shadow_ms[16];
+    /* traversal-loop efficiency (instrumented renders): wave iterations and the
+     * lanes that had a record to fetch in them (busy / (64 * iters) = lane use) */
+    uint64_t bounce_wave_iters[16], bounce_lanes_busy[16];
+    uint64_t bounce_shadow_wave_iters[16], bounce_shadow_lanes_busy[16];
 } khp_stats;
+#define KHP_MAX_BOUNCE_STATS 16
 
 #define KHP_CTX_STATS  (1u << 0)   /* instrumented kernels: count node/prim visits */
 

@@ -212,3 +212,37 @@ def test_cpp_host_program_matches(hip_ctx, tmp_path):
     hip_ctx.build_accel()
     want = hip_ctx.render(64, 40, 2, 5)
     assert np.array_equal(img.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("name,kw", [("config2", dict(n_strands=3000)), ("config5", dict(n_strands=2000,
+                                                                                          torus_grid=30))])
+def test_production_traversal_kernels_ray_by_ray(hip_ctx, mode, name, kw):
+    """KHP_TRACE_PERSISTENT routes the batch queries through the renderer's own
+    persistent kernels: 1 = instrumented (KIRK's node/candidate visit counts must
+    match the oracle's), 2 = the production build used in timed frames."""
+    sd = S.build_config(name, width=32, height=32, **kw)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    o = oracle_ffi.Oracle(sd)
+    rng = np.random.default_rng(17)
+    n = 100000
+    orig = rng.uniform(-1.5, 1.5, (n, 3)).astype(np.float32) + np.float32([0, 1, 0])
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    tmax = rng.uniform(0.01, 2.0, n).astype(np.float32)
+    t0, obj0, uv0, nodes, prims = o.trace_closest(orig, d)
+    any0 = o.trace_any(orig, d, tmax)
+    os.environ["KHP_TRACE_PERSISTENT"] = mode
+    try:
+        t, obj, uv = hip_ctx.trace_closest(orig, d)
+        st = hip_ctx.stats()
+        a = hip_ctx.trace_any(orig, d, tmax)
+    finally:
+        del os.environ["KHP_TRACE_PERSISTENT"]
+    assert np.array_equal(obj, obj0)
+    assert np.array_equal(t.view(np.uint32), t0.view(np.uint32))
+    assert np.array_equal(uv.view(np.uint32), uv0.view(np.uint32))
+    assert np.array_equal(a, any0)
+    if mode == "1":
+        assert (st["node_visits"], st["prim_tests"]) == (nodes, prims)
