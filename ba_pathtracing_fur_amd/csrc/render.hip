@@ -19,6 +19,7 @@
 #include <chrono>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "device.h"
@@ -36,6 +37,7 @@ struct Counters {
     unsigned long long ext_rays, sh_rays;
     unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests, spills;
     unsigned long long iters, lanes_busy, sh_iters, sh_lanes_busy;  // wave iterations, lanes with work
+    unsigned long long step_cycles[4];  // KHP_PROFILE_STEPS: resolve, fetch, compute, loop/refill (extend)
 };
 
 struct Wave {
@@ -142,6 +144,12 @@ constexpr int RING = KHP_RING;      // LDS ring entries per lane (3 x 4 B each)
 constexpr int REFILL = KHP_REFILL;  // refill when >= REFILL lanes are idle
 constexpr size_t LDS_BYTES = 3 * RING * 256 * sizeof(uint32_t);
 
+#ifndef KHP_TOPREG
+#define KHP_TOPREG 0   // 1: stack top in registers with a prefetched next top (exact; measured 16 % slower)
+#endif
+template <int R, bool COUNT>
+using TravStack = typename std::conditional<KHP_TOPREG != 0, LdsStackT<R, COUNT>, LdsStack<R, COUNT>>::type;
+
 struct SpillArea {
     int4* base;
     uint32_t stride;   // lanes in the grid
@@ -195,6 +203,9 @@ struct Claimer {
 #ifndef KHP_WW
 #define KHP_WW 0   // 1: while-while phases (measured 35 % slower: waves wait for the longest interior run); 0: if-if
 #endif
+#ifndef KHP_PROFILE_STEPS
+#define KHP_PROFILE_STEPS 0   // diagnostic build: s_memtime per traversal phase (instrumented kernels)
+#endif
 #ifndef KHP_ONEFETCH
 #define KHP_ONEFETCH 1   // one record fetch per lane per iteration (nodes and candidates alike)
 #endif
@@ -231,7 +242,7 @@ template <bool STATS>
 __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = Wv.cnt->nq[cur];
-    LdsStack<RING, STATS> stk;
+    TravStack<RING, STATS> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0};
     TravRay tr;
@@ -241,6 +252,9 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
     bool has = false, exhausted = false;
     uint32_t idx = 0;
     unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
+#if KHP_PROFILE_STEPS
+    uint64_t prof[4] = {0, 0, 0, 0}, prof_last = __builtin_amdgcn_s_memtime(), prof_t0 = prof_last;
+#endif
     Claimer cl;
     cl.init(Wv.cnt->fetch_ext, n);
     for (;;) {
@@ -274,6 +288,9 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
         }
         for (;;) {
 #if KHP_ONEFETCH
+#if KHP_PROFILE_STEPS
+            uint64_t tp0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
+#endif
             const bool work = has && resolve<STATS>(S, h.t, stk, c, lf, st);
             if (has && !work) {
                 Wv.ht[idx] = h.t;
@@ -287,6 +304,24 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
                 ++wit;
                 wbusy += (uint32_t)__popcll(wm);
             }
+#if KHP_PROFILE_STEPS
+            if (STATS) {
+                uint64_t tp1 = __builtin_amdgcn_s_memtime();
+                float4 q0, q1, q2, q3;
+                if (work) {
+                    const float4* pp = work_record(S, c, lf);
+                    q0 = pp[0]; q1 = pp[1]; q2 = pp[2]; q3 = pp[3];
+                    pin(q0); pin(q1); pin(q2); pin(q3);
+                }
+                uint64_t tp2 = __builtin_amdgcn_s_memtime();
+                if (work) step1_closest_rec<STATS>(tr, h, stk, c, lf, st, q0, q1, q2, q3);
+                uint64_t tp3 = __builtin_amdgcn_s_memtime();
+                prof[0] += tp1 - tp0;
+                prof[1] += tp2 - tp1;
+                prof[2] += tp3 - tp2;
+                prof_last = tp3;
+            } else
+#endif
             if (work) step1_closest<STATS>(S, tr, h, stk, c, lf, st);
 #else
             trav_round<STATS, KHP_WW_EXT>(S, tr, h.t, has, stk, c, st,
@@ -314,6 +349,13 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
             atomicAdd(&Wv.cnt->spills, sp_);
             atomicAdd(&Wv.cnt->iters, wit);
             atomicAdd(&Wv.cnt->lanes_busy, wbusy);
+#if KHP_PROFILE_STEPS
+            uint64_t total = __builtin_amdgcn_s_memtime() - prof_t0;
+            atomicAdd(&Wv.cnt->step_cycles[0], (unsigned long long)prof[0]);
+            atomicAdd(&Wv.cnt->step_cycles[1], (unsigned long long)prof[1]);
+            atomicAdd(&Wv.cnt->step_cycles[2], (unsigned long long)prof[2]);
+            atomicAdd(&Wv.cnt->step_cycles[3], (unsigned long long)(total - prof[0] - prof[1] - prof[2]));
+#endif
         }
     }
 }
@@ -539,7 +581,7 @@ template <bool STATS>
 __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = Wv.cnt->nsh;
-    LdsStack<RING, STATS> stk;
+    TravStack<RING, STATS> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0};
     TravRay tr;
@@ -759,6 +801,7 @@ struct khp_ctx {
     // framebuffer + pixel list
     DevMem fb, pix, stage, stage_pix, snap;   // snap: per-bounce Counters snapshots (stats renders)
     int cur_bounce = -1;
+    std::vector<float> dump;   // KHP_DUMP_BOUNCE: SoA o.xyz, d.xyz of one bounce's extension queue
     uint32_t fbW = 0, fbH = 0;
     std::vector<uint32_t> pix_host;
     uint32_t pix_key[5] = {0, 0, 0, 0, 0};
@@ -1029,6 +1072,8 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     SpillArea sp_sh{c->spill.as<int4>(), (uint32_t)c->grid_sh * 256u};
     size_t n_snap = 0;
     std::vector<uint32_t> snap_bounce;
+    const char* dump_env = getenv("KHP_DUMP_BOUNCE");
+    const int dump_b = dump_env ? atoi(dump_env) : -1;
     if (stats) {
         size_t chunks = (size_t)((P_all + P_chunk - 1) / P_chunk) * ((p->spp + S_chunk - 1) / S_chunk);
         HIPCHK(c->snap.ensure(chunks * p->depth * sizeof(Counters)));
@@ -1051,6 +1096,16 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
             for (uint32_t b = 0; b < p->depth; ++b) {
                 int cur = b & 1;
                 c->cur_bounce = (int)b;
+                if (dump_b == (int)b) {
+                    uint32_t nq = 0;
+                    HIPCHK(hipMemcpyAsync(&nq, &Wv.cnt->nq[cur], 4, hipMemcpyDeviceToHost, c->stream));
+                    HIPCHK(hipStreamSynchronize(c->stream));
+                    c->dump.resize(6 * (size_t)nq);
+                    for (int k = 0; k < 3; ++k) {
+                        HIPCHK(hipMemcpy(c->dump.data() + (size_t)k * nq, Wv.qo[cur][k], 4 * (size_t)nq, hipMemcpyDeviceToHost));
+                        HIPCHK(hipMemcpy(c->dump.data() + (size_t)(3 + k) * nq, Wv.qd[cur][k], 4 * (size_t)nq, hipMemcpyDeviceToHost));
+                    }
+                }
                 hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, c->stream, Wv.cnt, cur);
                 timed(c, 0, true);
                 if (stats)
@@ -1126,6 +1181,7 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     c->st.shadow_node_visits = hc.sh_node_visits;
     c->st.shadow_prim_tests = hc.sh_prim_tests;
     c->st.stack_spills = hc.spills;
+    for (int k = 0; k < 4; ++k) c->st.step_cycles[k] = hc.step_cycles[k];
     if (n_snap) {
         std::vector<Counters> sn(n_snap);
         HIPCHK(hipMemcpy(sn.data(), c->snap.p, n_snap * sizeof(Counters), hipMemcpyDeviceToHost));
@@ -1147,6 +1203,20 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
             prev = sn[k];
         }
     }
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_debug_queue(khp_ctx* c, uint32_t* n, float* orig, float* dir) {
+    if (!c || !n) return fail(KHP_EINVAL, "null argument");
+    const uint32_t m = (uint32_t)(c->dump.size() / 6);
+    if (orig && dir) {
+        for (uint32_t i = 0; i < m && i < *n; ++i)
+            for (int k = 0; k < 3; ++k) {
+                orig[3 * (size_t)i + k] = c->dump[(size_t)k * m + i];
+                dir[3 * (size_t)i + k] = c->dump[(size_t)(3 + k) * m + i];
+            }
+    }
+    *n = m;
     return KHP_OK;
 }
 
@@ -1214,16 +1284,20 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
     hipLaunchKernelGGL(k_load_rays, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, o.as<float>(), d.as<float>(),
                        Wv, shadow ? 1 : 0, tm.as<float>());
     const bool prod = trace_persistent() == 2;
+    hipEvent_t e0 = next_event(c), e1 = next_event(c);
+    (void)hipEventRecord(e0, c->stream);
     if (shadow) {
         SpillArea sp{c->spill.as<int4>(), (uint32_t)c->grid_sh * 256u};
         if (prod) hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp);
         else hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp);
+        (void)hipEventRecord(e1, c->stream);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(hit_out, Wv.vis, n, hipMemcpyDeviceToHost, c->stream));
     } else {
         SpillArea sp{c->spill.as<int4>(), (uint32_t)c->grid_ext * 256u};
         if (prod) hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(256), LDS_BYTES, c->stream, c->S, Wv, 0, sp);
         else hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(256), LDS_BYTES, c->stream, c->S, Wv, 0, sp);
+        (void)hipEventRecord(e1, c->stream);
         HIPCHK(t.ensure(4 * (size_t)n));
         HIPCHK(ob.ensure(4 * (size_t)n));
         HIPCHK(uv.ensure(8 * (size_t)n));
@@ -1240,6 +1314,10 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
     c->st.node_visits = shadow ? hc.sh_node_visits : hc.node_visits;
     c->st.prim_tests = shadow ? hc.sh_prim_tests : hc.prim_tests;
     c->st.stack_spills = hc.spills;
+    float kms = 0.0f;
+    (void)hipEventElapsedTime(&kms, e0, e1);
+    c->st.render_ms = kms;  // persistent query: traversal kernel time
+    c->ev_next = 0;
     return KHP_OK;
 }
 

@@ -114,6 +114,86 @@ struct LdsStack {
     }
 };
 
+// LdsStack with the top entry held in registers.  pop() returns the register
+// top at once and issues the LDS (or spill) read of the entry below it, whose
+// latency then overlaps the rest of the iteration; push() writes the old top
+// back only if it is not already in its ring slot (`clean`).
+//   entries [0, lo) live in the global spill column, [lo, sp-1) in the LDS
+//   ring, entry sp-1 (the top) in registers -- and also in its ring slot when
+//   clean.  At most R entries occupy the ring.
+template <int R, bool COUNT>
+struct LdsStackT {
+    static_assert((R & (R - 1)) == 0, "ring size must be a power of two");
+    uint32_t* lds;
+    int4* spill;
+    uint32_t stride;
+    int sp, lo;
+    uint32_t tr;
+    float ta, tb;
+    bool clean;
+    uint32_t spills;
+    __device__ __forceinline__ void init(uint32_t* lds_base, int4* spill_base, uint32_t grid_lanes) {
+        lds = lds_base;
+        spill = spill_base;
+        stride = grid_lanes;
+        sp = lo = 0;
+        clean = false;
+        spills = 0;
+    }
+    __device__ __forceinline__ void clear() {
+        sp = lo = 0;
+        clean = false;
+    }
+    __device__ __forceinline__ bool empty() const { return sp == 0; }
+    __device__ __forceinline__ uint32_t slot(int e) const { return (uint32_t)(e & (R - 1)) * 256u + threadIdx.x; }
+    __device__ __forceinline__ int4* gcell(int e) const {
+        return spill + (size_t)e * stride + blockIdx.x * blockDim.x + threadIdx.x;
+    }
+    __device__ __forceinline__ void push(uint32_t r, float a, float b) {
+        if (sp > 0 && !clean) {
+            const int e = sp - 1;
+            if (e - lo == R) {  // ring full: the oldest ring entry goes to the spill column
+                uint32_t k = slot(lo);
+                *gcell(lo) = make_int4((int)lds[k], (int)lds[k + R * 256], (int)lds[k + 2 * R * 256], 0);
+                ++lo;
+                if (COUNT) ++spills;
+            }
+            uint32_t k = slot(e);
+            lds[k] = tr;
+            lds[k + R * 256] = bits_from_f(ta);
+            lds[k + 2 * R * 256] = bits_from_f(tb);
+        }
+        tr = r;
+        ta = a;
+        tb = b;
+        clean = false;
+        ++sp;
+    }
+    __device__ __forceinline__ void pop(uint32_t& r, float& a, float& b) {
+        r = tr;
+        a = ta;
+        b = tb;
+        --sp;
+        if (sp > 0) {
+            const int e = sp - 1;
+            if (e >= lo) {
+                uint32_t k = slot(e);
+                tr = lds[k];
+                ta = f_from_bits(lds[k + R * 256]);
+                tb = f_from_bits(lds[k + 2 * R * 256]);
+                clean = true;
+            } else {
+                int4 v = *gcell(e);
+                tr = (uint32_t)v.x;
+                ta = f_from_bits((uint32_t)v.y);
+                tb = f_from_bits((uint32_t)v.z);
+                lo = e;
+                clean = false;
+            }
+        }
+    }
+};
+
 #ifndef KHP_PIN
 #define KHP_PIN 0   // 1: force whole-record loads (measured 10 % slower: the split lets lanes that fail an early-out skip the late fields)
 #endif
@@ -281,6 +361,14 @@ __device__ __forceinline__ void leaf_candidate(float4 p0, float4 p1, float4 p2, 
                                                float& lv) {
     float t, u = 0.0f, v = 0.0f;
     bool ok;
+#if KHP_EXP_DOUBLE_CONE
+    {   // timing experiment only: an extra, discarded cone test
+        float tx;
+        bool okx = cone_closest(p0, p1, p2, p3, r, 0.0f, tMax + (float)slot * 0.0f, tx);
+        float sink = okx ? tx : 0.0f;
+        asm volatile("" : "+v"(sink));
+    }
+#endif
     if (is_tri(p0)) ok = tri_test(p0, p1, p2, r, 0.0f, tMax, t, u, v);
     else ok = cone_closest(p0, p1, p2, p3, r, 0.0f, tMax, t);
     if (ok) {
@@ -449,6 +537,15 @@ __device__ __forceinline__ void interior_apply(const TravRay& tr, float4 a, floa
                                                Cur& c, TravStats& st) {
     if (STATS) st.nodes++;
     float l0, l1, r0, r1;
+#if KHP_EXP_DOUBLE_SLAB
+    {   // timing experiment only: an extra, discarded slab pair
+        float x0, x1, y0, y1;
+        bool xa = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, x0, x1);
+        bool ya = slab(b.z, b.w, cc.x, cc.y, cc.z, cc.w, tr.r, tr.inv, y0, y1);
+        float sink = (xa ? x0 : x1) + (ya ? y0 : y1);
+        asm volatile("" : "+v"(sink));
+    }
+#endif
     bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, l0, l1);
     bool rh = slab(b.z, b.w, cc.x, cc.y, cc.z, cc.w, tr.r, tr.inv, r0, r1);
     if (lh && rh) {
@@ -477,6 +574,29 @@ __device__ __forceinline__ void step1_closest(const DevScene& S, const TravRay& 
 #if KHP_PIN1
     pin(q0); pin(q1); pin(q2); pin(q3);
 #endif
+    if (lf.left > 0) {
+        if (STATS) st.prims++;
+        leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);
+        ++lf.slot;
+        if (--lf.left == 0) {
+            if (lf.sl >= 0 && lf.tl < h.t) {
+                h.t = lf.tl;
+                h.slot = lf.sl;
+                h.u = lf.lu;
+                h.v = lf.lv;
+            }
+            cur_next(stk, c);
+        }
+    } else {
+        int4 rf = make_int4(__float_as_int(q3.x), __float_as_int(q3.y), __float_as_int(q3.z), __float_as_int(q3.w));
+        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st);
+    }
+}
+
+// step1_closest on an already fetched record (diagnostic timing build).
+template <bool STATS, class Stack>
+__device__ __forceinline__ void step1_closest_rec(const TravRay& tr, Hit& h, Stack& stk, Cur& c, LeafCur& lf,
+                                                  TravStats& st, float4 q0, float4 q1, float4 q2, float4 q3) {
     if (lf.left > 0) {
         if (STATS) st.prims++;
         leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);

@@ -79,7 +79,8 @@ class Stats(ctypes.Structure):
                 ("bounce_shadow_nodes", c_uint64 * 16), ("bounce_shadow_prims", c_uint64 * 16),
                 ("bounce_extend_ms", c_double * 16), ("bounce_shadow_ms", c_double * 16),
                 ("bounce_wave_iters", c_uint64 * 16), ("bounce_lanes_busy", c_uint64 * 16),
-                ("bounce_shadow_wave_iters", c_uint64 * 16), ("bounce_shadow_lanes_busy", c_uint64 * 16)]
+                ("bounce_shadow_wave_iters", c_uint64 * 16), ("bounce_shadow_lanes_busy", c_uint64 * 16),
+                ("step_cycles", c_uint64 * 4)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if not isinstance(getattr(self, k), (int, float)) else getattr(self, k))
@@ -91,7 +92,7 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_render", "khp_read_framebuffer", "khp_trace_closest", "khp_trace_any", "khp_get_stats",
             "khp_comm_unique_id", "khp_comm_init", "khp_gather_framebuffer", "khp_bsdf_kind_from_name",
             "khp_bsdf_name", "khp_shader_kind_from_name", "khp_camera_setup", "khp_fibers_to_cones",
-            "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus", "khp_host_build"]
+            "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus", "khp_host_build", "khp_debug_queue"]
 
 _lib = None
 
@@ -140,6 +141,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
                                      P(c_float)]),
         "khp_gen_icosphere": (c_int, [c_uint32, P(c_float), c_float, P(c_float), P(c_float)]),
         "khp_gen_torus": (c_int, [c_uint32, c_uint32, P(c_float), c_float, c_float, P(c_float), P(c_float)]),
+        "khp_debug_queue": (c_int, [c_void_p, P(c_uint32), P(c_float), P(c_float)]),
         "khp_host_build": (c_int, [P(SceneDesc), P(c_uint32), P(c_uint32), P(c_float), P(c_int32), P(c_int32),
                                    P(c_int32), P(c_float), P(c_float)]),
     }

@@ -175,6 +175,9 @@ typedef struct {
      * lanes that had a record to fetch in them (busy / (64 * iters) = lane use) */
     uint64_t bounce_wave_iters[16], bounce_lanes_busy[16];
     uint64_t bounce_shadow_wave_iters[16], bounce_shadow_lanes_busy[16];
+    /* diagnostic builds (KHP_PROFILE_STEPS=1) only: k_extend wave cycles spent in
+     * resolve / record fetch / compute / loop+refill, summed over waves */
+    uint64_t step_cycles[4];
 } khp_stats;
 #define KHP_MAX_BOUNCE_STATS 16
 
@@ -236,6 +239,11 @@ khp_status khp_gather_framebuffer(khp_ctx* ctx, const khp_render_params* p, int 
 khp_status khp_host_build(const khp_scene* scene, uint32_t* n_nodes, uint32_t* depth, float* node_boxes,
                           int32_t* node_first, int32_t* node_count, int32_t* object_ids, float* obj_bounds,
                           float* records);
+
+/* Debug introspection: when the last khp_render ran with the environment
+ * variable KHP_DUMP_BOUNCE=b, the extension rays of bounce b (queue order) are
+ * kept on the host.  Call with null arrays to get *n, then with [n][3] arrays. */
+khp_status khp_debug_queue(khp_ctx* ctx, uint32_t* n, float* orig, float* dir);
 
 /* ---- registries / host helpers --------------------------------------------- */
 /* BsdfFactory::getBsdf / ShaderFactory::getShader by KIRK name; -1 if unknown
