@@ -135,14 +135,19 @@ __global__ void k_prep(Counters* c, int cur) {
 #define KHP_REFILL 16
 #endif
 #ifndef KHP_TRAV_WAVES
-#define KHP_TRAV_WAVES 5   // 96 VGPRs, no scratch; measured best (4: -9 %, 6: spills)
+#define KHP_TRAV_WAVES 6   // 65 VGPRs without SLP packing; 6 x 24 KB LDS rings fill 144 of 160 KB (measured best)
 #endif
 #ifndef KHP_SH_WAVES
 #define KHP_SH_WAVES KHP_TRAV_WAVES
 #endif
-constexpr int RING = KHP_RING;      // LDS ring entries per lane (3 x 4 B each)
+#ifndef KHP_RING_SH
+#define KHP_RING_SH KHP_RING
+#endif
+constexpr int RING = KHP_RING;        // k_extend LDS ring entries per lane (3 x 4 B each)
+constexpr int RING_SH = KHP_RING_SH;  // k_shadow
 constexpr int REFILL = KHP_REFILL;  // refill when >= REFILL lanes are idle
 constexpr size_t LDS_BYTES = 3 * RING * 256 * sizeof(uint32_t);
+constexpr size_t LDS_BYTES_SH = 3 * RING_SH * 256 * sizeof(uint32_t);
 
 #ifndef KHP_TOPREG
 #define KHP_TOPREG 0   // 1: stack top in registers with a prefetched next top (exact; measured 16 % slower)
@@ -249,6 +254,7 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
     Hit h;
     Cur c{0u, 0.0f, 0.0f, false};
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
+    Prefetch pf{0.0f, 0.0f};
     bool has = false, exhausted = false;
     uint32_t idx = 0;
     unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
@@ -322,7 +328,7 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
                 prof_last = tp3;
             } else
 #endif
-            if (work) step1_closest<STATS>(S, tr, h, stk, c, lf, st);
+            if (work) step1_closest<STATS>(S, tr, h, stk, c, lf, st, pf);
 #else
             trav_round<STATS, KHP_WW_EXT>(S, tr, h.t, has, stk, c, st,
                               [&] { leaf_step_closest<STATS>(S, tr, h, stk, c, st); }, &h.t);
@@ -581,12 +587,13 @@ template <bool STATS>
 __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = Wv.cnt->nsh;
-    TravStack<RING, STATS> stk;
+    TravStack<RING_SH, STATS> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0};
     TravRay tr;
     Cur c{0u, 0.0f, 0.0f, false};
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
+    Prefetch pf{0.0f, 0.0f};
     unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
     float tmax = 0.0f;
     bool has = false, exhausted = false;
@@ -635,7 +642,7 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
                 ++wit;
                 wbusy += (uint32_t)__popcll(wm);
             }
-            if (work && step1_any<STATS>(S, tr, tmax, stk, c, lf, st)) {
+            if (work && step1_any<STATS>(S, tr, tmax, stk, c, lf, st, pf)) {
                 Wv.vis[idx] = 1;
                 has = false;
             }
@@ -930,7 +937,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, 256, LDS_BYTES));
     c->grid_ext = std::max(1, nb) * c->n_cu;
     nb = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, 256, LDS_BYTES));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, 256, LDS_BYTES_SH));
     c->grid_sh = std::max(1, nb) * c->n_cu;
     nb = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade, 256, 0));
@@ -1118,9 +1125,9 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
                 timed(c, 1, false);
                 timed(c, 2, true);
                 if (stats)
-                    hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp_sh);
+                    hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, c->stream, c->S, Wv, sp_sh);
                 else
-                    hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp_sh);
+                    hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, c->stream, c->S, Wv, sp_sh);
                 timed(c, 2, false);
                 timed(c, 2, true);   // shadow stage = any-hit traversal + finish
                 hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, c->stream, c->S, Wv);
@@ -1288,8 +1295,8 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
     (void)hipEventRecord(e0, c->stream);
     if (shadow) {
         SpillArea sp{c->spill.as<int4>(), (uint32_t)c->grid_sh * 256u};
-        if (prod) hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp);
-        else hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES, c->stream, c->S, Wv, sp);
+        if (prod) hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, c->stream, c->S, Wv, sp);
+        else hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, c->stream, c->S, Wv, sp);
         (void)hipEventRecord(e1, c->stream);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(hit_out, Wv.vis, n, hipMemcpyDeviceToHost, c->stream));
