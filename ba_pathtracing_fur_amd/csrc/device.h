@@ -408,7 +408,15 @@ __device__ __forceinline__ v3 hair_r(const ShadeCtx& s, v3 in, v3 n, float sampl
 
 // BSDF::sample (Bsdf.cpp:179-184) + localSample dispatch; valid=false on the
 // `dot(ray_in, normal) == 0` early exit.
-__device__ __noinline__ v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float h1, v3& out,
+#ifndef KHP_BSDF_INLINE
+#define KHP_BSDF_INLINE 0
+#endif
+#if KHP_BSDF_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float h1, v3& out,
                                        float& pdf, int& flags, bool& valid) {
     v3 zero = mk(0.0f, 0.0f, 0.0f);
     valid = true;

@@ -29,10 +29,16 @@ using namespace khp;
 // ============================================================================
 //  wavefront state
 // ============================================================================
-struct Counters {
+#ifndef KHP_MAX_SEG
+#define KHP_MAX_SEG 64
+#endif
+struct alignas(128) Counters {
     uint32_t nq[2];        // ray queue sizes
+    uint32_t pad_a[30];
     uint32_t nsh;          // shadow queue size
-    uint32_t fetch_ext[8], fetch_sh[8];   // queue-segment claim cursors (one per XCD group)
+    uint32_t pad_b[31];
+    uint32_t fetch_ext[KHP_MAX_SEG * 32];  // queue-segment claim cursors, one 128-B line each
+    uint32_t fetch_sh[KHP_MAX_SEG * 32];
     uint32_t pad[3];
     unsigned long long ext_rays, sh_rays;
     unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests, spills;
@@ -116,9 +122,9 @@ __global__ void k_prep(Counters* c, int cur) {
     c->sh_rays += c->nsh;   // shadow rays of the previous bounce
     c->nq[nxt] = 0;
     c->nsh = 0;
-    for (int g = 0; g < 8; ++g) {
-        c->fetch_ext[g] = 0;
-        c->fetch_sh[g] = 0;
+    for (int g = 0; g < KHP_MAX_SEG; ++g) {
+        c->fetch_ext[32 * g] = 0;
+        c->fetch_sh[32 * g] = 0;
     }
     c->ext_rays += c->nq[cur];
 }
@@ -170,7 +176,10 @@ struct SpillArea {
 #ifndef KHP_XCD_SPLIT
 #define KHP_XCD_SPLIT 1
 #endif
-constexpr uint32_t NSEG = KHP_XCD_SPLIT ? 8u : 1u;
+#ifndef KHP_SEG_PER_XCD
+#define KHP_SEG_PER_XCD 4   // sub-segments per XCD group: spreads claim atomics over more lines
+#endif
+constexpr uint32_t NSEG = KHP_XCD_SPLIT ? 8u * KHP_SEG_PER_XCD : 1u;
 
 struct Claimer {
     uint32_t* fetch;  // NSEG cursors
@@ -180,7 +189,8 @@ struct Claimer {
     __device__ __forceinline__ void init(uint32_t* f, uint32_t len) {
         fetch = f;
         n = len;
-        sg = NSEG > 1 ? blockIdx.x % NSEG : 0u;
+        // group g = blockIdx % 8 (one XCD) owns the contiguous segments [g*K, g*K + K)
+        sg = NSEG > 1 ? (blockIdx.x % 8u) * (NSEG / 8u) + (blockIdx.x / 8u) % (NSEG / 8u) : 0u;
         tried = 0;
     }
     __device__ __forceinline__ uint32_t lo(uint32_t g) const { return (uint32_t)((uint64_t)n * g / NSEG); }
@@ -190,7 +200,7 @@ struct Claimer {
         const uint32_t lane = lane_id();
         const uint32_t k = (uint32_t)__popcll(idle);
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&fetch[sg], k);
+        if (lane == 0) base = atomicAdd(&fetch[32 * sg], k);
         base = __shfl(base, 0);
         const uint32_t s0 = lo(sg), len = lo(sg + 1) - s0;
         const uint32_t off = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
@@ -368,11 +378,54 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
 
 // ---- shade: traceRay light test + shaders (CPU_PathTracer.cpp:141-208; SimpleShader.h;
 //      MarschnerHairShader.h; LightShader.h; EnvironmentShader.h) ------------------------
-__global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
+// Block-aggregated queue allocation for the two outputs of k_shade: one
+// atomic per 256-thread block and queue instead of one per wave.  Device-scope
+// atomics on a single counter serialize across the XCDs; with wave-level
+// allocation k_shade spent most of its time waiting on them.
+#ifndef KHP_BLOCK_ALLOC
+#define KHP_BLOCK_ALLOC 1
+#endif
+struct BlockAlloc2 {
+    uint32_t wcnt[2][4];
+    uint32_t base[2];
+};
+__device__ __forceinline__ void block_alloc2(bool p0, bool p1, uint32_t* c0, uint32_t* c1, BlockAlloc2& sh,
+                                             uint32_t& i0, uint32_t& i1) {
+    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+    const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (lane == 0) {
+        sh.wcnt[0][wid] = (uint32_t)__popcll(m0);
+        sh.wcnt[1][wid] = (uint32_t)__popcll(m1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const uint32_t q = threadIdx.x;
+        const uint32_t tot = sh.wcnt[q][0] + sh.wcnt[q][1] + sh.wcnt[q][2] + sh.wcnt[q][3];
+        sh.base[q] = tot ? atomicAdd(q == 0 ? c0 : c1, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t o0 = sh.base[0], o1 = sh.base[1];
+    for (uint32_t w = 0; w < wid; ++w) {
+        o0 += sh.wcnt[0][w];
+        o1 += sh.wcnt[1][w];
+    }
+    i0 = o0 + (uint32_t)__popcll(m0 & lt);
+    i1 = o1 + (uint32_t)__popcll(m1 & lt);
+    __syncthreads();  // sh is reused by the next iteration
+}
+
+#ifndef KHP_SHADE_WAVES
+#define KHP_SHADE_WAVES 1
+#endif
+__global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
     const uint32_t n = Wv.cnt->nq[cur];
     const int nxt = cur ^ 1;
     const bool last = bounce + 1 >= Wv.depth;
     const uint32_t stride = gridDim.x * blockDim.x;
+#if KHP_BLOCK_ALLOC
+    __shared__ BlockAlloc2 balloc;
+#endif
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {
         uint32_t i = base + threadIdx.x;
         bool active = i < n;
@@ -527,13 +580,20 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
             Wv.flags[pid] = flags;
             emit_ray = !last && !is_zero(T) && !is_zero(nr.d);
         }
+#if KHP_BLOCK_ALLOC
+        uint32_t qi, si;
+        block_alloc2(emit_ray, emit_sh, &Wv.cnt->nq[nxt], &Wv.cnt->nsh, balloc, qi, si);
+#else
         uint32_t qi = wave_alloc(emit_ray, &Wv.cnt->nq[nxt]);
+#endif
         if (emit_ray) {
             Wv.qo[nxt][0][qi] = nr.o.x; Wv.qo[nxt][1][qi] = nr.o.y; Wv.qo[nxt][2][qi] = nr.o.z;
             Wv.qd[nxt][0][qi] = nr.d.x; Wv.qd[nxt][1][qi] = nr.d.y; Wv.qd[nxt][2][qi] = nr.d.z;
             Wv.qpid[nxt][qi] = pid;
         }
+#if !KHP_BLOCK_ALLOC
         uint32_t si = wave_alloc(emit_sh, &Wv.cnt->nsh);
+#endif
         if (emit_sh) {
             float4* rec = Wv.sh + 6 * (size_t)si;
             rec[0] = make_float4(shr.o.x, shr.o.y, shr.o.z, sh_tmax);
