@@ -35,15 +35,20 @@ using namespace khp;
 struct alignas(128) Counters {
     uint32_t nq[2];        // ray queue sizes
     uint32_t pad_a[30];
-    uint32_t nsh;          // shadow queue size
-    uint32_t pad_b[31];
     uint32_t fetch_ext[KHP_MAX_SEG * 32];  // queue-segment claim cursors, one 128-B line each
-    uint32_t fetch_sh[KHP_MAX_SEG * 32];
-    uint32_t pad[3];
     unsigned long long ext_rays, sh_rays;
     unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests, spills;
     unsigned long long iters, lanes_busy, sh_iters, sh_lanes_busy;  // wave iterations, lanes with work
     unsigned long long step_cycles[4];  // KHP_PROFILE_STEPS: resolve, fetch, compute, loop/refill (extend)
+};
+
+// One bounce's shadow-ray queue (count + claim cursors).  Two of them
+// (bounce parity) let k_shade of bounce b+1 fill one while k_shadow of bounce
+// b drains the other on the second stream.
+struct alignas(128) ShadowQ {
+    uint32_t nsh;
+    uint32_t pad[31];
+    uint32_t fetch[KHP_MAX_SEG * 32];
 };
 
 struct Wave {
@@ -58,7 +63,8 @@ struct Wave {
     float* C[3];
     int32_t* flags;
     uint32_t* key;
-    uint8_t* vis;        // shadow-ray occlusion flag per shadow record
+    uint8_t* vis;        // shadow-ray occlusion flag per shadow record (this parity)
+    ShadowQ* shq;        // shadow queue of this parity
     float4* sh;          // 6 float4 per shadow record
     Counters* cnt;
     const uint32_t* pix;  // owned pixel ids (y*W+x)
@@ -117,14 +123,13 @@ __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
     Wv.key[pid] = key;
 }
 
-__global__ void k_prep(Counters* c, int cur) {
+__global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
     int nxt = cur ^ 1;
-    c->sh_rays += c->nsh;   // shadow rays of the previous bounce
     c->nq[nxt] = 0;
-    c->nsh = 0;
+    q->nsh = 0;
     for (int g = 0; g < KHP_MAX_SEG; ++g) {
         c->fetch_ext[32 * g] = 0;
-        c->fetch_sh[32 * g] = 0;
+        q->fetch[32 * g] = 0;
     }
     c->ext_rays += c->nq[cur];
 }
@@ -181,35 +186,53 @@ struct SpillArea {
 #endif
 constexpr uint32_t NSEG = KHP_XCD_SPLIT ? 8u * KHP_SEG_PER_XCD : 1u;
 
+#ifndef KHP_CLAIM_CHUNK
+#define KHP_CLAIM_CHUNK 0   // >0: indices a wave reserves per atomic (measured: no gain once cursors are line-padded)
+#endif
 struct Claimer {
-    uint32_t* fetch;  // NSEG cursors
+    uint32_t* fetch;  // NSEG cursors, one 128-B line each
     uint32_t n;       // queue length
     uint32_t sg;      // segment this wave is draining (wave-uniform)
     uint32_t tried;   // segments found exhausted
+    uint32_t res_lo, res_hi;  // reserved, not yet handed out (KHP_CLAIM_CHUNK)
     __device__ __forceinline__ void init(uint32_t* f, uint32_t len) {
         fetch = f;
         n = len;
         // group g = blockIdx % 8 (one XCD) owns the contiguous segments [g*K, g*K + K)
         sg = NSEG > 1 ? (blockIdx.x % 8u) * (NSEG / 8u) + (blockIdx.x / 8u) % (NSEG / 8u) : 0u;
         tried = 0;
+        res_lo = res_hi = 0;
     }
     __device__ __forceinline__ uint32_t lo(uint32_t g) const { return (uint32_t)((uint64_t)n * g / NSEG); }
-    // Claims popc(idle) indices for the idle lanes; returns true for this lane
-    // if it received one (my).  Sets done when every segment is drained.
+    // Reserve up to `want` indices from the current segment (moving on when it runs dry).
+    __device__ __forceinline__ void reserve(uint32_t want) {
+        while (res_lo >= res_hi && tried < NSEG) {
+            uint32_t base = 0;
+            if (lane_id() == 0) base = atomicAdd(&fetch[32 * sg], want);
+            base = __shfl(base, 0);
+            const uint32_t s0 = lo(sg), len = lo(sg + 1) - s0;
+            if (base < len) {
+                res_lo = s0 + base;
+                res_hi = s0 + (base + want < len ? base + want : len);
+            }
+            if (base + want >= len) {
+                sg = (sg + 1) % NSEG;
+                ++tried;
+            }
+        }
+    }
+    // Hands indices to the idle lanes; returns true for this lane if it got one (my).
+    // Sets done once every segment is drained and the reservoir is empty.
     __device__ __forceinline__ bool claim(unsigned long long idle, uint32_t& my, bool& done) {
         const uint32_t lane = lane_id();
         const uint32_t k = (uint32_t)__popcll(idle);
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&fetch[32 * sg], k);
-        base = __shfl(base, 0);
-        const uint32_t s0 = lo(sg), len = lo(sg + 1) - s0;
-        const uint32_t off = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-        my = s0 + off;
-        const bool got = off < len;
-        if (base + k >= len) {
-            sg = (sg + 1) % NSEG;
-            if (++tried == NSEG) done = true;
-        }
+        reserve(KHP_CLAIM_CHUNK > 0 && KHP_CLAIM_CHUNK > k ? (uint32_t)KHP_CLAIM_CHUNK : k);
+        const uint32_t avail = res_hi - res_lo, take = k < avail ? k : avail;
+        const uint32_t off = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+        my = res_lo + off;
+        const bool got = (idle >> lane & 1ull) && off < take;
+        res_lo += take;
+        if (tried >= NSEG && res_lo >= res_hi) done = true;
         return got;
     }
 };
@@ -582,7 +605,7 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
         }
 #if KHP_BLOCK_ALLOC
         uint32_t qi, si;
-        block_alloc2(emit_ray, emit_sh, &Wv.cnt->nq[nxt], &Wv.cnt->nsh, balloc, qi, si);
+        block_alloc2(emit_ray, emit_sh, &Wv.cnt->nq[nxt], &Wv.shq->nsh, balloc, qi, si);
 #else
         uint32_t qi = wave_alloc(emit_ray, &Wv.cnt->nq[nxt]);
 #endif
@@ -592,7 +615,7 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
             Wv.qpid[nxt][qi] = pid;
         }
 #if !KHP_BLOCK_ALLOC
-        uint32_t si = wave_alloc(emit_sh, &Wv.cnt->nsh);
+        uint32_t si = wave_alloc(emit_sh, &Wv.shq->nsh);
 #endif
         if (emit_sh) {
             float4* rec = Wv.sh + 6 * (size_t)si;
@@ -611,7 +634,8 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
 // k_shadow_finish: one shadow record per lane, streaming; kept out of the
 // traversal kernel so k_shadow's registers go to traversal only.
 __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
-    const uint32_t n = Wv.cnt->nsh;
+    const uint32_t n = Wv.shq->nsh;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Wv.cnt->sh_rays, (unsigned long long)n);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const float4* rec = Wv.sh + 6 * (size_t)i;
         float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3], e = rec[4];
@@ -646,7 +670,7 @@ __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
 template <bool STATS>
 __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
     extern __shared__ uint32_t lds[];
-    const uint32_t n = Wv.cnt->nsh;
+    const uint32_t n = Wv.shq->nsh;
     TravStack<RING_SH, STATS> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0};
@@ -661,7 +685,7 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
     bool found = false;
 #endif
     Claimer cl;
-    cl.init(Wv.cnt->fetch_sh, n);
+    cl.init(Wv.shq->fetch, n);
     uint32_t idx = 0;
     for (;;) {
         unsigned long long idle = __ballot(!has);
@@ -734,10 +758,6 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
 }
 
 // ---- accumulate: PathTracer::drawTexture running mean (CPU_PathTracer.cpp:61-90) -------
-__global__ void k_tail(Counters* c) {
-    c->sh_rays += c->nsh;
-    c->nsh = 0;
-}
 
 __global__ __launch_bounds__(256) void k_accumulate(Wave Wv, float* fb) {
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -857,6 +877,8 @@ struct khp_ctx {
     int device = 0;
     uint32_t flags = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;   // shadow stage of bounce b beside extend of bounce b+1
+    std::vector<hipEvent_t> sync_pool;  // ordering events (no timing)
     int n_cu = 256;
     HostScene hs;
     bool scene_set = false, built = false;
@@ -864,7 +886,7 @@ struct khp_ctx {
     DevScene S{};
     // wavefront
     size_t cap = 0;
-    DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb, visb, cnt, spill;
+    DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
     // framebuffer + pixel list
     DevMem fb, pix, stage, stage_pix, snap;   // snap: per-bounce Counters snapshots (stats renders)
     int cur_bounce = -1;
@@ -894,6 +916,16 @@ static hipEvent_t next_event(khp_ctx* c) {
     return c->ev_pool[c->ev_next++];
 }
 
+// Ordering event k of this render (created once, reused across renders).
+static hipEvent_t sync_event(khp_ctx* c, size_t k) {
+    while (c->sync_pool.size() <= k) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        c->sync_pool.push_back(e);
+    }
+    return c->sync_pool[k];
+}
+
 extern "C" int khp_abi_version(void) { return KHP_ABI_VERSION; }
 extern "C" const char* khp_last_error(void) { return last_error(); }
 
@@ -909,7 +941,9 @@ extern "C" khp_status khp_create(khp_ctx** out, int device, uint32_t flags) {
     c->flags = flags;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+        if (c->stream) (void)hipStreamDestroy(c->stream);
         delete c;
         return fail(KHP_EDEVICE, "hipStreamCreate failed");
     }
@@ -922,7 +956,10 @@ extern "C" void khp_destroy(khp_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    for (auto e : c->sync_pool) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1020,12 +1057,16 @@ static khp_status ensure_wave(khp_ctx* c, size_t cap) {
     }
     HIPCHK(c->flagsb.ensure(cap * 4));
     HIPCHK(c->keyb.ensure(cap * 4));
-    HIPCHK(c->visb.ensure(cap));
-    HIPCHK(c->shb.ensure(cap * 6 * sizeof(float4)));
+    for (int q = 0; q < 2; ++q) {
+        HIPCHK(c->visb[q].ensure(cap));
+        HIPCHK(c->shb[q].ensure(cap * 6 * sizeof(float4)));
+    }
+    HIPCHK(c->shqb.ensure(2 * sizeof(ShadowQ)));
     HIPCHK(c->cnt.ensure(sizeof(Counters)));
     // traversal-stack spill columns: one per resident lane, STACK_MAX entries deep
-    size_t lanes = (size_t)std::max(c->grid_ext, c->grid_sh) * 256;
-    HIPCHK(c->spill.ensure(lanes * STACK_MAX * sizeof(int4)));
+    // separate spill columns: k_extend and k_shadow may run at the same time
+    HIPCHK(c->spill.ensure((size_t)c->grid_ext * 256 * STACK_MAX * sizeof(int4)));
+    HIPCHK(c->spill_sh.ensure((size_t)c->grid_sh * 256 * STACK_MAX * sizeof(int4)));
     c->cap = cap;
     return KHP_OK;
 }
@@ -1050,8 +1091,9 @@ static Wave wave_view(khp_ctx* c) {
     }
     Wv.flags = c->flagsb.as<int32_t>();
     Wv.key = c->keyb.as<uint32_t>();
-    Wv.vis = c->visb.as<uint8_t>();
-    Wv.sh = c->shb.as<float4>();
+    Wv.vis = c->visb[0].as<uint8_t>();
+    Wv.sh = c->shb[0].as<float4>();
+    Wv.shq = c->shqb.as<ShadowQ>();
     Wv.cnt = c->cnt.as<Counters>();
     return Wv;
 }
@@ -1097,10 +1139,10 @@ static khp_status check_params(khp_ctx* c, const khp_render_params* p) {
     return KHP_OK;
 }
 
-static void timed(khp_ctx* c, int kind, bool begin) {
+static void timed(khp_ctx* c, int kind, bool begin, hipStream_t st = nullptr) {
     hipEvent_t e = next_event(c);
     if (!e) return;
-    (void)hipEventRecord(e, c->stream);
+    (void)hipEventRecord(e, st ? st : c->stream);
     if (begin) c->launches.push_back(TimedLaunch{kind, c->cur_bounce, e, nullptr});
     else c->launches.back().b = e;
 }
@@ -1136,7 +1178,8 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     Wv.seed = p->seed;
     Wv.depth = p->depth;
     SpillArea sp_ext{c->spill.as<int4>(), (uint32_t)c->grid_ext * 256u};
-    SpillArea sp_sh{c->spill.as<int4>(), (uint32_t)c->grid_sh * 256u};
+    SpillArea sp_sh{c->spill_sh.as<int4>(), (uint32_t)c->grid_sh * 256u};
+    HIPCHK(hipMemsetAsync(c->shqb.p, 0, 2 * sizeof(ShadowQ), c->stream));
     size_t n_snap = 0;
     std::vector<uint32_t> snap_bounce;
     const char* dump_env = getenv("KHP_DUMP_BOUNCE");
@@ -1145,9 +1188,25 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
         size_t chunks = (size_t)((P_all + P_chunk - 1) / P_chunk) * ((p->spp + S_chunk - 1) / S_chunk);
         HIPCHK(c->snap.ensure(chunks * p->depth * sizeof(Counters)));
     }
+    // Two streams: A runs generate / extend / shade / accumulate, B runs the
+    // shadow stage (k_shadow + k_shadow_finish) of bounce b while A already
+    // traverses bounce b+1, so each persistent kernel's tail fills with the
+    // other's blocks.  Ordering: B(b) after shade(b) on A; shade(b+1) after
+    // B(b) (both update the path colour C in bounce order); the shadow queue
+    // of bounce b+2 reuses parity b's buffers only after shade(b+1), which
+    // already waited for B(b).  Instrumented renders stay on one stream so the
+    // per-bounce counter snapshots are exact.
+    const bool overlap = !stats && !getenv("KHP_NO_OVERLAP");
+    hipStream_t sA = c->stream, sB = overlap ? c->stream2 : c->stream;
+    size_t n_sync = 0;
     c->cur_bounce = -1;
     hipEvent_t ev_start = next_event(c);
-    (void)hipEventRecord(ev_start, c->stream);
+    (void)hipEventRecord(ev_start, sA);
+    if (overlap) {
+        hipEvent_t e0 = sync_event(c, n_sync++);
+        HIPCHK(hipEventRecord(e0, sA));
+        HIPCHK(hipStreamWaitEvent(sB, e0, 0));
+    }
     for (uint32_t p0 = 0; p0 < P_all; p0 += P_chunk) {
         uint32_t P = std::min(P_chunk, P_all - p0);
         for (uint32_t s0 = 0; s0 < p->spp; s0 += S_chunk) {
@@ -1157,53 +1216,74 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
             Wv.sample0 = p->first_sample + s0;
             Wv.n_samples = ns;
             uint32_t npaths = P * ns;
-            timed(c, 3, true);
-            hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, c->stream, c->S, Wv);
-            timed(c, 3, false);
+            timed(c, 3, true, sA);
+            hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wv);
+            timed(c, 3, false, sA);
+            hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
             for (uint32_t b = 0; b < p->depth; ++b) {
                 int cur = b & 1;
+                const int par = b & 1;
                 c->cur_bounce = (int)b;
+                Wave Wb = Wv;
+                Wb.sh = c->shb[par].as<float4>();
+                Wb.vis = c->visb[par].as<uint8_t>();
+                Wb.shq = c->shqb.as<ShadowQ>() + par;
                 if (dump_b == (int)b) {
                     uint32_t nq = 0;
-                    HIPCHK(hipMemcpyAsync(&nq, &Wv.cnt->nq[cur], 4, hipMemcpyDeviceToHost, c->stream));
-                    HIPCHK(hipStreamSynchronize(c->stream));
+                    HIPCHK(hipMemcpyAsync(&nq, &Wv.cnt->nq[cur], 4, hipMemcpyDeviceToHost, sA));
+                    HIPCHK(hipStreamSynchronize(sA));
                     c->dump.resize(6 * (size_t)nq);
                     for (int k = 0; k < 3; ++k) {
                         HIPCHK(hipMemcpy(c->dump.data() + (size_t)k * nq, Wv.qo[cur][k], 4 * (size_t)nq, hipMemcpyDeviceToHost));
                         HIPCHK(hipMemcpy(c->dump.data() + (size_t)(3 + k) * nq, Wv.qd[cur][k], 4 * (size_t)nq, hipMemcpyDeviceToHost));
                     }
                 }
-                hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, c->stream, Wv.cnt, cur);
-                timed(c, 0, true);
+                hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
+                timed(c, 0, true, sA);
                 if (stats)
-                    hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(256), LDS_BYTES, c->stream, c->S, Wv, cur, sp_ext);
+                    hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(256), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
                 else
-                    hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(256), LDS_BYTES, c->stream, c->S, Wv, cur, sp_ext);
-                timed(c, 0, false);
-                timed(c, 1, true);
-                hipLaunchKernelGGL(k_shade, dim3(c->grid_shade), dim3(256), 0, c->stream, c->S, Wv, cur, b);
-                timed(c, 1, false);
-                timed(c, 2, true);
+                    hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(256), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                timed(c, 0, false, sA);
+                if (done_b) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
+                timed(c, 1, true, sA);
+                hipLaunchKernelGGL(k_shade, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                timed(c, 1, false, sA);
+                if (overlap) {
+                    hipEvent_t shaded = sync_event(c, n_sync++);
+                    HIPCHK(hipEventRecord(shaded, sA));
+                    HIPCHK(hipStreamWaitEvent(sB, shaded, 0));
+                }
+                timed(c, 2, true, sB);
                 if (stats)
-                    hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, c->stream, c->S, Wv, sp_sh);
+                    hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, sB, c->S, Wb, sp_sh);
                 else
-                    hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, c->stream, c->S, Wv, sp_sh);
-                timed(c, 2, false);
-                timed(c, 2, true);   // shadow stage = any-hit traversal + finish
-                hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, c->stream, c->S, Wv);
-                timed(c, 2, false);
+                    hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, sB, c->S, Wb, sp_sh);
+                timed(c, 2, false, sB);
+                timed(c, 2, true, sB);   // shadow stage = any-hit traversal + finish
+                hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
+                timed(c, 2, false, sB);
+                if (overlap) {
+                    done_b = sync_event(c, n_sync++);
+                    HIPCHK(hipEventRecord(done_b, sB));
+                }
                 if (stats) {
                     HIPCHK(hipMemcpyAsync(c->snap.as<Counters>() + n_snap, c->cnt.p, sizeof(Counters),
-                                          hipMemcpyDeviceToDevice, c->stream));
+                                          hipMemcpyDeviceToDevice, sA));
                     snap_bounce.push_back(b);
                     ++n_snap;
                 }
             }
             c->cur_bounce = -1;
-            hipLaunchKernelGGL(k_tail, dim3(1), dim3(1), 0, c->stream, Wv.cnt);
-            timed(c, 3, true);
-            hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, c->stream, Wv, c->fb.as<float>());
-            timed(c, 3, false);
+            if (done_b) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
+            timed(c, 3, true, sA);
+            hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, c->fb.as<float>());
+            timed(c, 3, false, sA);
+            if (overlap) {  // the next chunk's shadow stages come after this chunk's accumulate
+                hipEvent_t acc = sync_event(c, n_sync++);
+                HIPCHK(hipEventRecord(acc, sA));
+                HIPCHK(hipStreamWaitEvent(sB, acc, 0));
+            }
         }
     }
     hipEvent_t ev_end = next_event(c);
@@ -1259,7 +1339,7 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
                 c->st.bounce_rays[b] += sn[k].ext_rays - prev.ext_rays;
                 c->st.bounce_nodes[b] += sn[k].node_visits - prev.node_visits;
                 c->st.bounce_prims[b] += sn[k].prim_tests - prev.prim_tests;
-                c->st.bounce_shadow_rays[b] += sn[k].nsh;
+                c->st.bounce_shadow_rays[b] += sn[k].sh_rays - prev.sh_rays;
                 c->st.bounce_shadow_nodes[b] += sn[k].sh_node_visits - prev.sh_node_visits;
                 c->st.bounce_shadow_prims[b] += sn[k].sh_prim_tests - prev.sh_prim_tests;
                 c->st.bounce_wave_iters[b] += sn[k].iters - prev.iters;
@@ -1306,7 +1386,7 @@ __global__ void k_load_rays(uint32_t n, const float* orig, const float* dir, Wav
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) {
         Wv.cnt->nq[0] = as_shadow ? 0u : n;
-        Wv.cnt->nsh = as_shadow ? n : 0u;
+        Wv.shq->nsh = as_shadow ? n : 0u;
     }
     if (i >= n) return;
     Ray r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
@@ -1347,6 +1427,7 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
     HIPCHK(upload(d, dir, 3 * (size_t)n, c->stream));
     if (shadow) HIPCHK(upload(tm, tmax_h, (size_t)n, c->stream));
     HIPCHK(hipMemsetAsync(c->cnt.p, 0, sizeof(Counters), c->stream));
+    HIPCHK(hipMemsetAsync(c->shqb.p, 0, 2 * sizeof(ShadowQ), c->stream));
     Wave Wv = wave_view(c);
     hipLaunchKernelGGL(k_load_rays, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, o.as<float>(), d.as<float>(),
                        Wv, shadow ? 1 : 0, tm.as<float>());
@@ -1354,7 +1435,7 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
     hipEvent_t e0 = next_event(c), e1 = next_event(c);
     (void)hipEventRecord(e0, c->stream);
     if (shadow) {
-        SpillArea sp{c->spill.as<int4>(), (uint32_t)c->grid_sh * 256u};
+        SpillArea sp{c->spill_sh.as<int4>(), (uint32_t)c->grid_sh * 256u};
         if (prod) hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, c->stream, c->S, Wv, sp);
         else hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, c->stream, c->S, Wv, sp);
         (void)hipEventRecord(e1, c->stream);
