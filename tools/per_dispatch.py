@@ -1,7 +1,7 @@
 """Per-dispatch view of a profile dir: python tools/per_dispatch.py gpurun_out/prof_<tag> [passes...]"""
 import csv, collections, sys
 src = sys.argv[1]
-passes = sys.argv[2:] or ["ta", "tas", "tcp", "tcpa", "sq", "lat", "ea", "tcc"]
+passes = sys.argv[2:] or ["ta", "tas", "tcp", "tcpa", "sq", "lat", "ea", "tcc", "mix", "mix2"]
 per = collections.defaultdict(lambda: collections.defaultdict(dict))
 for p in passes:
     try:
@@ -23,7 +23,10 @@ for k, dd in per.items():
                                ("TCP_PENDING_STALL_CYCLES_sum", "tcp", 256)):
             if cn in v and "GRBM_GUI_ACTIVE@" + pas in v:
                 out.append(f"{cn.split('_sum')[0].split('_avr')[0]}={v[cn] / v['GRBM_GUI_ACTIVE@' + pas] / scale:.2f}")
-        for cn in ("TCP_TOTAL_CACHE_ACCESSES_sum", "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"):
+        for cn in ("TCP_TOTAL_CACHE_ACCESSES_sum", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH",
+                   "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
+                   "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS",
+                   "SQ_WAIT_INST_LDS", "SQ_INSTS_VALU_TRANS_F32"):
             if cn in v:
                 out.append(f"{cn}={v[cn]:.3g}")
         print(" ".join(out))
