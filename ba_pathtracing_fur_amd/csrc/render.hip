@@ -781,6 +781,138 @@ __global__ __launch_bounds__(256) void k_accumulate(Wave Wv, float* fb) {
     o[0] = r; o[1] = g; o[2] = b;
 }
 
+// ---- output stage: Texture::setPixel byte conversion and Tonemapper::map ---------------
+// Texture::toByte (Texture.h:252-254): (uchar)std::max(std::min(f * 255, 255), 0).
+// std::min(a, b) = (b < a) ? b : a and std::max(a, b) = (a < b) ? b : a, so a
+// NaN passes both and its conversion is undefined in C++; x86 and gfx950 both
+// give 0, which is the value used here.
+__device__ __forceinline__ uint8_t to_byte(float f) {
+    const float a = f * 255.0f;
+    const float lo = (255.0f < a) ? 255.0f : a;
+    const float v = (lo < 0.0f) ? 0.0f : lo;
+    return (v == v) ? (uint8_t)(uint32_t)v : (uint8_t)0;
+}
+
+__global__ void k_rgba8(const float* fb, uint32_t n, uint8_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* c = fb + 3 * (size_t)i;
+    uchar4 o = make_uchar4(to_byte(c[0]), to_byte(c[1]), to_byte(c[2]), 255);
+    reinterpret_cast<uchar4*>(out)[i] = o;
+}
+
+// Tonemapper::RGB_to_Yxy (Tonemapping.cpp): per pixel Yxy, the max luminance
+// (glm::max, NaN-ignoring) and the log-luminance sum.  KIRK accumulates the
+// sum sequentially in float; this sums in double in parallel (stated tolerance
+// in tests/test_output.py).
+__device__ __forceinline__ float gdot3(float a0, float a1, float a2, float b0, float b1, float b2) {
+    return (a0 * b0 + a1 * b1) + a2 * b2;  // glm::dot operand order
+}
+__global__ __launch_bounds__(256) void k_tm_yxy(const float* fb, uint32_t n, float* yxy, float* bmax, double* bsum) {
+    __shared__ float smax[256];
+    __shared__ double ssum[256];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    float Y = 0.0f, xx = 0.0f, yy = 0.0f, mx = 1e-06f;
+    double lg = 0.0;
+    if (i < n) {
+        const float r = fb[3 * (size_t)i], g = fb[3 * (size_t)i + 1], b = fb[3 * (size_t)i + 2];
+        const float X = gdot3(0.5141364f, 0.3238786f, 0.16036376f, r, g, b);
+        const float Yv = gdot3(0.265068f, 0.67023428f, 0.06409157f, r, g, b);
+        const float Z = gdot3(0.0241188f, 0.1228178f, 0.84442666f, r, g, b);
+        const float W = gdot3(X, Yv, Z, 1.0f, 1.0f, 1.0f);
+        if (W > 0.0f) {
+            Y = Yv;
+            xx = X / W;
+            yy = Yv / W;
+        }
+        mx = (mx < Y) ? Y : mx;
+        lg = log(2.3e-5 + (double)Y);
+        yxy[3 * (size_t)i] = Y;
+        yxy[3 * (size_t)i + 1] = xx;
+        yxy[3 * (size_t)i + 2] = yy;
+    }
+    smax[threadIdx.x] = mx;
+    ssum[threadIdx.x] = lg;
+    __syncthreads();
+    for (uint32_t w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            const float o = smax[threadIdx.x + w];
+            smax[threadIdx.x] = (smax[threadIdx.x] < o) ? o : smax[threadIdx.x];
+            ssum[threadIdx.x] += ssum[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        bmax[blockIdx.x] = smax[0];
+        bsum[blockIdx.x] = ssum[0];
+    }
+}
+
+// Tonemapper::luminance_from_center (Tonemapping.cpp:183-245): the log-sum of
+// the Gaussian-weighted window, with the reference's i1 = x*(y_start+ks)+y
+// indexing.  mask (ks*ks doubles) and `mean` are built on the host.
+__global__ __launch_bounds__(256) void k_tm_center(const float* yxy, int ks, int xs, int ys, const double* mask,
+                                                   double mean, double* bsum) {
+    __shared__ double ssum[256];
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    double lg = 0.0;
+    if (t < ks * ks) {
+        const int i = t / ks, j = t % ks;
+        const int i1 = (xs + i) * (ys + ks) + (ys + j);
+        lg = log(2.3e-5 + (double)yxy[3 * (size_t)i1] * mask[j * ks + i] * mean);
+    }
+    ssum[threadIdx.x] = lg;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) ssum[threadIdx.x] += ssum[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bsum[blockIdx.x] = ssum[0];
+}
+
+struct TmScalars {
+    float av_lum, biasP, contP, Lmax, divider, exposure, inv_gamma, slope, start, white, black;
+    int contrast_on, gamma_on, rec, clamp_on;
+};
+
+// Tonemapper::tonemapping + Yxy_to_RGB + gamma_calc / rec_gamma_calc + clamp,
+// then Texture::setPixel(vec4(rgb, 1)).
+__global__ __launch_bounds__(256) void k_tm_map(const float* yxy, uint32_t n, TmScalars t, uint8_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float v = yxy[3 * (size_t)i];
+    const float xc = yxy[3 * (size_t)i + 1], yc = yxy[3 * (size_t)i + 2];
+    if (t.contrast_on) v = powf(v, t.contP);
+    v /= t.av_lum;
+    v *= t.exposure;
+    const float bias = (float)pow((double)(v / t.Lmax), (double)t.biasP);
+    const float interpol = logf(2.0f + bias * 8.0f);
+    v = logf(v + 1.0f) / interpol / t.divider;
+    const float eps = 1e-06f;
+    float X, Z;
+    if (v > eps && xc > eps && yc > eps) {
+        X = xc * v / yc;
+        Z = X / xc - X - v;
+    } else {
+        X = Z = eps;
+    }
+    float rgb[3] = {gdot3(2.5651f, -1.1665f, -0.3986f, X, v, Z), gdot3(-1.0217f, 1.9777f, 0.0439f, X, v, Z),
+                    gdot3(0.0753f, -0.2543f, 1.1892f, X, v, Z)};
+    for (int k = 0; k < 3; ++k) {
+        float c = rgb[k];
+        if (t.gamma_on) {
+            if (t.rec) c = c <= t.start ? c * t.slope : (float)(1.099 * (double)powf(c, t.inv_gamma) - 0.099);
+            else c = powf(c, t.inv_gamma);
+        }
+        if (t.clamp_on) {
+            c = (c < t.black) ? t.black : c;  // glm::clamp = min(max(x, lo), hi)
+            c = (t.white < c) ? t.white : c;
+        }
+        rgb[k] = c;
+    }
+    reinterpret_cast<uchar4*>(out)[i] = make_uchar4(to_byte(rgb[0]), to_byte(rgb[1]), to_byte(rgb[2]), 255);
+}
+
 // ---- batch ray queries for khp_trace_* ---------------------------------------------------
 template <bool STATS>
 __global__ __launch_bounds__(256) void k_trace_closest(DevScene S, uint32_t n, const float* orig, const float* dir,
@@ -1350,6 +1482,118 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
             prev = sn[k];
         }
     }
+    return KHP_OK;
+}
+
+
+extern "C" void khp_tonemap_defaults(khp_tonemap* t) {
+    if (!t) return;
+    *t = khp_tonemap{};
+    t->bias = 0.85f;
+    t->gamma = 1.0f;
+    t->white = 1.0f;
+    t->kernel_multiplier = 0.125f;
+    t->center_x = t->center_y = -1;
+}
+
+extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t* out_rgba) {
+    if (!c || !out_rgba) return fail(KHP_EINVAL, "null argument");
+    if (!c->fb.p) return fail(KHP_ENOTREADY, "nothing rendered yet");
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t n = c->fbW * c->fbH;
+    const uint32_t nb = (n + 255) / 256;
+    DevMem out, yxy, bmax, bsum;
+    HIPCHK(out.ensure(4 * (size_t)n));
+    if (!tm) {
+        hipLaunchKernelGGL(k_rgba8, dim3(nb), dim3(256), 0, c->stream, c->fb.as<float>(), n, out.as<uint8_t>());
+    } else {
+        HIPCHK(yxy.ensure(12 * (size_t)n));
+        HIPCHK(bmax.ensure(4 * (size_t)nb));
+        HIPCHK(bsum.ensure(8 * (size_t)nb));
+        hipLaunchKernelGGL(k_tm_yxy, dim3(nb), dim3(256), 0, c->stream, c->fb.as<float>(), n, yxy.as<float>(),
+                           bmax.as<float>(), bsum.as<double>());
+        std::vector<float> hm(nb);
+        std::vector<double> hs(nb);
+        HIPCHK(hipMemcpyAsync(hm.data(), bmax.p, 4 * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(hs.data(), bsum.p, 8 * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        float mx = 1e-06f;
+        double sum = 0.0;
+        for (uint32_t b = 0; b < nb; ++b) {
+            mx = (mx < hm[b]) ? hm[b] : mx;
+            sum += hs[b];
+        }
+        // Tonemapper::map / tonemapping scalars, in KIRK's float/double mix
+        float world_lum = (float)sum / (float)n;
+        if (tm->center_weight) {
+            // window and mask on the host, as Tonemapping.cpp:186-236 builds them
+            const int width = (int)c->fbW, height = (int)c->fbH;
+            const int cx = tm->center_x < 0 ? width / 2 : tm->center_x;
+            const int cy = tm->center_y < 0 ? height / 2 : tm->center_y;
+            int ks = width < height ? (int)(width * tm->kernel_multiplier) : (int)(height * tm->kernel_multiplier);
+            if (ks > width || ks > height) ks = std::min(width, height);
+            else if (ks < 1) ks = 1;
+            if (ks % 2 == 0) ks -= 1;
+            const int half = (int)std::floor(ks * 0.5);
+            const int xs = cx + half > width ? width - ks : (cx - half < 0 ? 0 : cx - half);
+            const int ys = cy + half > height ? height - ks : (cy - half < 0 ? 0 : cy - half);
+            if ((long)(xs + ks) * (ys + ks) > (long)width * height || xs < 0 || ys < 0)
+                return fail(KHP_EINVAL, "tonemap center window reads outside the image");
+            std::vector<double> mask((size_t)ks * ks);
+            double acc = 0.0;
+            for (int idx = 0; idx < ks * ks; ++idx) {
+                const int x = idx % ks - half, y = idx / ks - half;
+                const float r = (float)std::sqrt((double)(x * x + y * y));
+                mask[idx] = std::exp(-std::log(2.0) * std::pow((double)(r / (float)half), 2.0));
+            }
+            for (double m : mask) acc += m;
+            const double mean = (double)(ks * ks) / acc;
+            const uint32_t nbc = (uint32_t)(ks * ks + 255) / 256;
+            DevMem dmask, csum;
+            HIPCHK(dmask.ensure(mask.size() * 8));
+            HIPCHK(csum.ensure(8 * (size_t)nbc));
+            HIPCHK(hipMemcpyAsync(dmask.p, mask.data(), mask.size() * 8, hipMemcpyHostToDevice, c->stream));
+            hipLaunchKernelGGL(k_tm_center, dim3(nbc), dim3(256), 0, c->stream, yxy.as<float>(), ks, xs, ys,
+                               dmask.as<double>(), mean, csum.as<double>());
+            std::vector<double> hc(nbc);
+            HIPCHK(hipMemcpyAsync(hc.data(), csum.p, 8 * (size_t)nbc, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            double cs = 0.0;
+            for (double v : hc) cs += v;
+            world_lum = (float)(cs / (ks * ks));
+        }
+        TmScalars t{};
+        t.exposure = (float)pow(2.0, (double)tm->exposure);
+        t.av_lum = expf(world_lum) / 1.0f;
+        t.biasP = logf(tm->bias) / -0.693147f;
+        t.contP = 1.0f / tm->contrast;
+        t.contrast_on = tm->contrast != 0.0f;
+        t.Lmax = mx / t.av_lum;
+        t.divider = log10f(t.Lmax + 1.0f);
+        t.gamma_on = (double)tm->gamma != 1.0;
+        t.rec = tm->rec_gamma != 0;
+        if (t.rec) {
+            t.inv_gamma = (float)(0.45 / (double)tm->gamma * 2.0);
+            t.slope = 4.5f;
+            t.start = 0.018f;
+            if ((double)tm->gamma >= 2.1) {
+                t.start = (float)(0.018 / ((double)(tm->gamma - 2.0f) * 7.5));
+                t.slope = (float)(4.5 * ((double)(tm->gamma - 2.0f) * 7.5));
+            } else if ((double)tm->gamma <= 1.9) {
+                t.start = (float)(0.018 * ((double)(2.0f - tm->gamma) * 7.5));
+                t.slope = (float)(4.5 / ((double)(2.0f - tm->gamma) * 7.5));
+            }
+        } else {
+            t.inv_gamma = 1.0f / tm->gamma;
+        }
+        t.clamp_on = tm->white != 1.0f || tm->black != 0.0f;
+        t.white = tm->white;
+        t.black = tm->black;
+        hipLaunchKernelGGL(k_tm_map, dim3(nb), dim3(256), 0, c->stream, yxy.as<float>(), n, t, out.as<uint8_t>());
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out_rgba, out.p, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return KHP_OK;
 }
 

@@ -87,12 +87,30 @@ class Stats(ctypes.Structure):
                 for k, _ in self._fields_}
 
 
+class Tonemap(ctypes.Structure):
+    """khp_tonemap: KIRK::Tonemapper's parameters (Utils/Tonemapping.h:22-33)."""
+    _fields_ = [("exposure", c_float), ("bias", c_float), ("gamma", c_float), ("contrast", c_float),
+                ("white", c_float), ("black", c_float), ("rec_gamma", c_int32), ("center_weight", c_int32),
+                ("kernel_multiplier", c_float), ("center_x", c_int32), ("center_y", c_int32)]
+
+    @classmethod
+    def defaults(cls, **kw) -> "Tonemap":
+        t = cls(exposure=0.0, bias=0.85, gamma=1.0, contrast=0.0, white=1.0, black=0.0, rec_gamma=0,
+                center_weight=0, kernel_multiplier=0.125, center_x=-1, center_y=-1)
+        for k, v in kw.items():
+            if not hasattr(t, k):
+                raise AttributeError(f"khp_tonemap has no field {k}")
+            setattr(t, k, v)
+        return t
+
+
 # every symbol the header declares (checked by tests/test_abi.py)
 EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "khp_set_scene", "khp_build_accel",
             "khp_render", "khp_read_framebuffer", "khp_trace_closest", "khp_trace_any", "khp_get_stats",
             "khp_comm_unique_id", "khp_comm_init", "khp_gather_framebuffer", "khp_bsdf_kind_from_name",
             "khp_bsdf_name", "khp_shader_kind_from_name", "khp_camera_setup", "khp_fibers_to_cones",
-            "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus", "khp_host_build", "khp_debug_queue"]
+            "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus", "khp_host_build", "khp_debug_queue",
+            "khp_read_rgba8", "khp_tonemap_defaults"]
 
 _lib = None
 
@@ -124,6 +142,8 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_build_accel": (c_int, [c_void_p]),
         "khp_render": (c_int, [c_void_p, P(RenderParams), c_void_p]),
         "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
+        "khp_read_rgba8": (c_int, [c_void_p, P(Tonemap), P(c_uint8)]),
+        "khp_tonemap_defaults": (None, [P(Tonemap)]),
         "khp_trace_closest": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_int32),
                                       P(c_float)]),
         "khp_trace_any": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_uint8)]),

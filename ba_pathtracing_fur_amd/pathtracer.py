@@ -90,6 +90,17 @@ class HipContext:
         N.check(self.lib, self.lib.khp_read_framebuffer(self.ptr, N.fptr(out)), "khp_read_framebuffer")
         return out
 
+    def read_rgba8(self, width, height, tonemap: "N.Tonemap | None" = None) -> np.ndarray:
+        """Device output stage (khp_read_rgba8): (H, W, 4) uint8, row 0 = bottom.
+
+        tonemap=None: Texture::setPixel of the running mean; otherwise
+        Tonemapper::map first (PathTracer::applyToneMapping)."""
+        out = np.zeros((height, width, 4), np.uint8)
+        tm = ctypes.byref(tonemap) if tonemap is not None else None
+        N.check(self.lib, self.lib.khp_read_rgba8(self.ptr, tm, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
+                "khp_read_rgba8")
+        return out
+
     def trace_closest(self, orig, direction):
         o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
         d = np.ascontiguousarray(direction, np.float32).reshape(-1, 3)
@@ -158,6 +169,8 @@ class PathTracer:
         self.c_sample = 0
         self.width, self.height = width, height
         self.seed = seed
+        self.m_use_tonemapping = False      # CPU_PathTracer.h:152
+        self.m_tonemapper = N.Tonemap.defaults()  # CPU_PathTracer.h:38, Tonemapping.h:23-33
         if scene is not None:
             self.init(scene)
 
@@ -191,6 +204,13 @@ class PathTracer:
         """Render every remaining sample; returns the float RGB framebuffer (H, W, 3), row 0 = bottom."""
         self.render(self.m_samples_per_pixel - self.c_sample)
         return self.ctx.read_framebuffer(self.width, self.height)
+
+    def texture_rgba8(self) -> np.ndarray:
+        """The 8-bit render texture after the current samples, on the device:
+        drawTexture's setPixel, or applyToneMapping when m_use_tonemapping
+        (CPU_PathTracer.cpp:43-47, 61-104).  (H, W, 4) uint8, row 0 = bottom."""
+        tm = self.m_tonemapper if self.m_use_tonemapping else None
+        return self.ctx.read_rgba8(self.width, self.height, tm)
 
     @staticmethod
     def to_rgba8(fb: np.ndarray) -> np.ndarray:

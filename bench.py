@@ -224,6 +224,21 @@ def main():
                 for b in range(min(depth, 16))],
         },
     }
+    if rank == 0:
+        # output stage, outside the timed region: the device
+        # 8-bit conversion and Tonemapper::map, wall time including the D2H copy of
+        # W*H*4 bytes (kernel durations: profiles/*_kernel_stats.csv)
+        from ba_pathtracing_fur_amd import native as N
+        tm = N.Tonemap.defaults(gamma=2.2)
+        o = {}
+        for key, t in (("rgba8_ms", None), ("tonemap_rgba8_ms", tm)):
+            ctx.read_rgba8(W, H, t)
+            t1 = time.perf_counter()
+            for _ in range(5):
+                ctx.read_rgba8(W, H, t)
+            o[key] = round((time.perf_counter() - t1) / 5 * 1e3, 3)
+        o["bytes_per_pixel"] = {"rgba8": 16, "tonemap": 40}
+        out["output_stage"] = o
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(sd, args, args.cpu_seconds)

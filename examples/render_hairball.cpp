@@ -2,7 +2,8 @@
 //
 // Builds BASELINE config 3 (seeded hairball on a diffuse plane, 2x2 quad light,
 // sky) exactly like ba_pathtracing_fur_amd.scenes.config3, renders it with the
-// HIP core and optionally writes the fp32 radiance as a PFM.  This is the
+// HIP core and optionally writes the fp32 radiance as a PFM (or, for a .ppm
+// name, the tonemapped 8-bit texture from the device output stage).  This is the
 // shape of KIRK's host side calling the core and doubles as a
 // C++ bench:
 //
@@ -10,6 +11,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../include/kirk_hip.hpp"
@@ -80,7 +82,21 @@ int main(int argc, char** argv) {
                "\"extend_ms\": %.2f, \"shade_ms\": %.2f, \"shadow_ms\": %.2f}\n",
                sb.n_objects(), build_s, frames, dt / frames * 1e3, (double)W * H * spp * frames / dt / 1e6,
                st.extend_ms, st.shade_ms, st.shadow_ms);
-        if (out) {
+        const size_t olen = out ? strlen(out) : 0;
+        if (out && olen > 4 && strcmp(out + olen - 4, ".ppm") == 0) {
+            // 8-bit texture on the device, after Tonemapper::map with gamma 2.2
+            khp_tonemap tm;
+            khp_tonemap_defaults(&tm);
+            tm.gamma = 2.2f;
+            std::vector<uint8_t> rgba((size_t)W * H * 4);
+            ctx.read_rgba8(rgba.data(), &tm);
+            FILE* f = fopen(out, "wb");
+            if (!f) throw std::runtime_error("cannot open output");
+            fprintf(f, "P6\n%u %u\n255\n", W, H);
+            for (uint32_t y = H; y-- > 0;)  // PPM rows are top-to-bottom; row 0 of the texture is the bottom
+                for (uint32_t x = 0; x < W; ++x) fwrite(&rgba[((size_t)y * W + x) * 4], 1, 3, f);
+            fclose(f);
+        } else if (out) {
             std::vector<float> fb((size_t)W * H * 3);
             ctx.read_framebuffer(fb.data());
             FILE* f = fopen(out, "wb");

@@ -206,6 +206,32 @@ khp_status khp_render(khp_ctx* ctx, const khp_render_params* p, float* out_rgb);
 /* Copy the device framebuffer (running mean, W*H*3) to host. */
 khp_status khp_read_framebuffer(khp_ctx* ctx, float* out_rgb);
 
+/* KIRK::Tonemapper parameters (Utils/Tonemapping.h:22-33; defaults in the
+ * comments; khp_tonemap_defaults() fills them). */
+typedef struct {
+    float exposure;     /* m_exposure   0     (exposure factor 2^exposure) */
+    float bias;         /* m_biasParam  0.85                               */
+    float gamma;        /* m_gammaval   1                                  */
+    float contrast;     /* m_contParam  0     (0: off)                     */
+    float white, black; /* m_white 1, m_black 0                            */
+    int32_t rec_gamma;  /* m_use_rec_gamma 0                               */
+    int32_t center_weight;   /* m_center_weight 0: world luminance from a
+                                Gaussian window (luminance_from_center)     */
+    float kernel_multiplier; /* m_kernel_multiplier 0.125                   */
+    int32_t center_x, center_y; /* m_center_x/y -1: W/2, H/2                */
+} khp_tonemap;
+
+/* Output stage on the device: PathTracer::drawTexture -> Texture::setPixel
+ * (CPU_PathTracer.cpp:61-90, Texture.h:252-254), optionally after
+ * PathTracer::applyToneMapping -> Tonemapper::map (CPU_PathTracer.cpp:92-104,
+ * Tonemapping.cpp).  out_rgba: W*H*4 bytes, row y = KIRK texture row y (row 0
+ * = bottom of the frame); byte = (uint8)max(min(c*255, 255), 0) truncated,
+ * NaN -> 0; alpha 255.  tm = NULL: no tonemapping. */
+khp_status khp_read_rgba8(khp_ctx* ctx, const khp_tonemap* tm, uint8_t* out_rgba);
+
+/* The Tonemapper member defaults (Tonemapping.h:23-33). */
+void khp_tonemap_defaults(khp_tonemap* tm);
+
 /* Batch forms of CPU_DataStructure::closestIntersection / isIntersection
  * (CPU_DataStructure.h:25-28, BVH impl CPU_BVH.cpp:51-93), on the GPU.
  * orig/dir: [n][3] host arrays; dir is normalised like KIRK::Ray (Ray.cpp:11-15).

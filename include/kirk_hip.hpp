@@ -102,6 +102,10 @@ class Context {
         check(khp_render(c_, &p, out_rgb), "khp_render");
     }
     void read_framebuffer(float* out_rgb) { check(khp_read_framebuffer(c_, out_rgb), "khp_read_framebuffer"); }
+    // 8-bit texture (W*H*4); tm == nullptr: no tonemapping
+    void read_rgba8(uint8_t* out_rgba, const khp_tonemap* tm = nullptr) {
+        check(khp_read_rgba8(c_, tm, out_rgba), "khp_read_rgba8");
+    }
     void trace_closest(uint32_t n, const float* o, const float* d, float* t, int32_t* obj, float* uv = nullptr) {
         check(khp_trace_closest(c_, n, o, d, t, obj, uv), "khp_trace_closest");
     }

@@ -85,6 +85,13 @@ int ko_bsdf_sample(ko_ctx* c, int hit_obj, const khp_material* mat, const float 
                    float sample_io[2], const float rng_hair[2], int flags_in,
                    float out_dir[3], float* pdf, float f[3]);
 
+/* Output stage (kirk_tonemap.c): Texture::setPixel byte conversion and
+ * Tonemapper::map, sequential in KIRK's order. */
+void ko_tonemap_defaults(khp_tonemap* t);
+void ko_to_rgba8(uint32_t n_pixels, const float* rgb, uint8_t* out_rgba);
+int ko_tonemap(uint32_t W, uint32_t H, const float* rgb, const khp_tonemap* tm, float* out_rgb, float* max_lum,
+               float* world_lum);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,8 @@ def load():
         "ko_rand_u32": (c_uint32, [c_uint32, c_uint32, c_uint32, c_uint32]),
         "ko_bsdf_sample": (c_int, [c_void_p, c_int, c_void_p, P(c_float), P(c_float), P(c_float), P(c_float), c_int,
                                    P(c_float), P(c_float), P(c_float)]),
+        "ko_to_rgba8": (None, [c_uint32, P(c_float), P(c_uint8)]),
+        "ko_tonemap": (c_int, [c_uint32, c_uint32, P(c_float), c_void_p, P(c_float), P(c_float), P(c_float)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -172,3 +174,26 @@ class Oracle:
         fl = self.lib.ko_bsdf_sample(self.ptr, obj, ctypes.addressof(mat), _fp(ri), _fp(nn), _fp(s), _fp(hu),
                                      flags_in, _fp(out), ctypes.byref(pdf), _fp(f))
         return {"out": out, "pdf": pdf.value, "f": f, "flags": fl, "sample": s}
+
+
+def to_rgba8(rgb: np.ndarray) -> np.ndarray:
+    """Texture::setPixel byte conversion (oracle/kirk_tonemap.c): (H, W, 3) -> (H, W, 4) uint8."""
+    lib = load()
+    a = np.ascontiguousarray(rgb, np.float32)
+    out = np.empty(a.shape[:2] + (4,), np.uint8)
+    lib.ko_to_rgba8(a.shape[0] * a.shape[1], _fp(a), out.ctypes.data_as(POINTER(c_uint8)))
+    return out
+
+
+def tonemap(rgb: np.ndarray, tm) -> tuple[np.ndarray, float, float]:
+    """Tonemapper::map (oracle/kirk_tonemap.c) on (H, W, 3) floats; tm: native.Tonemap.
+    Returns (mapped floats, max luminance, world luminance)."""
+    lib = load()
+    a = np.ascontiguousarray(rgb, np.float32)
+    out = np.empty_like(a)
+    mx, wl = c_float(), c_float()
+    rc = lib.ko_tonemap(a.shape[1], a.shape[0], _fp(a), ctypes.addressof(tm), _fp(out), ctypes.byref(mx),
+                        ctypes.byref(wl))
+    if rc != 0:
+        raise ValueError("ko_tonemap: center window outside the image")
+    return out, mx.value, wl.value

@@ -1,0 +1,236 @@
+"""Output stage: Texture::setPixel's 8-bit conversion and
+Tonemapper::map, oracle (oracle/kirk_tonemap.c) vs the device path
+(khp_read_rgba8).
+
+References: Common/Texture.h:252-254 (toByte), Texture.cpp:222-241 (setPixel),
+CPU_PathTracer.cpp:61-104 (drawTexture / applyToneMapping),
+Utils/Tonemapping.cpp:9-245 (map and its stages).
+
+Tolerances, written here because they are the contract:
+  * no tonemapping: bytes identical (the conversion is one IEEE multiply and two
+    compares on both sides);
+  * tonemapping: the reference accumulates the log-luminance sum in float in
+    pixel order, the device reduces it in double in parallel, and the device's
+    expf/logf/powf are ocml's, not glibc's.  Mapped values agree to ~1e-5
+    relative, so a byte may flip by 1 where a value sits on a truncation edge:
+    bytes differ by at most 1 on at most 1% of channels.
+The tonemapper has no golden vectors in the reference (no tests, it cannot be
+built here); the oracle is pinned by an independent float64 numpy restatement
+and analytic known answers below (parity unpinned by the reference itself).
+"""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+from ba_pathtracing_fur_amd import native as N
+from ba_pathtracing_fur_amd import scenes as S
+
+TM_MAX_BYTE_DIFF = 1
+TM_MAX_FLIP_FRACTION = 0.01
+
+RGB2YXY = np.array([[0.5141364, 0.3238786, 0.16036376], [0.265068, 0.67023428, 0.06409157],
+                    [0.0241188, 0.1228178, 0.84442666]])
+YXY2RGB = np.array([[2.5651, -1.1665, -0.3986], [-1.0217, 1.9777, 0.0439], [0.0753, -0.2543, 1.1892]])
+
+
+def np_tonemap(img, exposure=0.0, bias=0.85, gamma=1.0, contrast=0.0, white=1.0, black=0.0, rec=False):
+    """Float64 restatement of Tonemapper::map without center weighting (an
+    independent check of the C oracle, not bit-compatible with it)."""
+    v = img.reshape(-1, 3).astype(np.float64)
+    res = v @ RGB2YXY.T
+    W = res.sum(1)
+    ok = W > 0
+    Y = np.where(ok, res[:, 1], 0.0)
+    x = np.where(ok, res[:, 0] / np.where(ok, W, 1), 0.0)
+    y = np.where(ok, res[:, 1] / np.where(ok, W, 1), 0.0)
+    mx = max(1e-6, Y.max())
+    wl = np.log(2.3e-5 + Y).sum() / len(Y)
+    av = np.exp(wl)
+    biasP = np.log(bias) / -0.693147
+    Lmax = mx / av
+    div = np.log10(Lmax + 1)
+    if contrast:
+        Y = Y ** (1 / contrast)
+    Y = Y / av * 2.0 ** exposure
+    Y = np.log(Y + 1) / np.log(2 + (Y / Lmax) ** biasP * 8) / div
+    good = (Y > 1e-6) & (x > 1e-6) & (y > 1e-6)
+    X = np.where(good, x * Y / np.where(good, y, 1), 1e-6)
+    Z = np.where(good, X / np.where(good, x, 1) - X - Y, 1e-6)
+    rgb = np.stack([X, Y, Z], 1) @ YXY2RGB.T
+    if gamma != 1:
+        if rec:
+            ig = 0.45 / gamma * 2
+            start, slope = 0.018, 4.5
+            if gamma >= 2.1:
+                start, slope = 0.018 / ((gamma - 2) * 7.5), 4.5 * ((gamma - 2) * 7.5)
+            elif gamma <= 1.9:
+                start, slope = 0.018 * ((2 - gamma) * 7.5), 4.5 / ((2 - gamma) * 7.5)
+            rgb = np.where(rgb <= start, rgb * slope, 1.099 * np.abs(rgb) ** ig - 0.099)
+        else:
+            with np.errstate(invalid="ignore"):
+                rgb = rgb ** (1 / gamma)  # powf: NaN for a negative base
+    if white != 1 or black != 0:
+        rgb = np.clip(rgb, black, white)
+    return rgb.reshape(img.shape), mx, wl
+
+
+def _image(h=48, w=64, seed=0):
+    rng = np.random.default_rng(seed)
+    return rng.gamma(0.6, 0.5, (h, w, 3)).astype(np.float32)
+
+
+# ---------------------------------------------------------------- CPU: the oracle
+
+def test_to_byte_edges():
+    vals = np.array([np.nan, np.inf, -np.inf, -1.0, 0.0, 1 / 255, 0.5, 254.999 / 255, 1.0, 2.0, 1e30, -0.0],
+                    np.float32)
+    rgb = np.repeat(vals[:, None], 3, 1).reshape(1, -1, 3)
+    got = O.to_rgba8(rgb)[0]
+    a = vals * np.float32(255)
+    with np.errstate(invalid="ignore"):
+        want = np.where(np.isnan(a), 0, np.clip(a, 0, 255)).astype(np.uint8)
+    assert np.array_equal(got[:, 0], want) and np.all(got[:, 3] == 255)
+    assert list(got[:5, 0]) == [0, 255, 0, 0, 0] and got[7, 0] == 254 and got[8, 0] == 255
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(exposure=1.5), dict(bias=0.6, gamma=2.2), dict(contrast=2.0),
+                                dict(gamma=2.2, rec=True), dict(gamma=1.6, rec=True), dict(white=0.9, black=0.05),
+                                dict(gamma=2.0, rec=True, exposure=-0.5)])
+def test_oracle_tonemap_vs_float64(kw):
+    img = _image()
+    tm = N.Tonemap.defaults(exposure=kw.get("exposure", 0.0), bias=kw.get("bias", 0.85),
+                            gamma=kw.get("gamma", 1.0), contrast=kw.get("contrast", 0.0),
+                            white=kw.get("white", 1.0), black=kw.get("black", 0.0), rec_gamma=int(kw.get("rec", 0)))
+    got, mx, wl = O.tonemap(img, tm)
+    want, mx64, wl64 = np_tonemap(img, **kw)
+    assert abs(mx - mx64) <= 1e-6 * mx64 and abs(wl - wl64) <= 1e-5 * abs(wl64)
+    np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-4)  # gamma steepens errors near 0
+
+
+def test_oracle_tonemap_gray_maps_to_unit_luminance():
+    """Known answer: a uniform image has Y/av_lum = Y/(Y + ~2.3e-5) ~ 1 = Lmax, so
+    Y' = log(2)/log(2 + 8)/log10(2) = 1 for every pixel, whatever the gray level."""
+    for level in (0.05, 0.5, 3.0):
+        img = np.full((16, 24, 3), level, np.float32)
+        out, mx, wl = O.tonemap(img, N.Tonemap.defaults())
+        Y = out.reshape(-1, 3).astype(np.float64) @ RGB2YXY[1]
+        assert np.allclose(Y, 1.0, atol=2e-3), (level, Y[:3])
+
+
+def test_oracle_tonemap_nonfinite_pixels():
+    """A NaN radiance pixel fails RGB_to_Yxy's `W > 0` test and becomes Yxy 0 (the
+    rest of the frame maps normally); an inf pixel makes the log-luminance sum
+    inf, every mapped value NaN, and the whole frame converts to byte 0."""
+    img = _image()
+    ref, _, _ = O.tonemap(img, N.Tonemap.defaults())
+    img[3, 5, 1] = np.nan
+    out, _, wl = O.tonemap(img, N.Tonemap.defaults())
+    assert np.isfinite(wl) and np.isfinite(out).all()
+    assert np.abs(out[3, 5]).max() < 1e-5                       # Yxy 0 -> X = Z = epsilon
+    out[3, 5] = ref[3, 5]
+    assert np.abs(out - ref).max() < 0.01                        # the rest moves only through world_lum
+    img[3, 5, 1] = np.inf
+    out, _, _ = O.tonemap(img, N.Tonemap.defaults())
+    rgba = O.to_rgba8(out)
+    assert np.all(rgba[..., :3] == 0) and np.all(rgba[..., 3] == 255)
+
+
+def test_oracle_center_weight():
+    img = _image(64, 96)
+    tm = N.Tonemap.defaults(center_weight=1)
+    _, _, wl_c = O.tonemap(img, tm)
+    _, _, wl = O.tonemap(img, N.Tonemap.defaults())
+    assert np.isfinite(wl_c) and wl_c != wl
+    # a window that would read past the image (the reference's indexing) is refused
+    with pytest.raises(ValueError):
+        O.tonemap(img, N.Tonemap.defaults(center_weight=1, center_x=81, center_y=49, kernel_multiplier=0.5))
+
+
+def test_tonemap_struct_defaults_match_library():
+    lib = N.load_library()
+    t = N.Tonemap()
+    lib.khp_tonemap_defaults(t)
+    d = N.Tonemap.defaults()
+    for name, _ in N.Tonemap._fields_:
+        assert getattr(t, name) == pytest.approx(getattr(d, name)), name
+
+
+# ---------------------------------------------------------------- GPU: device vs oracle
+
+def _frame(hip_ctx, name, w, h, spp, depth, **kw):
+    sd = S.build_config(name, width=w, height=h, **kw)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    return hip_ctx.render(w, h, spp, depth)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw", [("config1", {}), ("config2", dict(n_strands=2000)), ("zoo", dict(n_strands=400))])
+def test_rgba8_exact(hip_ctx, name, kw):
+    fb = _frame(hip_ctx, name, 64, 48, 4, 5, **kw)
+    got = hip_ctx.read_rgba8(64, 48)
+    assert np.array_equal(got, O.to_rgba8(fb))
+
+
+TM_CASES = [dict(), dict(exposure=1.0, gamma=2.2), dict(gamma=2.2, rec_gamma=1), dict(contrast=1.5, bias=0.7),
+            dict(white=0.95, black=0.02, gamma=1.8, rec_gamma=1), dict(center_weight=1),
+            dict(center_weight=1, kernel_multiplier=0.3, center_x=20, center_y=10)]
+
+
+def _assert_bytes_close(got, want):
+    d = np.abs(got.astype(np.int16) - want.astype(np.int16))
+    assert d.max() <= TM_MAX_BYTE_DIFF, d.max()
+    assert (d > 0).mean() <= TM_MAX_FLIP_FRACTION, (d > 0).mean()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tkw", TM_CASES, ids=[str(i) for i in range(len(TM_CASES))])
+def test_rgba8_tonemapped(hip_ctx, tkw):
+    fb = _frame(hip_ctx, "config1", 96, 72, 4, 5)
+    assert np.isfinite(fb).all()
+    tm = N.Tonemap.defaults(**tkw)
+    got = hip_ctx.read_rgba8(96, 72, tm)
+    mapped, _, _ = O.tonemap(fb, tm)
+    _assert_bytes_close(got, O.to_rgba8(mapped))
+
+
+@pytest.mark.gpu
+def test_rgba8_tonemapped_full_size(hip_ctx):
+    """BASELINE config 3 resolution (1280x720): the sum over 921600 pixels is where
+    float-vs-double accumulation differs most."""
+    fb = _frame(hip_ctx, "config3", 1280, 720, 1, 4, n_strands=20000)
+    tm = N.Tonemap.defaults(gamma=2.2)
+    got = hip_ctx.read_rgba8(1280, 720, tm)
+    mapped, _, _ = O.tonemap(fb, tm)
+    want = O.to_rgba8(mapped)
+    if np.isinf(fb).any():  # an inf radiance pixel blacks out the whole mapped frame on both sides
+        assert np.array_equal(got, want)
+    else:
+        _assert_bytes_close(got, want)
+
+
+@pytest.mark.gpu
+def test_rgba8_errors(hip_ctx):
+    fresh = __import__("ba_pathtracing_fur_amd.pathtracer", fromlist=["HipContext"]).HipContext(0)
+    with pytest.raises(N.KhpError) as e:
+        fresh.read_rgba8(8, 8)
+    assert e.value.status == N.KHP_ENOTREADY
+    fresh.close()
+    _frame(hip_ctx, "config1", 32, 24, 1, 2)
+    with pytest.raises(N.KhpError) as e:
+        hip_ctx.read_rgba8(32, 24, N.Tonemap.defaults(center_weight=1, kernel_multiplier=0.9, center_x=22, center_y=14))
+    assert e.value.status == N.KHP_EINVAL
+
+
+@pytest.mark.gpu
+def test_pathtracer_texture(hip_ctx):
+    from ba_pathtracing_fur_amd.pathtracer import PathTracer
+    sd = S.config1(40, 30)
+    pt = PathTracer(sd, depth=4, width=40, height=30)
+    pt.set_sample_count(3)
+    fb = pt.render_to_texture()
+    assert np.array_equal(pt.texture_rgba8(), O.to_rgba8(fb))
+    pt.m_use_tonemapping = True
+    mapped, _, _ = O.tonemap(fb, pt.m_tonemapper)
+    _assert_bytes_close(pt.texture_rgba8(), O.to_rgba8(mapped))
+    pt.ctx.close()
