@@ -1,0 +1,883 @@
+// bvh_build.hip -- BVH::addBaseDataStructure (CPU_BVH.cpp:16-44, 95-138, 357-552)
+// on the GPU: the same binned-SAH tree, node for node and id for id, as the
+// host builder in scene.cpp.
+//
+// KIRK's tree is defined by a sequential recursion; three facts make it a
+// parallel build without changing a single node:
+//   * bins, node boxes and centroid boxes are min/max/count reductions, exact
+//     in any order (up to the sign of a zero);
+//   * the SAH sweep over 15 planes x 3 axes is tiny and runs once per node, in
+//     the host's loop order, on one thread;
+//   * the Hoare two-pointer partition (CPU_BVH.cpp:475-552) swaps the k-th
+//     right-belonging element of the left region with the k-th left-belonging
+//     element of the right region counted from the end.  Ranking both kinds by
+//     position (prefix sums) reproduces its permutation exactly.
+// Nodes with more than SMALL objects are built level by level (all nodes of a
+// level in one set of launches, chunks of CH objects per block); smaller nodes
+// are finished by one thread each with the literal recursion.  The DFS
+// preorder index of a node has a closed form,
+//     pre(node) = (#left turns from the root) + 2 * (#leaves starting before node.first),
+// so nodes are written straight into preorder once the leaf starts are scanned.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cfloat>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "scene.h"
+
+namespace khp {
+namespace gb {
+
+constexpr int NB = 16, NP = 15;
+constexpr uint32_t CH = 2048;          // objects per chunk (one 256-thread block)
+constexpr uint32_t SMALL = 256;        // nodes up to this many objects: one thread builds the subtree
+constexpr int BW = 3 * NB * 7;         // bin words per chunk: 3 axes x 16 bins x (count, min.xyz, max.xyz)
+constexpr int SUB_STACK = SMALL + 4;
+
+struct GNode {  // interior node of the level phase
+    float cb[6];
+    uint32_t first, count, lturns, depth;
+    int32_t axis, plane;
+    float k, cbmin;
+    uint32_t L, chunk0, nchunk, bad;
+};
+struct SRoot {  // root of a subtree finished by one thread
+    float cb[6];
+    uint32_t first, count, lturns, depth, n_local, pad;
+};
+struct LLeaf {  // leaf made by the level phase
+    uint32_t first, count, lturns, depth;
+};
+struct Ctr {
+    uint32_t n_gnode, n_sroot, n_lleaf, max_depth, max_leaf, error, pad[2];
+};
+
+// ---- box arithmetic, operand order of scene.cpp / BoundingBox.cpp ----------
+struct GBox {
+    float mn[3], mx[3];
+};
+KHD float smin(float a, float b) { return (b < a) ? b : a; }  // std::min
+KHD float smax(float a, float b) { return (a < b) ? b : a; }  // std::max
+KHD GBox box_empty() { return GBox{{FLT_MAX, FLT_MAX, FLT_MAX}, {-FLT_MAX, -FLT_MAX, -FLT_MAX}}; }
+KHD void grow(GBox& b, const GBox& o) {
+    for (int a = 0; a < 3; ++a) {
+        b.mn[a] = smin(b.mn[a], o.mn[a]);
+        b.mx[a] = smax(b.mx[a], o.mx[a]);
+    }
+}
+KHD void grow_pt(GBox& b, float x, float y, float z) {
+    b.mn[0] = smin(b.mn[0], x); b.mn[1] = smin(b.mn[1], y); b.mn[2] = smin(b.mn[2], z);
+    b.mx[0] = smax(b.mx[0], x); b.mx[1] = smax(b.mx[1], y); b.mx[2] = smax(b.mx[2], z);
+}
+KHD float area(const GBox& b) {
+    float sx = b.mx[0] - b.mn[0], sy = b.mx[1] - b.mn[1], sz = b.mx[2] - b.mn[2];
+    return 2.0f * (sx * sy + sx * sz + sy * sz);
+}
+KHD bool worth(const GBox& b) {
+    return b.mx[0] - b.mn[0] > 0.0f && b.mx[1] - b.mn[1] > 0.0f && b.mx[2] - b.mn[2] > 0.0f;
+}
+KHD float split_k(float cbmin, float cbmax) {
+    const float cbdiff = cbmax - cbmin;
+    const float epsilon = 0.1f;
+    return ((float)NB * (1.0f - epsilon)) / cbdiff;
+}
+KHD GBox cb_of(const float* c) { return GBox{{c[0], c[1], c[2]}, {c[3], c[4], c[5]}}; }
+KHD void cb_put(float* c, const GBox& b) {
+    for (int a = 0; a < 3; ++a) {
+        c[a] = b.mn[a];
+        c[3 + a] = b.mx[a];
+    }
+}
+
+// order-preserving float <-> uint (for min/max atomics on LDS words)
+__device__ __forceinline__ uint32_t fenc(float f) {
+    uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float fdec(uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); }
+__device__ __forceinline__ uint32_t bin_init(int w) {
+    const int f = w % 7;
+    return f == 0 ? 0u : (f <= 3 ? fenc(FLT_MAX) : fenc(-FLT_MAX));
+}
+__device__ __forceinline__ uint32_t bin_comb(int w, uint32_t a, uint32_t b) {
+    const int f = w % 7;
+    return f == 0 ? a + b : (f <= 3 ? min(a, b) : max(a, b));
+}
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// ---- setup ------------------------------------------------------------------
+__global__ void k_init(const float* cen, uint32_t n, float4* rec, uint32_t* leafstart, uint32_t* part) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ uint32_t red[6][256];
+    uint32_t v[6] = {fenc(FLT_MAX), fenc(FLT_MAX), fenc(FLT_MAX), fenc(-FLT_MAX), fenc(-FLT_MAX), fenc(-FLT_MAX)};
+    if (i < n) {
+        const float x = cen[3 * (size_t)i], y = cen[3 * (size_t)i + 1], z = cen[3 * (size_t)i + 2];
+        rec[i] = make_float4(x, y, z, __uint_as_float(i));
+        v[0] = fenc(x); v[1] = fenc(y); v[2] = fenc(z);
+        v[3] = v[0]; v[4] = v[1]; v[5] = v[2];
+    }
+    if (i <= n) leafstart[i] = 0u;
+    for (int a = 0; a < 6; ++a) red[a][threadIdx.x] = v[a];
+    __syncthreads();
+    for (uint32_t w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int a = 0; a < 6; ++a) {
+                uint32_t o = red[a][threadIdx.x + w];
+                red[a][threadIdx.x] = a < 3 ? min(red[a][threadIdx.x], o) : max(red[a][threadIdx.x], o);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) part[6 * blockIdx.x + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// ---- level phase ------------------------------------------------------------
+__global__ void k_nchunks(const GNode* g, uint32_t b, uint32_t n, uint32_t* nc) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) nc[i] = (g[b + i].count + CH - 1) / CH;
+    if (i == n) nc[i] = 0;
+}
+
+__global__ void k_chunk_list(GNode* g, uint32_t b, const uint32_t* c0, uint32_t* chunk_node) {
+    const uint32_t i = blockIdx.x;
+    const uint32_t base = c0[i], nc = c0[i + 1] - base;
+    if (threadIdx.x == 0) {
+        g[b + i].chunk0 = base;
+        g[b + i].nchunk = nc;
+    }
+    for (uint32_t j = threadIdx.x; j < nc; j += blockDim.x) chunk_node[base + j] = b + i;
+}
+
+// Per chunk: the 3 x 16 bins of BVHNode::partition's first loop (CPU_BVH.cpp:369-399).
+__global__ __launch_bounds__(256) void k_bin(const float4* __restrict__ rec, const GNode* __restrict__ g,
+                                             const uint32_t* __restrict__ chunk_node, uint32_t* __restrict__ part) {
+    __shared__ uint32_t tab[4][BW];
+    const uint32_t c = blockIdx.x, wave = threadIdx.x >> 6;
+    for (int w = threadIdx.x; w < 4 * BW; w += 256) tab[w / BW][w % BW] = bin_init(w % BW);
+    const GNode nd = g[chunk_node[c]];
+    const uint32_t start = nd.first + (c - nd.chunk0) * CH;
+    const uint32_t end = min(nd.first + nd.count, start + CH);
+    float k[3], cbmin[3];
+    for (int a = 0; a < 3; ++a) {
+        cbmin[a] = nd.cb[a];
+        k[a] = split_k(nd.cb[a], nd.cb[3 + a]);
+    }
+    __syncthreads();
+    for (uint32_t p = start + threadIdx.x; p < end; p += 256) {
+        const float4 e = rec[p];
+        const float cc[3] = {e.x, e.y, e.z};
+        const uint32_t ex = fenc(e.x), ey = fenc(e.y), ez = fenc(e.z);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const int bin = min(max((int)(k[a] * (cc[a] - cbmin[a])), 0), NB - 1);  // in range for valid input
+            uint32_t* t = &tab[wave][(a * NB + bin) * 7];
+            atomicAdd(&t[0], 1u);
+            atomicMin(&t[1], ex);
+            atomicMin(&t[2], ey);
+            atomicMin(&t[3], ez);
+            atomicMax(&t[4], ex);
+            atomicMax(&t[5], ey);
+            atomicMax(&t[6], ez);
+        }
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < BW; w += 256) {
+        uint32_t v = tab[0][w];
+        for (int q = 1; q < 4; ++q) v = bin_comb(w, v, tab[q][w]);
+        part[(size_t)c * BW + w] = v;
+    }
+}
+
+__device__ void spawn(uint32_t first, uint32_t count, const GBox& cb, uint32_t lturns, uint32_t depth, GNode* g,
+                      uint32_t gcap, SRoot* sr, uint32_t scap, LLeaf* ll, uint32_t lcap, uint32_t* leafstart, Ctr* ct) {
+    atomicMax(&ct->max_depth, depth);
+    if (count - 1u > 1u && worth(cb)) {
+        if (count <= SMALL) {
+            const uint32_t s = atomicAdd(&ct->n_sroot, 1u);
+            if (s >= scap) { atomicOr(&ct->error, 1u); return; }
+            SRoot r{};
+            cb_put(r.cb, cb);
+            r.first = first; r.count = count; r.lturns = lturns; r.depth = depth;
+            sr[s] = r;
+        } else {
+            const uint32_t s = atomicAdd(&ct->n_gnode, 1u);
+            if (s >= gcap) { atomicOr(&ct->error, 2u); return; }
+            GNode q{};
+            cb_put(q.cb, cb);
+            q.first = first; q.count = count; q.lturns = lturns; q.depth = depth;
+            q.plane = -1;
+            g[s] = q;
+        }
+    } else {
+        const uint32_t s = atomicAdd(&ct->n_lleaf, 1u);
+        if (s >= lcap) { atomicOr(&ct->error, 4u); return; }
+        ll[s] = LLeaf{first, count, lturns, depth};
+        leafstart[first] = 1u;
+        atomicMax(&ct->max_leaf, count);
+    }
+}
+
+// Per node: reduce the chunk bins, run the SAH sweep exactly as the host loop
+// (CPU_BVH.cpp:400-470), spawn the two children.
+__global__ __launch_bounds__(256) void k_pick(GNode* g, uint32_t b, const uint32_t* __restrict__ part, uint32_t gcap,
+                                              SRoot* sr, uint32_t scap, LLeaf* ll, uint32_t lcap, uint32_t* leafstart,
+                                              Ctr* ct) {
+    __shared__ uint32_t red[BW];
+    const uint32_t i = b + blockIdx.x;
+    const uint32_t c0 = g[i].chunk0, nc = g[i].nchunk;
+    for (int w = threadIdx.x; w < BW; w += 256) {
+        uint32_t v = bin_init(w);
+        for (uint32_t c = c0; c < c0 + nc; ++c) v = bin_comb(w, v, part[(size_t)c * BW + w]);
+        red[w] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    GNode nd = g[i];
+    float best = FLT_MAX;
+    int best_axis = 0, best_plane = 0;
+    uint32_t bestL = 0;
+    GBox lcb = box_empty(), rcb = box_empty();
+    for (int axis = 0; axis < 3; ++axis) {
+        GBox bb[NB];
+        uint32_t bn[NB];
+        for (int q = 0; q < NB; ++q) {
+            const uint32_t* t = &red[(axis * NB + q) * 7];
+            bn[q] = t[0];
+            bb[q] = GBox{{fdec(t[1]), fdec(t[2]), fdec(t[3])}, {fdec(t[4]), fdec(t[5]), fdec(t[6])}};
+        }
+        uint32_t ln[NP];
+        GBox lb[NP];
+        lb[0] = box_empty();
+        grow(lb[0], bb[0]);
+        ln[0] = bn[0];
+        for (int p = 1; p < NP; ++p) {
+            lb[p] = box_empty();
+            grow(lb[p], lb[p - 1]);
+            grow(lb[p], bb[p]);
+            ln[p] = ln[p - 1] + bn[p];
+        }
+        GBox rb_next = box_empty();
+        uint32_t rn_next = 0;
+        for (int p = NP - 1; p >= 0; --p) {
+            GBox rb = box_empty();
+            grow(rb, bb[p + 1]);
+            uint32_t rn = bn[p + 1];
+            if (p != NP - 1) {
+                grow(rb, rb_next);
+                rn += rn_next;
+            }
+            const float cost = area(lb[p]) * (float)ln[p] + area(rb) * (float)rn;
+            if (cost < best) {
+                best = cost;
+                best_axis = axis;
+                best_plane = p;
+                lcb = lb[p];
+                rcb = rb;
+                bestL = ln[p];
+            }
+            rb_next = rb;
+            rn_next = rn;
+        }
+    }
+    nd.axis = best_axis;
+    nd.plane = best_plane;
+    nd.cbmin = nd.cb[best_axis];
+    nd.k = split_k(nd.cb[best_axis], nd.cb[3 + best_axis]);
+    nd.L = bestL;
+    if (bestL == 0 || bestL >= nd.count) {  // cannot happen for worth(cb) boxes; refuse rather than loop
+        nd.bad = 1;
+        atomicOr(&ct->error, 8u);
+    }
+    g[i] = nd;
+    if (nd.bad) return;
+    spawn(nd.first, bestL, lcb, nd.lturns + 1, nd.depth + 1, g, gcap, sr, scap, ll, lcap, leafstart, ct);
+    spawn(nd.first + bestL, nd.count - bestL, rcb, nd.lturns, nd.depth + 1, g, gcap, sr, scap, ll, lcap, leafstart, ct);
+}
+
+__device__ __forceinline__ bool right_side(const GNode& nd, float4 e) {
+    const float c = nd.axis == 0 ? e.x : (nd.axis == 1 ? e.y : e.z);
+    return (int)(nd.k * (c - nd.cbmin)) > nd.plane;
+}
+
+// Per chunk: count right-belonging objects in the left region and left-belonging
+// objects in the right region.  (hi 32 bits, lo 32 bits)
+__global__ __launch_bounds__(256) void k_classify(const float4* __restrict__ rec, const GNode* __restrict__ g,
+                                                  const uint32_t* __restrict__ chunk_node, uint64_t* cnt) {
+    __shared__ uint32_t sL, sR;
+    if (threadIdx.x == 0) sL = sR = 0;
+    __syncthreads();
+    const uint32_t c = blockIdx.x;
+    const GNode nd = g[chunk_node[c]];
+    const uint32_t start = nd.first + (c - nd.chunk0) * CH;
+    const uint32_t end = min(nd.first + nd.count, start + CH);
+    const uint32_t mid = nd.first + nd.L;
+    uint32_t l = 0, r = 0;
+    if (!nd.bad)
+        for (uint32_t p = start + threadIdx.x; p < end; p += 256) {
+            const bool rs = right_side(nd, rec[p]);
+            l += (p < mid && rs);
+            r += (p >= mid && !rs);
+        }
+    if (l) atomicAdd(&sL, l);
+    if (r) atomicAdd(&sR, r);
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[c] = ((uint64_t)sL << 32) | sR;
+    if (threadIdx.x == 0 && c == gridDim.x - 1) cnt[c + 1] = 0;
+}
+
+// Per chunk: rank the misplaced objects by position and stage the swap pairs.
+__global__ __launch_bounds__(256) void k_swap_write(const float4* __restrict__ rec, const GNode* __restrict__ g,
+                                                    const uint32_t* __restrict__ chunk_node, const uint64_t* off,
+                                                    float4* SL, float4* SR, uint32_t* PL, uint32_t* PR) {
+    __shared__ uint32_t wl[4], wr[4];
+    const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const GNode nd = g[chunk_node[c]];
+    if (nd.bad) return;
+    const uint32_t start = nd.first + (c - nd.chunk0) * CH;
+    const uint32_t end = min(nd.first + nd.count, start + CH);
+    const uint32_t mid = nd.first + nd.L;
+    const uint64_t o0 = off[nd.chunk0], oc = off[c], oe = off[nd.chunk0 + nd.nchunk];
+    uint32_t baseL = (uint32_t)(oc >> 32) - (uint32_t)(o0 >> 32);
+    uint32_t baseR = (uint32_t)oc - (uint32_t)o0;
+    const uint32_t mR = (uint32_t)oe - (uint32_t)o0;
+    (void)lane;
+    for (uint32_t r0 = start; r0 < end; r0 += 256) {
+        const uint32_t p = r0 + threadIdx.x;
+        float4 e = make_float4(0, 0, 0, 0);
+        bool fl = false, fr = false;
+        if (p < end) {
+            e = rec[p];
+            const bool rs = right_side(nd, e);
+            fl = p < mid && rs;
+            fr = p >= mid && !rs;
+        }
+        const uint64_t bl = __ballot(fl), br = __ballot(fr);
+        if ((threadIdx.x & 63) == 0) {
+            wl[wave] = (uint32_t)__popcll(bl);
+            wr[wave] = (uint32_t)__popcll(br);
+        }
+        __syncthreads();
+        uint32_t pl = baseL, pr = baseR, tl = 0, tr = 0;
+        for (uint32_t q = 0; q < 4; ++q) {
+            if (q < wave) { pl += wl[q]; pr += wr[q]; }
+            tl += wl[q];
+            tr += wr[q];
+        }
+        if (fl) {
+            const uint32_t kk = pl + lane_rank(bl);
+            SL[nd.first + kk] = e;
+            PL[nd.first + kk] = p;
+        }
+        if (fr) {
+            const uint32_t kk = mR - 1u - (pr + lane_rank(br));
+            SR[nd.first + kk] = e;
+            PR[nd.first + kk] = p;
+        }
+        baseL += tl;
+        baseR += tr;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_swap_apply(float4* rec, const GNode* __restrict__ g,
+                                                    const uint32_t* __restrict__ chunk_node, const uint64_t* off,
+                                                    const float4* SL, const float4* SR, const uint32_t* PL,
+                                                    const uint32_t* PR) {
+    const uint32_t c = blockIdx.x;
+    const GNode nd = g[chunk_node[c]];
+    if (nd.bad) return;
+    const uint32_t m = (uint32_t)(off[nd.chunk0 + nd.nchunk] >> 32) - (uint32_t)(off[nd.chunk0] >> 32);
+    const uint32_t start = (c - nd.chunk0) * CH;
+    const uint32_t end = min(m, start + CH);
+    for (uint32_t kk = start + threadIdx.x; kk < end; kk += 256) {
+        const uint32_t s = nd.first + kk;
+        rec[PL[s]] = SR[s];
+        rec[PR[s]] = SL[s];
+    }
+}
+
+// ---- small subtrees: the literal recursion of BVHNode::split, one thread each ----
+struct Frame {
+    float cb[6];
+    uint32_t first, second, depth;
+    int32_t parent;  // local index of the parent, -1 for the subtree root
+    int32_t side;
+};
+
+__global__ __launch_bounds__(64) void k_subtree(float4* rec, const float* __restrict__ bounds, SRoot* sr, uint32_t n,
+                                                BuildNode* T, uint32_t* leafstart, Ctr* ct) {
+    // per-thread bins in LDS: bb (16 x 7) + lb (15 x 7) words
+    __shared__ float lds[64][NB * 7 + NP * 7];
+    const uint32_t si = blockIdx.x * blockDim.x + threadIdx.x;
+    if (si >= n) return;
+    float* bbw = lds[threadIdx.x];
+    float* lbw = bbw + NB * 7;
+    SRoot root = sr[si];
+    BuildNode* out = T + 2 * (size_t)root.first;
+    Frame st[SUB_STACK];
+    int sp = 0;
+    st[sp].first = root.first;
+    st[sp].second = root.first + root.count - 1;
+    st[sp].depth = root.depth;
+    st[sp].parent = -1;
+    st[sp].side = 0;
+    for (int a = 0; a < 6; ++a) st[sp].cb[a] = root.cb[a];
+    ++sp;
+    int32_t local = 0;
+    uint32_t maxd = 0, maxl = 0;
+    while (sp > 0) {
+        const Frame f = st[--sp];
+        const int32_t ni = local++;
+        if (f.parent >= 0) {
+            if (f.side == 0) out[f.parent].left = ni;
+            else out[f.parent].right = ni;
+        }
+        GBox bv = box_empty();
+        for (uint32_t id = f.first; id <= f.second; ++id) {
+            const float* bb = &bounds[6 * (size_t)__float_as_uint(rec[id].w)];
+            bv.mn[0] = smin(bv.mn[0], bb[0]); bv.mn[1] = smin(bv.mn[1], bb[1]); bv.mn[2] = smin(bv.mn[2], bb[2]);
+            bv.mx[0] = smax(bv.mx[0], bb[3]); bv.mx[1] = smax(bv.mx[1], bb[4]); bv.mx[2] = smax(bv.mx[2], bb[5]);
+        }
+        BuildNode node{};
+        node.mn = mk(bv.mn[0], bv.mn[1], bv.mn[2]);
+        node.mx = mk(bv.mx[0], bv.mx[1], bv.mx[2]);
+        maxd = max(maxd, f.depth);
+        const GBox cb = cb_of(f.cb);
+        if (f.second - f.first > 1u && worth(cb)) {
+            // BVHNode::partition (CPU_BVH.cpp:357-552), as scene.cpp Builder::partition
+            float best = FLT_MAX;
+            int best_axis = 0, best_plane = 0;
+            GBox lcb = box_empty(), rcb = box_empty();
+            float cbmins[3], ks[3];
+            for (int axis = 0; axis < 3; ++axis) {
+                const float cbmin = cb.mn[axis];
+                const float k = split_k(cb.mn[axis], cb.mx[axis]);
+                cbmins[axis] = cbmin;
+                ks[axis] = k;
+                for (int q = 0; q < NB; ++q) {
+                    float* t = bbw + 7 * q;
+                    t[0] = __uint_as_float(0u);
+                    t[1] = t[2] = t[3] = FLT_MAX;
+                    t[4] = t[5] = t[6] = -FLT_MAX;
+                }
+                for (uint32_t id = f.first; id <= f.second; ++id) {
+                    const float4 e = rec[id];
+                    const float cc = axis == 0 ? e.x : (axis == 1 ? e.y : e.z);
+                    const int bin = min(max((int)(k * (cc - cbmin)), 0), NB - 1);
+                    float* t = bbw + 7 * bin;
+                    t[1] = smin(t[1], e.x); t[2] = smin(t[2], e.y); t[3] = smin(t[3], e.z);
+                    t[4] = smax(t[4], e.x); t[5] = smax(t[5], e.y); t[6] = smax(t[6], e.z);
+                    t[0] = __uint_as_float(__float_as_uint(t[0]) + 1u);
+                }
+                // lb prefix
+                {
+                    GBox acc = box_empty();
+                    const float* t = bbw;
+                    GBox b0{{t[1], t[2], t[3]}, {t[4], t[5], t[6]}};
+                    grow(acc, b0);
+                    uint32_t cnt = __float_as_uint(t[0]);
+                    float* o = lbw;
+                    o[0] = __uint_as_float(cnt);
+                    for (int a = 0; a < 3; ++a) { o[1 + a] = acc.mn[a]; o[4 + a] = acc.mx[a]; }
+                    for (int p = 1; p < NP; ++p) {
+                        const float* tp = bbw + 7 * p;
+                        GBox lbp = box_empty();
+                        grow(lbp, acc);
+                        GBox bp{{tp[1], tp[2], tp[3]}, {tp[4], tp[5], tp[6]}};
+                        grow(lbp, bp);
+                        acc = lbp;
+                        cnt += __float_as_uint(tp[0]);
+                        float* op = lbw + 7 * p;
+                        op[0] = __uint_as_float(cnt);
+                        for (int a = 0; a < 3; ++a) { op[1 + a] = acc.mn[a]; op[4 + a] = acc.mx[a]; }
+                    }
+                }
+                GBox rb_next = box_empty();
+                uint32_t rn_next = 0;
+                for (int p = NP - 1; p >= 0; --p) {
+                    const float* tb = bbw + 7 * (p + 1);
+                    GBox rb = box_empty();
+                    GBox bq{{tb[1], tb[2], tb[3]}, {tb[4], tb[5], tb[6]}};
+                    grow(rb, bq);
+                    uint32_t rn = __float_as_uint(tb[0]);
+                    if (p != NP - 1) {
+                        grow(rb, rb_next);
+                        rn += rn_next;
+                    }
+                    const float* tl = lbw + 7 * p;
+                    GBox lbp{{tl[1], tl[2], tl[3]}, {tl[4], tl[5], tl[6]}};
+                    const float cost = area(lbp) * (float)__float_as_uint(tl[0]) + area(rb) * (float)rn;
+                    if (cost < best) {
+                        best = cost;
+                        best_axis = axis;
+                        best_plane = p;
+                        lcb = lbp;
+                        rcb = rb;
+                    }
+                    rb_next = rb;
+                    rn_next = rn;
+                }
+            }
+            const float cbmin = cbmins[best_axis], k = ks[best_axis];
+            auto bin_of = [&](uint32_t pos) {
+                const float4 e = rec[pos];
+                const float cc = best_axis == 0 ? e.x : (best_axis == 1 ? e.y : e.z);
+                return (int)(k * (cc - cbmin));
+            };
+            int left = (int)f.first, right = (int)f.second;
+            bool ls = false, rs = false;
+            while (left < right) {
+                if (!ls) {
+                    if (bin_of((uint32_t)left) > best_plane) ls = true;
+                    else ++left;
+                }
+                if (!rs) {
+                    if (bin_of((uint32_t)right) <= best_plane) rs = true;
+                    else --right;
+                }
+                if (ls && rs) {
+                    const float4 tmp = rec[left];
+                    rec[left] = rec[right];
+                    rec[right] = tmp;
+                    ls = rs = false;
+                    ++left;
+                    --right;
+                }
+            }
+            uint32_t lsec, rfirst;
+            if (left > right) { lsec = (uint32_t)right; rfirst = (uint32_t)left; }
+            else if (ls) { lsec = (uint32_t)(left - 1); rfirst = (uint32_t)left; }
+            else if (rs) { lsec = (uint32_t)right; rfirst = (uint32_t)(right + 1); }
+            else if (bin_of((uint32_t)left) > best_plane) { lsec = (uint32_t)(left - 1); rfirst = (uint32_t)left; }
+            else { lsec = (uint32_t)left; rfirst = (uint32_t)(left + 1); }
+            node.count = 0;
+            out[ni] = node;
+            if (sp + 2 > SUB_STACK || (int)lsec < (int)f.first || rfirst > f.second) {  // deeper than any subtree of SMALL objects can be
+                atomicOr(&ct->error, 16u);
+                break;
+            }
+            Frame r{};
+            cb_put(r.cb, rcb);
+            r.first = rfirst; r.second = f.second; r.depth = f.depth + 1; r.parent = ni; r.side = 1;
+            st[sp++] = r;
+            Frame l{};
+            cb_put(l.cb, lcb);
+            l.first = f.first; l.second = lsec; l.depth = f.depth + 1; l.parent = ni; l.side = 0;
+            st[sp++] = l;
+        } else {
+            node.first = (int32_t)f.first;
+            node.count = (int32_t)(f.second - f.first + 1);
+            node.left = node.right = -1;
+            out[ni] = node;
+            leafstart[f.first] = 1u;
+            maxl = max(maxl, f.second - f.first + 1);
+        }
+    }
+    sr[si].n_local = (uint32_t)local;
+    atomicMax(&ct->max_depth, maxd);
+    atomicMax(&ct->max_leaf, maxl);
+}
+
+// ---- assembly into DFS preorder ---------------------------------------------
+__global__ void k_copy_subtrees(const SRoot* sr, uint32_t n, const BuildNode* T, const uint32_t* P, BuildNode* fin) {
+    const uint32_t si = blockIdx.x * blockDim.x + threadIdx.x;
+    if (si >= n) return;
+    const SRoot r = sr[si];
+    const int32_t pre = (int32_t)(r.lturns + 2u * P[r.first]);
+    const BuildNode* src = T + 2 * (size_t)r.first;
+    for (uint32_t j = 0; j < r.n_local; ++j) {
+        BuildNode nd = src[j];
+        if (nd.count == 0) {
+            nd.left += pre;
+            nd.right += pre;
+        }
+        fin[pre + j] = nd;
+    }
+}
+
+__global__ void k_level_leaves(const LLeaf* ll, uint32_t n, const float4* rec, const float* bounds, const uint32_t* P,
+                               BuildNode* fin) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const LLeaf l = ll[i];
+    GBox bv = box_empty();
+    for (uint32_t id = l.first; id < l.first + l.count; ++id) {
+        const float* bb = &bounds[6 * (size_t)__float_as_uint(rec[id].w)];
+        bv.mn[0] = smin(bv.mn[0], bb[0]); bv.mn[1] = smin(bv.mn[1], bb[1]); bv.mn[2] = smin(bv.mn[2], bb[2]);
+        bv.mx[0] = smax(bv.mx[0], bb[3]); bv.mx[1] = smax(bv.mx[1], bb[4]); bv.mx[2] = smax(bv.mx[2], bb[5]);
+    }
+    BuildNode nd{};
+    nd.mn = mk(bv.mn[0], bv.mn[1], bv.mn[2]);
+    nd.mx = mk(bv.mx[0], bv.mx[1], bv.mx[2]);
+    nd.left = nd.right = -1;
+    nd.first = (int32_t)l.first;
+    nd.count = (int32_t)l.count;
+    fin[l.lturns + 2u * P[l.first]] = nd;
+}
+
+__global__ void k_level_interior(const GNode* g, uint32_t b, uint32_t n, const uint32_t* P, BuildNode* fin) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const GNode nd = g[b + i];
+    const int32_t pre = (int32_t)(nd.lturns + 2u * P[nd.first]);
+    const int32_t l = pre + 1;
+    const int32_t r = pre + 2 * (int32_t)(P[nd.first + nd.L] - P[nd.first]);
+    const BuildNode L = fin[l], R = fin[r];
+    GBox bv = box_empty();
+    grow(bv, GBox{{L.mn.x, L.mn.y, L.mn.z}, {L.mx.x, L.mx.y, L.mx.z}});
+    grow(bv, GBox{{R.mn.x, R.mn.y, R.mn.z}, {R.mx.x, R.mx.y, R.mx.z}});
+    BuildNode o{};
+    o.mn = mk(bv.mn[0], bv.mn[1], bv.mn[2]);
+    o.mx = mk(bv.mx[0], bv.mx[1], bv.mx[2]);
+    o.left = l;
+    o.right = r;
+    o.first = 0;
+    o.count = 0;
+    fin[pre] = o;
+}
+
+__global__ void k_ids(const float4* rec, uint32_t n, uint32_t* ids) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) ids[i] = __float_as_uint(rec[i].w);
+}
+
+// ---- host driver --------------------------------------------------------------
+struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~Buf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t ensure(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n ? n : 16);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    // grow keeping the first `keep` bytes
+    hipError_t grow(size_t n, size_t keep, hipStream_t s) {
+        if (n <= bytes && p) return hipSuccess;
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, n);
+        if (e != hipSuccess) return e;
+        if (p && keep) e = hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
+        if (p) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(p);
+        }
+        p = q;
+        bytes = n;
+        return hipSuccess;
+    }
+    template <typename T>
+    T* as() const { return (T*)p; }
+};
+
+#define GBCHK(expr)                                                                  \
+    do {                                                                             \
+        hipError_t e_ = (expr);                                                      \
+        if (e_ != hipSuccess) return std::string(#expr) + ": " + hipGetErrorString(e_); \
+    } while (0)
+
+static uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b - 1) / b); }
+
+}  // namespace gb
+
+// Builds hs.nodes (DFS preorder), hs.ids, hs.depth, hs.max_leaf on the device from
+// hs.centroid / hs.bounds; identical to build_bvh().  Returns an error string.
+std::string device_build_bvh(HostScene& hs, hipStream_t st, double* kernel_ms) {
+    using namespace gb;
+    const uint32_t N = hs.n_obj;
+    if (N == 0) return "no objects";
+    auto t0 = std::chrono::steady_clock::now();
+    Buf cen, bnd, rec, leafstart, part0;
+    GBCHK(cen.ensure(12 * (size_t)N));
+    GBCHK(bnd.ensure(24 * (size_t)N));
+    GBCHK(rec.ensure(16 * (size_t)N));
+    GBCHK(leafstart.ensure(4 * ((size_t)N + 1)));
+    const uint32_t nb0 = blocks(N + 1, 256);
+    GBCHK(part0.ensure(24 * (size_t)nb0));
+    GBCHK(hipMemcpyAsync(cen.p, hs.centroid.data(), 12 * (size_t)N, hipMemcpyHostToDevice, st));
+    GBCHK(hipMemcpyAsync(bnd.p, hs.bounds.data(), 24 * (size_t)N, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_init, dim3(nb0), dim3(256), 0, st, cen.as<float>(), N, rec.as<float4>(),
+                       leafstart.as<uint32_t>(), part0.as<uint32_t>());
+    GBCHK(hipGetLastError());
+    hipEvent_t ev0, ev1;
+    GBCHK(hipEventCreate(&ev0));
+    GBCHK(hipEventCreate(&ev1));
+    GBCHK(hipEventRecord(ev0, st));
+    std::vector<uint32_t> hp(6 * (size_t)nb0);
+    GBCHK(hipMemcpyAsync(hp.data(), part0.p, hp.size() * 4, hipMemcpyDeviceToHost, st));
+    GBCHK(hipStreamSynchronize(st));
+    auto dec = [](uint32_t u) {
+        uint32_t b = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+        float f;
+        memcpy(&f, &b, 4);
+        return f;
+    };
+    uint32_t red[6] = {hp[0], hp[1], hp[2], hp[3], hp[4], hp[5]};
+    for (uint32_t b = 1; b < nb0; ++b)
+        for (int a = 0; a < 6; ++a) red[a] = a < 3 ? std::min(red[a], hp[6 * b + a]) : std::max(red[a], hp[6 * b + a]);
+    GBox rootcb;
+    for (int a = 0; a < 3; ++a) {
+        rootcb.mn[a] = dec(red[a]);
+        rootcb.mx[a] = dec(red[3 + a]);
+    }
+
+    // scratch of the level phase, grown on demand
+    Buf gn, srb, llb, ctr, nc, c0, chunk_node, part, cnt, off, SL, SR, PL, PR, tmp;
+    size_t gcap = 1024, scap = 1024, lcap = 1024;
+    GBCHK(gn.ensure(gcap * sizeof(GNode)));
+    GBCHK(srb.ensure(scap * sizeof(SRoot)));
+    GBCHK(llb.ensure(lcap * sizeof(LLeaf)));
+    GBCHK(ctr.ensure(sizeof(Ctr)));
+    Ctr hc{};
+    // the root: KIRK's split() on (0, N-1) with the centroid box of everything
+    const bool root_split = (N - 1u > 1u) && worth(rootcb);
+    if (root_split && N > SMALL) {
+        GNode r{};
+        cb_put(r.cb, rootcb);
+        r.first = 0; r.count = N; r.lturns = 0; r.depth = 1; r.plane = -1;
+        GBCHK(hipMemcpyAsync(gn.p, &r, sizeof(r), hipMemcpyHostToDevice, st));
+        hc.n_gnode = 1;
+    } else if (root_split) {
+        SRoot r{};
+        cb_put(r.cb, rootcb);
+        r.first = 0; r.count = N; r.lturns = 0; r.depth = 1;
+        GBCHK(hipMemcpyAsync(srb.p, &r, sizeof(r), hipMemcpyHostToDevice, st));
+        hc.n_sroot = 1;
+    } else {
+        LLeaf l{0, N, 0, 1};
+        GBCHK(hipMemcpyAsync(llb.p, &l, sizeof(l), hipMemcpyHostToDevice, st));
+        const uint32_t one = 1;
+        GBCHK(hipMemcpyAsync(leafstart.p, &one, 4, hipMemcpyHostToDevice, st));
+        hc.n_lleaf = 1;
+        hc.max_leaf = N;
+    }
+    hc.max_depth = 1;
+    GBCHK(hipMemcpyAsync(ctr.p, &hc, sizeof(hc), hipMemcpyHostToDevice, st));
+    // hipcub scratch
+    size_t tb1 = 0, tb2 = 0;
+    GBCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)N + 2, st));
+    GBCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)N + 2, st));
+    GBCHK(tmp.ensure(std::max(tb1, tb2)));
+    GBCHK(SL.ensure(16 * (size_t)N));
+    GBCHK(SR.ensure(16 * (size_t)N));
+    GBCHK(PL.ensure(4 * (size_t)N));
+    GBCHK(PR.ensure(4 * (size_t)N));
+    std::vector<std::pair<uint32_t, uint32_t>> levels;  // (begin, count) in gn
+    uint32_t lb = 0, le = hc.n_gnode;
+    while (le > lb) {
+        const uint32_t n = le - lb;
+        levels.emplace_back(lb, n);
+        // children of this level: at most 2 per node in each list
+        if (le + 2 * (size_t)n > gcap) {
+            size_t nc2 = std::max(gcap * 2, (size_t)le + 2 * n);
+            GBCHK(gn.grow(nc2 * sizeof(GNode), (size_t)le * sizeof(GNode), st));
+            gcap = nc2;
+        }
+        if (hc.n_sroot + 2 * (size_t)n > scap) {
+            size_t nc2 = std::max(scap * 2, (size_t)hc.n_sroot + 2 * n);
+            GBCHK(srb.grow(nc2 * sizeof(SRoot), (size_t)hc.n_sroot * sizeof(SRoot), st));
+            scap = nc2;
+        }
+        if (hc.n_lleaf + 2 * (size_t)n > lcap) {
+            size_t nc2 = std::max(lcap * 2, (size_t)hc.n_lleaf + 2 * n);
+            GBCHK(llb.grow(nc2 * sizeof(LLeaf), (size_t)hc.n_lleaf * sizeof(LLeaf), st));
+            lcap = nc2;
+        }
+        GBCHK(nc.ensure(4 * ((size_t)n + 1)));
+        GBCHK(c0.ensure(4 * ((size_t)n + 1)));
+        hipLaunchKernelGGL(k_nchunks, dim3(blocks(n + 1, 256)), dim3(256), 0, st, gn.as<GNode>(), lb, n,
+                           nc.as<uint32_t>());
+        size_t tbytes = tmp.bytes;
+        GBCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tbytes, nc.as<uint32_t>(), c0.as<uint32_t>(), (int)n + 1, st));
+        uint32_t nch = 0;
+        GBCHK(hipMemcpyAsync(&nch, c0.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, st));
+        GBCHK(hipStreamSynchronize(st));
+        GBCHK(chunk_node.ensure(4 * (size_t)nch));
+        GBCHK(part.ensure(4 * (size_t)BW * nch));
+        GBCHK(cnt.ensure(8 * ((size_t)nch + 1)));
+        GBCHK(off.ensure(8 * ((size_t)nch + 1)));
+        hipLaunchKernelGGL(k_chunk_list, dim3(n), dim3(256), 0, st, gn.as<GNode>(), lb, c0.as<uint32_t>(),
+                           chunk_node.as<uint32_t>());
+        hipLaunchKernelGGL(k_bin, dim3(nch), dim3(256), 0, st, rec.as<float4>(), gn.as<GNode>(),
+                           chunk_node.as<uint32_t>(), part.as<uint32_t>());
+        hipLaunchKernelGGL(k_pick, dim3(n), dim3(256), 0, st, gn.as<GNode>(), lb, part.as<uint32_t>(), (uint32_t)gcap,
+                           srb.as<SRoot>(), (uint32_t)scap, llb.as<LLeaf>(), (uint32_t)lcap,
+                           leafstart.as<uint32_t>(), ctr.as<Ctr>());
+        hipLaunchKernelGGL(k_classify, dim3(nch), dim3(256), 0, st, rec.as<float4>(), gn.as<GNode>(),
+                           chunk_node.as<uint32_t>(), cnt.as<uint64_t>());
+        tbytes = tmp.bytes;
+        GBCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tbytes, cnt.as<uint64_t>(), off.as<uint64_t>(), (int)nch + 1, st));
+        hipLaunchKernelGGL(k_swap_write, dim3(nch), dim3(256), 0, st, rec.as<float4>(), gn.as<GNode>(),
+                           chunk_node.as<uint32_t>(), off.as<uint64_t>(), SL.as<float4>(), SR.as<float4>(),
+                           PL.as<uint32_t>(), PR.as<uint32_t>());
+        hipLaunchKernelGGL(k_swap_apply, dim3(nch), dim3(256), 0, st, rec.as<float4>(), gn.as<GNode>(),
+                           chunk_node.as<uint32_t>(), off.as<uint64_t>(), SL.as<float4>(), SR.as<float4>(),
+                           PL.as<uint32_t>(), PR.as<uint32_t>());
+        GBCHK(hipGetLastError());
+        GBCHK(hipMemcpyAsync(&hc, ctr.p, sizeof(hc), hipMemcpyDeviceToHost, st));
+        GBCHK(hipStreamSynchronize(st));
+        if (hc.error) return "device BVH build failed (code " + std::to_string(hc.error) + ")";
+        lb = le;
+        le = hc.n_gnode;
+    }
+    // small subtrees
+    Buf T, fin, idsb;
+    GBCHK(T.ensure(2 * (size_t)N * sizeof(BuildNode)));
+    if (hc.n_sroot)
+        hipLaunchKernelGGL(k_subtree, dim3(blocks(hc.n_sroot, 64)), dim3(64), 0, st, rec.as<float4>(),
+                           bnd.as<float>(), srb.as<SRoot>(), hc.n_sroot, T.as<BuildNode>(), leafstart.as<uint32_t>(),
+                           ctr.as<Ctr>());
+    GBCHK(hipGetLastError());
+    // leaf starts -> P (exclusive), P[N] = leaves
+    Buf P;
+    GBCHK(P.ensure(4 * ((size_t)N + 1)));
+    size_t tbytes = tmp.bytes;
+    GBCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tbytes, leafstart.as<uint32_t>(), P.as<uint32_t>(), (int)N + 1, st));
+    uint32_t n_leaves = 0;
+    GBCHK(hipMemcpyAsync(&n_leaves, P.as<uint32_t>() + N, 4, hipMemcpyDeviceToHost, st));
+    GBCHK(hipMemcpyAsync(&hc, ctr.p, sizeof(hc), hipMemcpyDeviceToHost, st));
+    GBCHK(hipStreamSynchronize(st));
+    if (hc.error) return "device BVH build failed (code " + std::to_string(hc.error) + ")";
+    const size_t n_nodes = 2 * (size_t)n_leaves - 1;
+    GBCHK(fin.ensure(n_nodes * sizeof(BuildNode)));
+    if (hc.n_sroot)
+        hipLaunchKernelGGL(k_copy_subtrees, dim3(blocks(hc.n_sroot, 256)), dim3(256), 0, st, srb.as<SRoot>(),
+                           hc.n_sroot, T.as<BuildNode>(), P.as<uint32_t>(), fin.as<BuildNode>());
+    if (hc.n_lleaf)
+        hipLaunchKernelGGL(k_level_leaves, dim3(blocks(hc.n_lleaf, 256)), dim3(256), 0, st, llb.as<LLeaf>(),
+                           hc.n_lleaf, rec.as<float4>(), bnd.as<float>(), P.as<uint32_t>(), fin.as<BuildNode>());
+    for (size_t l = levels.size(); l-- > 0;)
+        hipLaunchKernelGGL(k_level_interior, dim3(blocks(levels[l].second, 256)), dim3(256), 0, st, gn.as<GNode>(),
+                           levels[l].first, levels[l].second, P.as<uint32_t>(), fin.as<BuildNode>());
+    GBCHK(idsb.ensure(4 * (size_t)N));
+    hipLaunchKernelGGL(k_ids, dim3(blocks(N, 256)), dim3(256), 0, st, rec.as<float4>(), N, idsb.as<uint32_t>());
+    GBCHK(hipGetLastError());
+    GBCHK(hipEventRecord(ev1, st));
+    hs.nodes.resize(n_nodes);
+    hs.ids.resize(N);
+    GBCHK(hipMemcpyAsync(hs.nodes.data(), fin.p, n_nodes * sizeof(BuildNode), hipMemcpyDeviceToHost, st));
+    GBCHK(hipMemcpyAsync(hs.ids.data(), idsb.p, 4 * (size_t)N, hipMemcpyDeviceToHost, st));
+    GBCHK(hipStreamSynchronize(st));
+    float ms = 0.0f;
+    GBCHK(hipEventElapsedTime(&ms, ev0, ev1));
+    (void)hipEventDestroy(ev0);
+    (void)hipEventDestroy(ev1);
+    if (kernel_ms) *kernel_ms = ms;
+    hs.depth = hc.max_depth;
+    hs.max_leaf = hc.max_leaf;
+    (void)t0;
+    return std::string();
+}
+
+}  // namespace khp

@@ -1103,7 +1103,8 @@ extern "C" khp_status khp_set_scene(khp_ctx* c, const khp_scene* s) {
     if (!err.empty()) return fail(KHP_EINVAL, err);
     c->scene_set = true;
     c->built = false;
-    c->st.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->st.flatten_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->st.build_ms = c->st.flatten_ms;
     return KHP_OK;
 }
 
@@ -1120,11 +1121,22 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     if (!c->scene_set) return fail(KHP_ENOTREADY, "khp_set_scene first");
     HIPCHK(hipSetDevice(c->device));
     auto t0 = std::chrono::steady_clock::now();
-    unsigned nt = std::thread::hardware_concurrency();
-    build_bvh(c->hs, (int)std::max(1u, std::min(nt, 32u)));
+    const bool host_build = (c->flags & KHP_CTX_HOST_BUILD) || getenv("KHP_HOST_BUILD");
+    c->st.bvh_kernel_ms = 0.0;
+    if (host_build) {
+        unsigned nt = std::thread::hardware_concurrency();
+        build_bvh(c->hs, (int)std::max(1u, std::min(nt, 32u)));
+    } else {
+        std::string err = device_build_bvh(c->hs, c->stream, &c->st.bvh_kernel_ms);
+        if (!err.empty()) return fail(KHP_EDEVICE, err);
+    }
+    c->st.bvh_on_device = host_build ? 0u : 1u;
+    auto tb = std::chrono::steady_clock::now();
     make_device_layout(c->hs);
     auto t1 = std::chrono::steady_clock::now();
-    c->st.build_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    c->st.bvh_ms = std::chrono::duration<double, std::milli>(tb - t0).count();
+    c->st.layout_ms = std::chrono::duration<double, std::milli>(t1 - tb).count();
+    c->st.build_ms = c->st.flatten_ms + c->st.bvh_ms + c->st.layout_ms;
     if (c->hs.depth + 1 > (uint32_t)STACK_MAX)
         return fail(KHP_EUNSUPPORTED, "BVH deeper than the traversal stack (" + std::to_string(c->hs.depth) + ")");
     if (c->hs.n_slots >= MAX_SLOTS)
@@ -1594,6 +1606,28 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out_rgba, out.p, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    return KHP_OK;
+}
+
+
+extern "C" khp_status khp_read_bvh(khp_ctx* c, uint32_t* n_nodes, uint32_t* depth, float* node_boxes,
+                                   int32_t* node_first, int32_t* node_count, int32_t* object_ids) {
+    if (!c || !n_nodes) return fail(KHP_EINVAL, "ctx or n_nodes is null");
+    if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
+    const HostScene& hs = c->hs;
+    *n_nodes = (uint32_t)hs.nodes.size();
+    if (depth) *depth = hs.depth;
+    for (size_t i = 0; i < hs.nodes.size(); ++i) {
+        const BuildNode& n = hs.nodes[i];
+        if (node_boxes) {
+            const float b[6] = {n.mn.x, n.mn.y, n.mn.z, n.mx.x, n.mx.y, n.mx.z};
+            memcpy(node_boxes + 6 * i, b, sizeof(b));
+        }
+        if (node_first) node_first[i] = n.count ? n.first : -1;
+        if (node_count) node_count[i] = n.count;
+    }
+    if (object_ids)
+        for (uint32_t i = 0; i < hs.n_obj; ++i) object_ids[i] = (int32_t)hs.ids[i];
     return KHP_OK;
 }
 

@@ -30,6 +30,7 @@ RENDER_OUT_DEVICE = 1 << 0
 RENDER_NO_READBACK = 1 << 1
 RENDER_STATS = 1 << 2
 CTX_STATS = 1 << 0
+CTX_HOST_BUILD = 1 << 1
 
 F3 = c_float * 3
 
@@ -80,7 +81,8 @@ class Stats(ctypes.Structure):
                 ("bounce_extend_ms", c_double * 16), ("bounce_shadow_ms", c_double * 16),
                 ("bounce_wave_iters", c_uint64 * 16), ("bounce_lanes_busy", c_uint64 * 16),
                 ("bounce_shadow_wave_iters", c_uint64 * 16), ("bounce_shadow_lanes_busy", c_uint64 * 16),
-                ("step_cycles", c_uint64 * 4)]
+                ("step_cycles", c_uint64 * 4), ("bvh_on_device", c_uint32), ("pad0", c_uint32),
+                ("flatten_ms", c_double), ("bvh_ms", c_double), ("bvh_kernel_ms", c_double), ("layout_ms", c_double)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if not isinstance(getattr(self, k), (int, float)) else getattr(self, k))
@@ -110,7 +112,7 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_comm_unique_id", "khp_comm_init", "khp_gather_framebuffer", "khp_bsdf_kind_from_name",
             "khp_bsdf_name", "khp_shader_kind_from_name", "khp_camera_setup", "khp_fibers_to_cones",
             "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus", "khp_host_build", "khp_debug_queue",
-            "khp_read_rgba8", "khp_tonemap_defaults"]
+            "khp_read_rgba8", "khp_tonemap_defaults", "khp_read_bvh"]
 
 _lib = None
 
@@ -144,6 +146,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
         "khp_read_rgba8": (c_int, [c_void_p, P(Tonemap), P(c_uint8)]),
         "khp_tonemap_defaults": (None, [P(Tonemap)]),
+        "khp_read_bvh": (c_int, [c_void_p, P(c_uint32), P(c_uint32), P(c_float), P(c_int32), P(c_int32), P(c_int32)]),
         "khp_trace_closest": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_int32),
                                       P(c_float)]),
         "khp_trace_any": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_uint8)]),

@@ -49,11 +49,11 @@ class ShaderFactory:
 class HipContext:
     """One khp_ctx: one GPU, one stream (one process per GPU)."""
 
-    def __init__(self, device: int = 0, stats: bool = False):
+    def __init__(self, device: int = 0, stats: bool = False, host_build: bool = False):
         self.lib = N.load_library()
         self.ptr = ctypes.c_void_p()
-        N.check(self.lib, self.lib.khp_create(ctypes.byref(self.ptr), device, N.CTX_STATS if stats else 0),
-                "khp_create")
+        flags = (N.CTX_STATS if stats else 0) | (N.CTX_HOST_BUILD if host_build else 0)
+        N.check(self.lib, self.lib.khp_create(ctypes.byref(self.ptr), device, flags), "khp_create")
         self._scene = None
 
     def close(self):
@@ -84,6 +84,21 @@ class HipContext:
         ptr = out.ctypes.data_as(ctypes.c_void_p) if (readback and out is not None) else None
         N.check(self.lib, self.lib.khp_render(self.ptr, ctypes.byref(p), ptr), "khp_render")
         return out
+
+    def read_bvh(self) -> dict:
+        """The tree khp_build_accel built (khp_read_bvh), in khp_host_build's layout."""
+        nn, dep = ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(self.lib, self.lib.khp_read_bvh(self.ptr, ctypes.byref(nn), ctypes.byref(dep), None, None, None, None),
+                "khp_read_bvh")
+        n = nn.value
+        boxes = np.empty((n, 6), np.float32)
+        first = np.empty(n, np.int32)
+        count = np.empty(n, np.int32)
+        ids = np.empty(self._scene.n_objects, np.int32)
+        ip = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        N.check(self.lib, self.lib.khp_read_bvh(self.ptr, ctypes.byref(nn), ctypes.byref(dep), N.fptr(boxes), ip(first),
+                                                ip(count), ip(ids)), "khp_read_bvh")
+        return {"boxes": boxes, "first": first, "count": count, "ids": ids, "depth": dep.value}
 
     def read_framebuffer(self, width, height) -> np.ndarray:
         out = np.zeros((height, width, 3), np.float32)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 2
+#define KHP_ABI_VERSION 3
 
 typedef struct khp_ctx khp_ctx;
 
@@ -178,10 +178,18 @@ typedef struct {
     /* diagnostic builds (KHP_PROFILE_STEPS=1) only: k_extend wave cycles spent in
      * resolve / record fetch / compute / loop+refill, summed over waves */
     uint64_t step_cycles[4];
+    /* ABI 3: where khp_build_accel built the BVH and how long it took */
+    uint32_t bvh_on_device, pad0;    /* 1: device build (default), 0: host   */
+    double flatten_ms;               /* khp_set_scene (host flatten)          */
+    double bvh_ms;                   /* BVH build wall time incl. transfers   */
+    double bvh_kernel_ms;            /* device build: GPU time of its kernels  */
+    double layout_ms;                /* node pairing + leaf slots (host)      */
 } khp_stats;
 #define KHP_MAX_BOUNCE_STATS 16
 
 #define KHP_CTX_STATS  (1u << 0)   /* instrumented kernels: count node/prim visits */
+#define KHP_CTX_HOST_BUILD (1u << 1) /* khp_build_accel builds the BVH on the host
+                                       (default: on the device, the same tree)   */
 
 /* ---- context --------------------------------------------------------------- */
 /* device: HIP device ordinal (one process per GPU). */
@@ -252,6 +260,11 @@ khp_status khp_comm_init(khp_ctx* ctx, int nranks, int rank, const uint8_t id[12
 /* Gather every rank's owned tiles (per p->tile_*) into rank root's device
  * framebuffer over RCCL; root may then khp_read_framebuffer. Collective. */
 khp_status khp_gather_framebuffer(khp_ctx* ctx, const khp_render_params* p, int root);
+
+/* The BVH khp_build_accel built (device or host path), in the layout of
+ * khp_host_build below: call with null arrays for *n_nodes / *depth. */
+khp_status khp_read_bvh(khp_ctx* ctx, uint32_t* n_nodes, uint32_t* depth, float* node_boxes, int32_t* node_first,
+                        int32_t* node_count, int32_t* object_ids);
 
 /* ---- host-only introspection (no device needed) ---------------------------- */
 /* Runs exactly the flatten + BVH build of khp_set_scene/khp_build_accel on the
