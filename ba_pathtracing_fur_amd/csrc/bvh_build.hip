@@ -26,6 +26,7 @@
 #include <string>
 #include <vector>
 
+#include "device_build.h"
 #include "scene.h"
 
 namespace khp {
@@ -691,9 +692,9 @@ static uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b - 1) /
 
 }  // namespace gb
 
-// Builds hs.nodes (DFS preorder), hs.ids, hs.depth, hs.max_leaf on the device from
-// hs.centroid / hs.bounds; identical to build_bvh().  Returns an error string.
-std::string device_build_bvh(HostScene& hs, hipStream_t st, double* kernel_ms) {
+// Builds the DFS-preorder tree of build_bvh() on the device from hs.centroid /
+// hs.bounds into t; sets hs.depth, hs.max_leaf.  Returns an error string.
+std::string device_build_bvh(HostScene& hs, hipStream_t st, DeviceTree& t, double* kernel_ms) {
     using namespace gb;
     const uint32_t N = hs.n_obj;
     if (N == 0) return "no objects";
@@ -832,7 +833,7 @@ std::string device_build_bvh(HostScene& hs, hipStream_t st, double* kernel_ms) {
         le = hc.n_gnode;
     }
     // small subtrees
-    Buf T, fin, idsb;
+    Buf T;
     GBCHK(T.ensure(2 * (size_t)N * sizeof(BuildNode)));
     if (hc.n_sroot)
         hipLaunchKernelGGL(k_subtree, dim3(blocks(hc.n_sroot, 64)), dim3(64), 0, st, rec.as<float4>(),
@@ -840,43 +841,245 @@ std::string device_build_bvh(HostScene& hs, hipStream_t st, double* kernel_ms) {
                            ctr.as<Ctr>());
     GBCHK(hipGetLastError());
     // leaf starts -> P (exclusive), P[N] = leaves
-    Buf P;
-    GBCHK(P.ensure(4 * ((size_t)N + 1)));
+    GBCHK(t.P.ensure(4 * ((size_t)N + 1)));
     size_t tbytes = tmp.bytes;
-    GBCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tbytes, leafstart.as<uint32_t>(), P.as<uint32_t>(), (int)N + 1, st));
+    GBCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tbytes, leafstart.as<uint32_t>(), t.P.as<uint32_t>(), (int)N + 1,
+                                           st));
     uint32_t n_leaves = 0;
-    GBCHK(hipMemcpyAsync(&n_leaves, P.as<uint32_t>() + N, 4, hipMemcpyDeviceToHost, st));
+    GBCHK(hipMemcpyAsync(&n_leaves, t.P.as<uint32_t>() + N, 4, hipMemcpyDeviceToHost, st));
     GBCHK(hipMemcpyAsync(&hc, ctr.p, sizeof(hc), hipMemcpyDeviceToHost, st));
     GBCHK(hipStreamSynchronize(st));
     if (hc.error) return "device BVH build failed (code " + std::to_string(hc.error) + ")";
     const size_t n_nodes = 2 * (size_t)n_leaves - 1;
-    GBCHK(fin.ensure(n_nodes * sizeof(BuildNode)));
+    GBCHK(t.nodes.ensure(n_nodes * sizeof(BuildNode)));
+    BuildNode* fin = t.nodes.as<BuildNode>();
+    const uint32_t* P = t.P.as<uint32_t>();
     if (hc.n_sroot)
         hipLaunchKernelGGL(k_copy_subtrees, dim3(blocks(hc.n_sroot, 256)), dim3(256), 0, st, srb.as<SRoot>(),
-                           hc.n_sroot, T.as<BuildNode>(), P.as<uint32_t>(), fin.as<BuildNode>());
+                           hc.n_sroot, T.as<BuildNode>(), P, fin);
     if (hc.n_lleaf)
         hipLaunchKernelGGL(k_level_leaves, dim3(blocks(hc.n_lleaf, 256)), dim3(256), 0, st, llb.as<LLeaf>(),
-                           hc.n_lleaf, rec.as<float4>(), bnd.as<float>(), P.as<uint32_t>(), fin.as<BuildNode>());
+                           hc.n_lleaf, rec.as<float4>(), bnd.as<float>(), P, fin);
     for (size_t l = levels.size(); l-- > 0;)
         hipLaunchKernelGGL(k_level_interior, dim3(blocks(levels[l].second, 256)), dim3(256), 0, st, gn.as<GNode>(),
-                           levels[l].first, levels[l].second, P.as<uint32_t>(), fin.as<BuildNode>());
-    GBCHK(idsb.ensure(4 * (size_t)N));
-    hipLaunchKernelGGL(k_ids, dim3(blocks(N, 256)), dim3(256), 0, st, rec.as<float4>(), N, idsb.as<uint32_t>());
+                           levels[l].first, levels[l].second, P, fin);
+    GBCHK(t.ids.ensure(4 * (size_t)N));
+    hipLaunchKernelGGL(k_ids, dim3(blocks(N, 256)), dim3(256), 0, st, rec.as<float4>(), N, t.ids.as<uint32_t>());
     GBCHK(hipGetLastError());
     GBCHK(hipEventRecord(ev1, st));
-    hs.nodes.resize(n_nodes);
-    hs.ids.resize(N);
-    GBCHK(hipMemcpyAsync(hs.nodes.data(), fin.p, n_nodes * sizeof(BuildNode), hipMemcpyDeviceToHost, st));
-    GBCHK(hipMemcpyAsync(hs.ids.data(), idsb.p, 4 * (size_t)N, hipMemcpyDeviceToHost, st));
+    GBCHK(hipEventSynchronize(ev1));
+    float ms = 0.0f;
+    GBCHK(hipEventElapsedTime(&ms, ev0, ev1));
+    (void)hipEventDestroy(ev0);
+    (void)hipEventDestroy(ev1);
+    if (kernel_ms) *kernel_ms = ms;
+    t.n_nodes = (uint32_t)n_nodes;
+    t.n_leaves = n_leaves;
+    hs.depth = hc.max_depth;
+    hs.max_leaf = hc.max_leaf;
+    (void)t0;
+    return std::string();
+}
+
+std::string download_tree(const DeviceTree& t, HostScene& hs, hipStream_t st) {
+    hs.nodes.resize(t.n_nodes);
+    hs.ids.resize(hs.n_obj);
+    GBCHK(hipMemcpyAsync(hs.nodes.data(), t.nodes.p, (size_t)t.n_nodes * sizeof(BuildNode), hipMemcpyDeviceToHost, st));
+    GBCHK(hipMemcpyAsync(hs.ids.data(), t.ids.p, 4 * (size_t)hs.n_obj, hipMemcpyDeviceToHost, st));
+    GBCHK(hipStreamSynchronize(st));
+    return std::string();
+}
+
+// ---- make_device_layout on the device (scene.cpp) -------------------------------
+namespace gb {
+
+// h[i] = interior node i with at least one interior child: it opens a record pair.
+__global__ void k_lay_flags(const BuildNode* fin, uint32_t n, uint32_t* h) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    uint32_t v = 0;
+    if (i < n) {
+        const BuildNode nd = fin[i];
+        if (nd.count == 0) v = (fin[nd.left].count == 0 || fin[nd.right].count == 0) ? 1u : 0u;
+    }
+    h[i] = v;
+}
+
+// The host pops interior nodes in preorder and gives the interior children of
+// the k-th pair-opening node the records (2 + 2k, 2 + 2k + 1).
+__global__ void k_lay_recof(const BuildNode* fin, uint32_t n, const uint32_t* H, int32_t* rec_of) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const BuildNode nd = fin[i];
+    if (i == 0) rec_of[0] = nd.count == 0 ? 0 : -1;
+    if (nd.count != 0) return;
+    const bool li = fin[nd.left].count == 0, ri = fin[nd.right].count == 0;
+    const int32_t base = (int32_t)(2u + 2u * H[i]);
+    if (li) rec_of[nd.left] = base;
+    if (ri) rec_of[nd.right] = li ? base + 1 : base;
+}
+
+// leaves in preorder = leaves by first; ordinal = P[first]
+__global__ void k_lay_leaves(const BuildNode* fin, uint32_t n, const uint32_t* P, uint32_t* lfirst, uint2* lfun) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const BuildNode nd = fin[i];
+    if (nd.count == 0) return;
+    const uint32_t l = P[nd.first], c = (uint32_t)nd.count;
+    lfirst[l] = (uint32_t)nd.first;
+    // slot advance as a function of the running slot count's parity:
+    // a leaf of >= 2 candidates starts at an even slot
+    lfun[l] = c >= 2 ? make_uint2(c, c + 1) : make_uint2(c, c);
+}
+
+struct ParityCompose {  // (f then g) for the parity-dependent slot advance
+    __host__ __device__ uint2 operator()(const uint2& f, const uint2& g) const {
+        return make_uint2(f.x + ((f.x & 1u) ? g.y : g.x), f.y + (((1u + f.y) & 1u) ? g.y : g.x));
+    }
+};
+
+__global__ void k_lay_slot0(const uint2* lfun, const uint2* scanned, uint32_t nl, uint32_t* slot0) {
+    const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= nl) return;
+    const uint32_t ns = scanned[l].x;  // slots before this leaf, from an even start
+    const bool two = lfun[l].y != lfun[l].x;
+    slot0[l] = ns + ((two && (ns & 1u)) ? 1u : 0u);
+}
+
+__device__ __forceinline__ void child_ref(const BuildNode* fin, int32_t c, const int32_t* rec_of, const uint32_t* P,
+                                          const uint32_t* slot0, int32_t& ref, int32_t& cnt) {
+    const BuildNode nd = fin[c];
+    if (nd.count > 0) {
+        const uint32_t ce = (uint32_t)nd.count < LEAF_CNT_ESC ? (uint32_t)nd.count : LEAF_CNT_ESC;
+        ref = (int32_t)(LEAF_BIT | (ce << 24) | slot0[P[nd.first]]);
+        cnt = nd.count;
+    } else {
+        ref = rec_of[c];
+        cnt = 0;
+    }
+}
+
+__global__ void k_lay_nodes(const BuildNode* fin, uint32_t n, const int32_t* rec_of, const uint32_t* P,
+                            const uint32_t* slot0, DevNode* dn) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const BuildNode nd = fin[i];
+    if (nd.count != 0) return;
+    const BuildNode L = fin[nd.left], R = fin[nd.right];
+    DevNode d;
+    d.a[0] = L.mn.x; d.a[1] = L.mn.y; d.a[2] = L.mn.z; d.a[3] = L.mx.x;
+    d.b[0] = L.mx.y; d.b[1] = L.mx.z; d.b[2] = R.mn.x; d.b[3] = R.mn.y;
+    d.c[0] = R.mn.z; d.c[1] = R.mx.x; d.c[2] = R.mx.y; d.c[3] = R.mx.z;
+    child_ref(fin, nd.left, rec_of, P, slot0, d.ref[0], d.cnt[0]);
+    child_ref(fin, nd.right, rec_of, P, slot0, d.ref[1], d.cnt[1]);
+    dn[rec_of[i]] = d;
+}
+
+// slot records: position p of the leaf order -> slot slot0[leaf] + (p - leaf.first)
+__global__ void k_lay_slots(const uint32_t* ids, uint32_t N, const uint32_t* P, const uint32_t* lfirst,
+                            const uint32_t* slot0, const uint2* lfun, const float4* rec_obj, const Aux* aux_obj,
+                            float4* prims, Aux* aux) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N) return;
+    const uint32_t l = P[p + 1] - 1u, k = p - lfirst[l], s = slot0[l] + k, o = ids[p];
+    const float4* src = rec_obj + 4 * (size_t)o;
+    float4* dst = prims + 4 * (size_t)s;
+    dst[0] = src[0];
+    dst[1] = src[1];
+    dst[2] = src[2];
+    dst[3] = src[3];
+    Aux a = aux_obj[o];
+    if (k == 0) a.flags |= lfun[l].x << 8;  // candidate count of the leaf starting here
+    aux[s] = a;
+}
+
+}  // namespace gb
+
+std::string device_layout(const HostScene& hs, DeviceTree& t, hipStream_t st, DevMem& dnodes, DevMem& prims,
+                          DevMem& aux, DeviceLayout& out, double* kernel_ms) {
+    using namespace gb;
+    const uint32_t N = hs.n_obj, n = t.n_nodes, nl = t.n_leaves;
+    const BuildNode* fin = t.nodes.as<BuildNode>();
+    const uint32_t* P = t.P.as<uint32_t>();
+    Buf recb, auxb, h, H, rec_of, lfirst, lfun, lscan, slot0, tmp;
+    GBCHK(recb.ensure(64 * (size_t)N));
+    GBCHK(auxb.ensure(sizeof(Aux) * (size_t)N));
+    GBCHK(hipMemcpyAsync(recb.p, hs.rec.data(), 64 * (size_t)N, hipMemcpyHostToDevice, st));
+    GBCHK(hipMemcpyAsync(auxb.p, hs.aux.data(), sizeof(Aux) * (size_t)N, hipMemcpyHostToDevice, st));
+    hipEvent_t ev0, ev1;
+    GBCHK(hipEventCreate(&ev0));
+    GBCHK(hipEventCreate(&ev1));
+    GBCHK(hipEventRecord(ev0, st));
+    GBCHK(h.ensure(4 * ((size_t)n + 1)));
+    GBCHK(H.ensure(4 * ((size_t)n + 1)));
+    GBCHK(rec_of.ensure(4 * (size_t)n));
+    GBCHK(lfirst.ensure(4 * (size_t)nl));
+    GBCHK(lfun.ensure(8 * ((size_t)nl + 1)));
+    GBCHK(lscan.ensure(8 * ((size_t)nl + 1)));
+    GBCHK(slot0.ensure(4 * (size_t)nl));
+    size_t tb1 = 0, tb2 = 0;
+    GBCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n + 1, st));
+    GBCHK(hipcub::DeviceScan::ExclusiveScan(nullptr, tb2, (uint2*)nullptr, (uint2*)nullptr, ParityCompose(),
+                                            make_uint2(0u, 0u), (int)nl + 1, st));
+    GBCHK(tmp.ensure(std::max(tb1, tb2)));
+    hipLaunchKernelGGL(k_lay_flags, dim3(blocks(n + 1, 256)), dim3(256), 0, st, fin, n, h.as<uint32_t>());
+    size_t tb = tmp.bytes;
+    GBCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, h.as<uint32_t>(), H.as<uint32_t>(), (int)n + 1, st));
+    hipLaunchKernelGGL(k_lay_recof, dim3(blocks(n, 256)), dim3(256), 0, st, fin, n, H.as<uint32_t>(),
+                       rec_of.as<int32_t>());
+    const uint2 ident = make_uint2(0u, 0u);
+    GBCHK(hipMemcpyAsync(lfun.as<uint2>() + nl, &ident, 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_lay_leaves, dim3(blocks(n, 256)), dim3(256), 0, st, fin, n, P, lfirst.as<uint32_t>(),
+                       lfun.as<uint2>());
+    tb = tmp.bytes;
+    GBCHK(hipcub::DeviceScan::ExclusiveScan(tmp.p, tb, lfun.as<uint2>(), lscan.as<uint2>(), ParityCompose(), ident,
+                                            (int)nl + 1, st));
+    hipLaunchKernelGGL(k_lay_slot0, dim3(blocks(nl, 256)), dim3(256), 0, st, lfun.as<uint2>(), lscan.as<uint2>(), nl,
+                       slot0.as<uint32_t>());
+    GBCHK(hipGetLastError());
+    uint32_t Htot = 0;
+    uint2 stot{0, 0};
+    BuildNode root{};
+    GBCHK(hipMemcpyAsync(&Htot, H.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, st));
+    GBCHK(hipMemcpyAsync(&stot, lscan.as<uint2>() + nl, 8, hipMemcpyDeviceToHost, st));
+    GBCHK(hipMemcpyAsync(&root, fin, sizeof(BuildNode), hipMemcpyDeviceToHost, st));
+    GBCHK(hipStreamSynchronize(st));
+    const bool root_interior = root.count == 0;
+    out.n_dnodes = root_interior ? 2u + 2u * Htot : 0u;
+    out.n_slots = stot.x;
+    GBCHK(dnodes.ensure(sizeof(DevNode) * (size_t)std::max(out.n_dnodes, 1u)));
+    GBCHK(prims.ensure(64 * (size_t)out.n_slots));
+    GBCHK(aux.ensure(sizeof(Aux) * (size_t)out.n_slots));
+    GBCHK(hipMemsetAsync(dnodes.p, 0, sizeof(DevNode) * (size_t)std::max(out.n_dnodes, 1u), st));
+    GBCHK(hipMemsetAsync(prims.p, 0, 64 * (size_t)out.n_slots, st));
+    GBCHK(hipMemsetAsync(aux.p, 0, sizeof(Aux) * (size_t)out.n_slots, st));
+    hipLaunchKernelGGL(k_lay_nodes, dim3(blocks(n, 256)), dim3(256), 0, st, fin, n, rec_of.as<int32_t>(), P,
+                       slot0.as<uint32_t>(), dnodes.as<DevNode>());
+    hipLaunchKernelGGL(k_lay_slots, dim3(blocks(N, 256)), dim3(256), 0, st, t.ids.as<uint32_t>(), N, P,
+                       lfirst.as<uint32_t>(), slot0.as<uint32_t>(), lfun.as<uint2>(), recb.as<float4>(),
+                       auxb.as<Aux>(), prims.as<float4>(), aux.as<Aux>());
+    GBCHK(hipGetLastError());
+    GBCHK(hipEventRecord(ev1, st));
+    // root reference (make_device_layout: child_ref(0, ...))
+    if (root_interior) {
+        out.root_ref = 0;
+        out.root_cnt = 0;
+    } else {
+        uint32_t s0 = 0;
+        GBCHK(hipMemcpyAsync(&s0, slot0.p, 4, hipMemcpyDeviceToHost, st));
+        GBCHK(hipStreamSynchronize(st));
+        const uint32_t ce = (uint32_t)root.count < LEAF_CNT_ESC ? (uint32_t)root.count : LEAF_CNT_ESC;
+        out.root_ref = (int32_t)(LEAF_BIT | (ce << 24) | s0);
+        out.root_cnt = root.count;
+    }
+    const float rb[6] = {root.mn.x, root.mn.y, root.mn.z, root.mx.x, root.mx.y, root.mx.z};
+    memcpy(out.root_box, rb, sizeof(rb));
     GBCHK(hipStreamSynchronize(st));
     float ms = 0.0f;
     GBCHK(hipEventElapsedTime(&ms, ev0, ev1));
     (void)hipEventDestroy(ev0);
     (void)hipEventDestroy(ev1);
     if (kernel_ms) *kernel_ms = ms;
-    hs.depth = hc.max_depth;
-    hs.max_leaf = hc.max_leaf;
-    (void)t0;
     return std::string();
 }
 

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "device.h"
+#include "device_build.h"
 
 using namespace khp;
 
@@ -980,25 +981,6 @@ __global__ void k_unpack(float* fb, const uint32_t* pix, uint32_t P, const float
         if (e_ != hipSuccess) return fail(KHP_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-struct DevMem {
-    void* p = nullptr;
-    size_t bytes = 0;
-    ~DevMem() {
-        if (p) (void)hipFree(p);
-    }
-    hipError_t ensure(size_t n) {
-        if (n <= bytes && p) return hipSuccess;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-        hipError_t e = hipMalloc(&p, n ? n : 16);
-        if (e == hipSuccess) bytes = n;
-        return e;
-    }
-    template <typename T>
-    T* as() const { return (T*)p; }
-};
-
 struct TimedLaunch {
     int kind;  // 0 extend, 1 shade, 2 shadow, 3 other
     int bounce;
@@ -1020,6 +1002,9 @@ struct khp_ctx {
     size_t cap = 0;
     DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
     // framebuffer + pixel list
+    DeviceTree tree;          // device-built BVH (preorder nodes, ids), kept for khp_read_bvh
+    bool tree_on_device = false;
+    uint32_t n_dnodes = 0, n_slots = 0;
     DevMem fb, pix, stage, stage_pix, snap;   // snap: per-bounce Counters snapshots (stats renders)
     int cur_bounce = -1;
     std::vector<float> dump;   // KHP_DUMP_BOUNCE: SoA o.xyz, d.xyz of one bounce's extension queue
@@ -1122,30 +1107,65 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     HIPCHK(hipSetDevice(c->device));
     auto t0 = std::chrono::steady_clock::now();
     const bool host_build = (c->flags & KHP_CTX_HOST_BUILD) || getenv("KHP_HOST_BUILD");
+    HostScene& hs = c->hs;
+    c->built = false;
     c->st.bvh_kernel_ms = 0.0;
-    if (host_build) {
-        unsigned nt = std::thread::hardware_concurrency();
-        build_bvh(c->hs, (int)std::max(1u, std::min(nt, 32u)));
-    } else {
-        std::string err = device_build_bvh(c->hs, c->stream, &c->st.bvh_kernel_ms);
-        if (!err.empty()) return fail(KHP_EDEVICE, err);
-    }
     c->st.bvh_on_device = host_build ? 0u : 1u;
-    auto tb = std::chrono::steady_clock::now();
-    make_device_layout(c->hs);
-    auto t1 = std::chrono::steady_clock::now();
+    double lay_kernel_ms = 0.0;
+    int32_t root_ref = 0, root_cnt = 0;
+    float root_box[6];
+    uint32_t n_dnodes = 0, n_slots = 0;
+    std::chrono::steady_clock::time_point tb, t1;
+    if (host_build) {
+        c->tree_on_device = false;
+        unsigned nt = std::thread::hardware_concurrency();
+        build_bvh(hs, (int)std::max(1u, std::min(nt, 32u)));
+        tb = std::chrono::steady_clock::now();
+        make_device_layout(hs);
+        t1 = std::chrono::steady_clock::now();
+        n_dnodes = (uint32_t)hs.dnodes.size();
+        n_slots = hs.n_slots;
+        if (n_slots >= MAX_SLOTS)
+            return fail(KHP_EUNSUPPORTED, "more than 2^24 primitive slots do not fit the packed leaf reference");
+        HIPCHK(upload(c->prims, hs.slot_rec.data(), hs.slot_rec.size(), c->stream));
+        HIPCHK(upload(c->aux, hs.slot_aux.data(), hs.slot_aux.size(), c->stream));
+        HIPCHK(upload(c->nodes, hs.dnodes.data(), hs.dnodes.size(), c->stream));
+        root_ref = hs.root_ref;
+        root_cnt = hs.root_cnt;
+        memcpy(root_box, hs.root_box, sizeof(root_box));
+        c->st.n_nodes = hs.nodes.size();
+        c->tree.release();
+    } else {
+        // the tree stays in HBM; hs.nodes / hs.ids are filled only on khp_read_bvh
+        hs.nodes.clear();
+        hs.ids.clear();
+        hs.dnodes.clear();
+        hs.slot_rec.clear();
+        hs.slot_aux.clear();
+        std::string err = device_build_bvh(hs, c->stream, c->tree, &c->st.bvh_kernel_ms);
+        if (!err.empty()) return fail(KHP_EDEVICE, err);
+        c->tree_on_device = true;
+        tb = std::chrono::steady_clock::now();
+        DeviceLayout lay;
+        err = device_layout(hs, c->tree, c->stream, c->nodes, c->prims, c->aux, lay, &lay_kernel_ms);
+        if (!err.empty()) return fail(KHP_EDEVICE, err);
+        t1 = std::chrono::steady_clock::now();
+        n_dnodes = lay.n_dnodes;
+        n_slots = lay.n_slots;
+        if (n_slots >= MAX_SLOTS)
+            return fail(KHP_EUNSUPPORTED, "more than 2^24 primitive slots do not fit the packed leaf reference");
+        root_ref = lay.root_ref;
+        root_cnt = lay.root_cnt;
+        memcpy(root_box, lay.root_box, sizeof(root_box));
+        c->st.n_nodes = c->tree.n_nodes;
+        c->st.bvh_kernel_ms += lay_kernel_ms;
+    }
     c->st.bvh_ms = std::chrono::duration<double, std::milli>(tb - t0).count();
     c->st.layout_ms = std::chrono::duration<double, std::milli>(t1 - tb).count();
     c->st.build_ms = c->st.flatten_ms + c->st.bvh_ms + c->st.layout_ms;
-    if (c->hs.depth + 1 > (uint32_t)STACK_MAX)
-        return fail(KHP_EUNSUPPORTED, "BVH deeper than the traversal stack (" + std::to_string(c->hs.depth) + ")");
-    if (c->hs.n_slots >= MAX_SLOTS)
-        return fail(KHP_EUNSUPPORTED, "more than 2^24 primitive slots do not fit the packed leaf reference");
-    HostScene& hs = c->hs;
-    HIPCHK(upload(c->prims, hs.slot_rec.data(), hs.slot_rec.size(), c->stream));
-    HIPCHK(upload(c->aux, hs.slot_aux.data(), hs.slot_aux.size(), c->stream));
+    if (hs.depth + 1 > (uint32_t)STACK_MAX)
+        return fail(KHP_EUNSUPPORTED, "BVH deeper than the traversal stack (" + std::to_string(hs.depth) + ")");
     HIPCHK(upload(c->trinrm, hs.tri_nrm.data(), hs.tri_nrm.size(), c->stream));
-    HIPCHK(upload(c->nodes, hs.dnodes.data(), hs.dnodes.size(), c->stream));
     HIPCHK(upload(c->mats, hs.mats.data(), hs.mats.size(), c->stream));
     HIPCHK(upload(c->lights, hs.lights.data(), hs.lights.size(), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1158,14 +1178,15 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     S.mats = c->mats.as<khp_material>();
     S.lights = c->lights.as<DevLight>();
     S.n_lights = (int32_t)hs.lights.size();
-    S.root_ref = hs.root_ref;
-    S.root_cnt = hs.root_cnt;
-    memcpy(S.root_box, hs.root_box, sizeof(S.root_box));
+    S.root_ref = root_ref;
+    S.root_cnt = root_cnt;
+    memcpy(S.root_box, root_box, sizeof(S.root_box));
+    c->n_dnodes = n_dnodes;
+    c->n_slots = n_slots;
     S.env = hs.env;
     S.cam = hs.cam;
     c->st.n_objects = hs.n_obj;
-    c->st.n_nodes = hs.nodes.size();
-    c->st.n_leaves = hs.nodes.size() - hs.dnodes.size();
+    c->st.n_leaves = (c->st.n_nodes + 1) / 2;
     c->st.bvh_depth = hs.depth;
     c->st.max_leaf_size = hs.max_leaf;
     c->st.device_bytes = c->prims.bytes + c->aux.bytes + c->trinrm.bytes + c->nodes.bytes + c->mats.bytes +
@@ -1614,7 +1635,12 @@ extern "C" khp_status khp_read_bvh(khp_ctx* c, uint32_t* n_nodes, uint32_t* dept
                                    int32_t* node_first, int32_t* node_count, int32_t* object_ids) {
     if (!c || !n_nodes) return fail(KHP_EINVAL, "ctx or n_nodes is null");
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
-    const HostScene& hs = c->hs;
+    HostScene& hs = c->hs;
+    if (c->tree_on_device && hs.nodes.size() != c->tree.n_nodes) {
+        HIPCHK(hipSetDevice(c->device));
+        std::string err = download_tree(c->tree, hs, c->stream);
+        if (!err.empty()) return fail(KHP_EDEVICE, err);
+    }
     *n_nodes = (uint32_t)hs.nodes.size();
     if (depth) *depth = hs.depth;
     for (size_t i = 0; i < hs.nodes.size(); ++i) {
@@ -1628,6 +1654,25 @@ extern "C" khp_status khp_read_bvh(khp_ctx* c, uint32_t* n_nodes, uint32_t* dept
     }
     if (object_ids)
         for (uint32_t i = 0; i < hs.n_obj; ++i) object_ids[i] = (int32_t)hs.ids[i];
+    return KHP_OK;
+}
+
+
+extern "C" khp_status khp_read_layout(khp_ctx* c, uint32_t* n_records, uint32_t* n_slots, void* node_records,
+                                      float* prim_records, uint32_t* prim_aux) {
+    if (!c || !n_records || !n_slots) return fail(KHP_EINVAL, "null argument");
+    if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
+    HIPCHK(hipSetDevice(c->device));
+    *n_records = c->n_dnodes;
+    *n_slots = c->n_slots;
+    if (node_records && c->n_dnodes)
+        HIPCHK(hipMemcpyAsync(node_records, c->nodes.p, sizeof(DevNode) * (size_t)c->n_dnodes, hipMemcpyDeviceToHost,
+                              c->stream));
+    if (prim_records && c->n_slots)
+        HIPCHK(hipMemcpyAsync(prim_records, c->prims.p, 64 * (size_t)c->n_slots, hipMemcpyDeviceToHost, c->stream));
+    if (prim_aux && c->n_slots)
+        HIPCHK(hipMemcpyAsync(prim_aux, c->aux.p, sizeof(Aux) * (size_t)c->n_slots, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return KHP_OK;
 }
 

@@ -83,9 +83,6 @@ struct HostScene {
 std::string flatten_scene(const khp_scene* s, HostScene& hs);
 void build_bvh(HostScene& hs, int n_threads);
 void make_device_layout(HostScene& hs);
-// The same tree built on the device (bvh_build.hip); kernel_ms: device time.
-// Declared with an opaque stream so scene.cpp stays host-only.
-std::string device_build_bvh(HostScene& hs, struct ihipStream_t* stream, double* kernel_ms);
 void light_init(DevLight& L, const khp_light& in);
 
 // Per-thread message behind khp_last_error(); every failing entry point sets it.

@@ -112,7 +112,8 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_comm_unique_id", "khp_comm_init", "khp_gather_framebuffer", "khp_bsdf_kind_from_name",
             "khp_bsdf_name", "khp_shader_kind_from_name", "khp_camera_setup", "khp_fibers_to_cones",
             "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus", "khp_host_build", "khp_debug_queue",
-            "khp_read_rgba8", "khp_tonemap_defaults", "khp_read_bvh"]
+            "khp_read_rgba8", "khp_tonemap_defaults", "khp_read_bvh",
+            "khp_read_layout"]
 
 _lib = None
 
@@ -146,6 +147,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
         "khp_read_rgba8": (c_int, [c_void_p, P(Tonemap), P(c_uint8)]),
         "khp_tonemap_defaults": (None, [P(Tonemap)]),
+        "khp_read_layout": (c_int, [c_void_p, P(c_uint32), P(c_uint32), c_void_p, P(c_float), P(c_uint32)]),
         "khp_read_bvh": (c_int, [c_void_p, P(c_uint32), P(c_uint32), P(c_float), P(c_int32), P(c_int32), P(c_int32)]),
         "khp_trace_closest": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_int32),
                                       P(c_float)]),

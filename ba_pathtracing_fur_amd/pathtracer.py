@@ -100,6 +100,20 @@ class HipContext:
                                                 ip(count), ip(ids)), "khp_read_bvh")
         return {"boxes": boxes, "first": first, "count": count, "ids": ids, "depth": dep.value}
 
+    def read_layout(self) -> dict:
+        """The traversal records in HBM (khp_read_layout): node records as (n, 16)
+        uint32 words, primitive records (n_slots, 16) float32, aux (n_slots, 4) uint32."""
+        nr, ns = ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(self.lib, self.lib.khp_read_layout(self.ptr, ctypes.byref(nr), ctypes.byref(ns), None, None, None),
+                "khp_read_layout")
+        nodes = np.zeros((nr.value, 16), np.uint32)
+        prims = np.zeros((ns.value, 16), np.float32)
+        aux = np.zeros((ns.value, 4), np.uint32)
+        N.check(self.lib, self.lib.khp_read_layout(self.ptr, ctypes.byref(nr), ctypes.byref(ns),
+                                                   nodes.ctypes.data_as(ctypes.c_void_p), N.fptr(prims),
+                                                   N.uptr(aux)), "khp_read_layout")
+        return {"nodes": nodes, "prims": prims, "aux": aux}
+
     def read_framebuffer(self, width, height) -> np.ndarray:
         out = np.zeros((height, width, 3), np.float32)
         N.check(self.lib, self.lib.khp_read_framebuffer(self.ptr, N.fptr(out)), "khp_read_framebuffer")

@@ -266,6 +266,13 @@ khp_status khp_gather_framebuffer(khp_ctx* ctx, const khp_render_params* p, int 
 khp_status khp_read_bvh(khp_ctx* ctx, uint32_t* n_nodes, uint32_t* depth, float* node_boxes, int32_t* node_first,
                         int32_t* node_count, int32_t* object_ids);
 
+/* The traversal records khp_build_accel left in HBM: n_records interior-node
+ * records (64 B each: L.min.xyz L.max.x | L.max.yz R.min.xy | R.min.z R.max.xyz
+ * | Lref Rref Lcnt Rcnt), n_slots primitive records (16 floats) and their aux
+ * words (base_d, material, object, flags).  Null arrays: sizes only. */
+khp_status khp_read_layout(khp_ctx* ctx, uint32_t* n_records, uint32_t* n_slots, void* node_records,
+                           float* prim_records, uint32_t* prim_aux);
+
 /* ---- host-only introspection (no device needed) ---------------------------- */
 /* Runs exactly the flatten + BVH build of khp_set_scene/khp_build_accel on the
  * host.  Call with null arrays first to get *n_nodes / *depth.  Nodes are in

@@ -25,15 +25,26 @@ def _same_tree(dev: dict, host: dict):
     assert np.array_equal(dev["boxes"].view(np.uint32), host["boxes"].view(np.uint32))
 
 
-def _device_tree(sd):
+def _device_tree(sd, layout=False):
     ctx = HipContext(0)
     ctx.set_scene(sd)
     ctx.build_accel()
     t = ctx.read_bvh()
     st = ctx.stats()
+    if layout:
+        t["layout"] = ctx.read_layout()
     ctx.close()
     assert st["bvh_on_device"] == 1
     return t, st
+
+
+def _host_layout(sd):
+    ctx = HipContext(0, host_build=True)
+    ctx.set_scene(sd)
+    ctx.build_accel()
+    lay = ctx.read_layout()
+    ctx.close()
+    return lay
 
 
 def _base(n_tris=0):
@@ -84,18 +95,27 @@ CASES = {
 @pytest.mark.parametrize("name", list(CASES))
 def test_device_build_equals_host_build(name):
     sd = CASES[name]()
-    dev, st = _device_tree(sd)
+    dev, st = _device_tree(sd, layout=True)
     host = N.host_build(sd)
     _same_tree(dev, host)
     assert st["n_nodes"] == len(host["boxes"])
+    # make_device_layout on the device: the same traversal records, bit for bit
+    hl, dl = _host_layout(sd), dev["layout"]
+    for k in ("nodes", "aux"):
+        assert np.array_equal(dl[k], hl[k]), k
+    assert np.array_equal(dl["prims"].view(np.uint32), hl["prims"].view(np.uint32))
 
 
 def test_device_build_full_size():
     """The metric-row scene (1M strands, 9,000,002 objects)."""
     sd = S.config3(64, 36, n_strands=1_000_000)
-    dev, st = _device_tree(sd)
+    dev, st = _device_tree(sd, layout=True)
     host = N.host_build(sd)
     _same_tree(dev, host)
+    hl, dl = _host_layout(sd), dev["layout"]
+    for k in ("nodes", "aux"):
+        assert np.array_equal(dl[k], hl[k]), k
+    assert np.array_equal(dl["prims"].view(np.uint32), hl["prims"].view(np.uint32))
     print(f"device BVH build: {st['bvh_ms']:.1f} ms wall ({st['bvh_kernel_ms']:.1f} ms kernels), "
           f"layout {st['layout_ms']:.1f} ms, flatten {st['flatten_ms']:.1f} ms")
 
