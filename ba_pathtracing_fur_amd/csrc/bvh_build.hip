@@ -694,21 +694,20 @@ static uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b - 1) /
 
 // Builds the DFS-preorder tree of build_bvh() on the device from hs.centroid /
 // hs.bounds into t; sets hs.depth, hs.max_leaf.  Returns an error string.
-std::string device_build_bvh(HostScene& hs, hipStream_t st, DeviceTree& t, double* kernel_ms) {
+std::string device_build_bvh(HostScene& hs, const DeviceObjects& o, hipStream_t st, DeviceTree& t,
+                             double* kernel_ms) {
     using namespace gb;
-    const uint32_t N = hs.n_obj;
+    const uint32_t N = o.n_obj;
     if (N == 0) return "no objects";
     auto t0 = std::chrono::steady_clock::now();
-    Buf cen, bnd, rec, leafstart, part0;
-    GBCHK(cen.ensure(12 * (size_t)N));
-    GBCHK(bnd.ensure(24 * (size_t)N));
+    Buf rec, leafstart, part0;
+    const float* cen = o.centroid.as<float>();
+    const float* bnd = o.bounds.as<float>();
     GBCHK(rec.ensure(16 * (size_t)N));
     GBCHK(leafstart.ensure(4 * ((size_t)N + 1)));
     const uint32_t nb0 = blocks(N + 1, 256);
     GBCHK(part0.ensure(24 * (size_t)nb0));
-    GBCHK(hipMemcpyAsync(cen.p, hs.centroid.data(), 12 * (size_t)N, hipMemcpyHostToDevice, st));
-    GBCHK(hipMemcpyAsync(bnd.p, hs.bounds.data(), 24 * (size_t)N, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_init, dim3(nb0), dim3(256), 0, st, cen.as<float>(), N, rec.as<float4>(),
+    hipLaunchKernelGGL(k_init, dim3(nb0), dim3(256), 0, st, cen, N, rec.as<float4>(),
                        leafstart.as<uint32_t>(), part0.as<uint32_t>());
     GBCHK(hipGetLastError());
     hipEvent_t ev0, ev1;
@@ -837,7 +836,7 @@ std::string device_build_bvh(HostScene& hs, hipStream_t st, DeviceTree& t, doubl
     GBCHK(T.ensure(2 * (size_t)N * sizeof(BuildNode)));
     if (hc.n_sroot)
         hipLaunchKernelGGL(k_subtree, dim3(blocks(hc.n_sroot, 64)), dim3(64), 0, st, rec.as<float4>(),
-                           bnd.as<float>(), srb.as<SRoot>(), hc.n_sroot, T.as<BuildNode>(), leafstart.as<uint32_t>(),
+                           bnd, srb.as<SRoot>(), hc.n_sroot, T.as<BuildNode>(), leafstart.as<uint32_t>(),
                            ctr.as<Ctr>());
     GBCHK(hipGetLastError());
     // leaf starts -> P (exclusive), P[N] = leaves
@@ -859,7 +858,7 @@ std::string device_build_bvh(HostScene& hs, hipStream_t st, DeviceTree& t, doubl
                            hc.n_sroot, T.as<BuildNode>(), P, fin);
     if (hc.n_lleaf)
         hipLaunchKernelGGL(k_level_leaves, dim3(blocks(hc.n_lleaf, 256)), dim3(256), 0, st, llb.as<LLeaf>(),
-                           hc.n_lleaf, rec.as<float4>(), bnd.as<float>(), P, fin);
+                           hc.n_lleaf, rec.as<float4>(), bnd, P, fin);
     for (size_t l = levels.size(); l-- > 0;)
         hipLaunchKernelGGL(k_level_interior, dim3(blocks(levels[l].second, 256)), dim3(256), 0, st, gn.as<GNode>(),
                            levels[l].first, levels[l].second, P, fin);
@@ -995,17 +994,13 @@ __global__ void k_lay_slots(const uint32_t* ids, uint32_t N, const uint32_t* P, 
 
 }  // namespace gb
 
-std::string device_layout(const HostScene& hs, DeviceTree& t, hipStream_t st, DevMem& dnodes, DevMem& prims,
+std::string device_layout(const DeviceObjects& o, DeviceTree& t, hipStream_t st, DevMem& dnodes, DevMem& prims,
                           DevMem& aux, DeviceLayout& out, double* kernel_ms) {
     using namespace gb;
-    const uint32_t N = hs.n_obj, n = t.n_nodes, nl = t.n_leaves;
+    const uint32_t N = o.n_obj, n = t.n_nodes, nl = t.n_leaves;
     const BuildNode* fin = t.nodes.as<BuildNode>();
     const uint32_t* P = t.P.as<uint32_t>();
-    Buf recb, auxb, h, H, rec_of, lfirst, lfun, lscan, slot0, tmp;
-    GBCHK(recb.ensure(64 * (size_t)N));
-    GBCHK(auxb.ensure(sizeof(Aux) * (size_t)N));
-    GBCHK(hipMemcpyAsync(recb.p, hs.rec.data(), 64 * (size_t)N, hipMemcpyHostToDevice, st));
-    GBCHK(hipMemcpyAsync(auxb.p, hs.aux.data(), sizeof(Aux) * (size_t)N, hipMemcpyHostToDevice, st));
+    Buf h, H, rec_of, lfirst, lfun, lscan, slot0, tmp;
     hipEvent_t ev0, ev1;
     GBCHK(hipEventCreate(&ev0));
     GBCHK(hipEventCreate(&ev1));
@@ -1056,8 +1051,8 @@ std::string device_layout(const HostScene& hs, DeviceTree& t, hipStream_t st, De
     hipLaunchKernelGGL(k_lay_nodes, dim3(blocks(n, 256)), dim3(256), 0, st, fin, n, rec_of.as<int32_t>(), P,
                        slot0.as<uint32_t>(), dnodes.as<DevNode>());
     hipLaunchKernelGGL(k_lay_slots, dim3(blocks(N, 256)), dim3(256), 0, st, t.ids.as<uint32_t>(), N, P,
-                       lfirst.as<uint32_t>(), slot0.as<uint32_t>(), lfun.as<uint2>(), recb.as<float4>(),
-                       auxb.as<Aux>(), prims.as<float4>(), aux.as<Aux>());
+                       lfirst.as<uint32_t>(), slot0.as<uint32_t>(), lfun.as<uint2>(), o.rec.as<float4>(),
+                       o.aux.as<Aux>(), prims.as<float4>(), aux.as<Aux>());
     GBCHK(hipGetLastError());
     GBCHK(hipEventRecord(ev1, st));
     // root reference (make_device_layout: child_ref(0, ...))

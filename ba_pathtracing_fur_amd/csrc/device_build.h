@@ -38,6 +38,25 @@ struct DevMem {
     T* as() const { return (T*)p; }
 };
 
+// Per-object state of the flattened scene in HBM (object-id order): the same
+// arrays HostScene holds on the host path.
+struct DeviceObjects {
+    DevMem rec;       // float4[4 * n_obj]: the 64-B intersection record
+    DevMem aux;       // Aux[n_obj]
+    DevMem bounds;    // float[6 * n_obj]
+    DevMem centroid;  // float[3 * n_obj]
+    DevMem tri_nrm;   // float[9 * n_tris]
+    uint32_t n_obj = 0, n_tris = 0, n_cones = 0;
+    void release() {
+        rec.release();
+        aux.release();
+        bounds.release();
+        centroid.release();
+        tri_nrm.release();
+        n_obj = n_tris = n_cones = 0;
+    }
+};
+
 // The BVH as the device build leaves it in HBM.
 struct DeviceTree {
     DevMem nodes;  // BuildNode[n_nodes], DFS preorder (the host builder's layout)
@@ -58,13 +77,25 @@ struct DeviceLayout {
     float root_box[6] = {0, 0, 0, 0, 0, 0};
 };
 
-// BVH::addBaseDataStructure on the device from hs.centroid / hs.bounds: the
-// host builder's tree (build_bvh), node for node.  Sets hs.depth / hs.max_leaf.
-std::string device_build_bvh(HostScene& hs, hipStream_t st, DeviceTree& t, double* kernel_ms);
+// CPU::Scene::flattenNode per-object state on the device (flatten.hip).
+// device_ptrs: the scene's geometry arrays are device pointers (else host,
+// copied).  Errors starting "EINVAL:" are input errors.
+std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_materials, DeviceObjects& o,
+                           hipStream_t st, double* kernel_ms);
+
+// khp_gen_hairball + khp_fibers_to_cones on the device, into device arrays of
+// n * (verts - 1) float4 each.
+std::string device_gen_hairball(uint32_t n, uint32_t verts, const float center[3], float ball_r, float root_r,
+                                uint32_t seed, float* d_base_r0, float* d_apex_r1, hipStream_t st);
+
+// BVH::addBaseDataStructure on the device from o.centroid / o.bounds: the host
+// builder's tree (build_bvh), node for node.  Sets hs.depth / hs.max_leaf.
+std::string device_build_bvh(HostScene& hs, const DeviceObjects& o, hipStream_t st, DeviceTree& t,
+                             double* kernel_ms);
 
 // make_device_layout on the device: interior records in pair order, leaf slots,
-// and the slot-ordered primitive records gathered from hs.rec / hs.aux.
-std::string device_layout(const HostScene& hs, DeviceTree& t, hipStream_t st, DevMem& dnodes, DevMem& prims,
+// and the slot-ordered primitive records gathered from o.rec / o.aux.
+std::string device_layout(const DeviceObjects& o, DeviceTree& t, hipStream_t st, DevMem& dnodes, DevMem& prims,
                           DevMem& aux, DeviceLayout& out, double* kernel_ms);
 
 // Copy the device tree into hs.nodes / hs.ids (introspection).

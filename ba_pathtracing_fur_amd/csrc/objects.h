@@ -1,0 +1,155 @@
+// objects.h -- per-object scene preparation shared by the host flatten
+// (scene.cpp, g++) and the device flatten (flatten.hip, hipcc): one source, so
+// both produce the same bits (both built with -ffp-contract=off).
+//   Triangle::Triangle            Common/Triangle.cpp:3-129 (identity model matrix)
+//   Cylinder::Cylinder/computeBounds  Common/Cylinder.cpp:5-67, 306-336
+//   CPU_Scene::flattenNode fibers CPU_Scene.cpp:121-144
+//   Mesh::addFurToFaces recurrence Mesh.cpp:111-142 (seeded hairball stand-in)
+#pragma once
+
+#include <cfloat>
+
+#include "kmath.h"
+
+namespace khp {
+
+constexpr float OBJ_RAY_EPS = 1e-4f;          // KIRK::cRayEpsilon (Common/Ray.h:9)
+constexpr uint32_t OBJ_TRI_TAG = 0x7fc0deadu;  // == TRI_TAG (scene.h)
+
+KHD void obj_set_comp(v3& a, int i, float v) {
+    if (i == 0) a.x = v;
+    else if (i == 1) a.y = v;
+    else a.z = v;
+}
+
+// Triangle ctor: vertices reordered by the longest AABB axis, edges with the
+// zero-guard, smooth normals normalized.  rec: (A, tag) (ab, 0) (ac, 0) (0);
+// bounds: bmin.xyz bmax.xyz; cen: centroid; nrm: nA nB nC.
+KHD void tri_object(v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc, float* rec, float* bounds, float* cen, float* nrm) {
+    v3 bmin = vmin(vmin(a, b), c) - mk(OBJ_RAY_EPS, OBJ_RAY_EPS, OBJ_RAY_EPS);
+    v3 bmax = vmax(vmax(a, b), c) + mk(OBJ_RAY_EPS, OBJ_RAY_EPS, OBJ_RAY_EPS);
+    v3 diff = bmax - bmin;
+    int lA = 0;
+    float longest = diff.x;
+    if (diff.y > longest) { longest = diff.y; lA = 1; }
+    if (diff.z > longest) { longest = diff.z; lA = 2; }
+    v3 Na = normalize(na), Nb = normalize(nb), Nc = normalize(nc);
+    v3 A = a, B = b, C = c, nA = Na, nB = Nb, nC = Nc;
+    float ca = comp(a, lA), cb = comp(b, lA), cc = comp(c, lA);
+    // six orderings, later matches override earlier ones (ties)
+    if (ca <= cb && cb <= cc) { A = a; B = b; C = c; nA = Na; nB = Nb; nC = Nc; }
+    if (cb <= ca && ca <= cc) { A = b; B = a; C = c; nA = Nb; nB = Na; nC = Nc; }
+    if (ca <= cc && cc <= cb) { A = a; B = c; C = b; nA = Na; nB = Nc; nC = Nb; }
+    if (cc <= ca && ca <= cb) { A = c; B = a; C = b; nA = Nc; nB = Na; nC = Nb; }
+    if (cb <= cc && cc <= ca) { A = b; B = c; C = a; nA = Nb; nB = Nc; nC = Na; }
+    if (cc <= cb && cb <= ca) { A = c; B = b; C = a; nA = Nc; nB = Nb; nC = Na; }
+    v3 ab = B - A, ac = C - A, bc = C - B;
+    if (comp(ab, lA) == 0.0f) obj_set_comp(ab, lA, 0.0001f);
+    if (comp(ac, lA) == 0.0f) obj_set_comp(ac, lA, 0.0001f);
+    if (comp(bc, lA) == 0.0f) obj_set_comp(bc, lA, 0.0001f);
+    v3 ce = ((A + B) + C) / 3.0f;
+    rec[0] = A.x; rec[1] = A.y; rec[2] = A.z; rec[3] = f_from_bits(OBJ_TRI_TAG);
+    rec[4] = ab.x; rec[5] = ab.y; rec[6] = ab.z; rec[7] = 0.0f;
+    rec[8] = ac.x; rec[9] = ac.y; rec[10] = ac.z; rec[11] = 0.0f;
+    rec[12] = 0.0f; rec[13] = 0.0f; rec[14] = 0.0f; rec[15] = 0.0f;
+    bounds[0] = bmin.x; bounds[1] = bmin.y; bounds[2] = bmin.z;
+    bounds[3] = bmax.x; bounds[4] = bmax.y; bounds[5] = bmax.z;
+    cen[0] = ce.x; cen[1] = ce.y; cen[2] = ce.z;
+    nrm[0] = nA.x; nrm[1] = nA.y; nrm[2] = nA.z;
+    nrm[3] = nB.x; nrm[4] = nB.y; nrm[5] = nB.z;
+    nrm[6] = nC.x; nrm[7] = nC.y; nrm[8] = nC.z;
+}
+
+// Cylinder ctor: frame (u, v, w), slope, axial extent, AABB of the rotated
+// local box, centroid at 40 % of the axis.  rec: (base, r0) (u, slope)
+// (v, min_d) (w, max_d); returns base_d = dot(base, v).
+KHD float cone_object(v3 base, v3 apex, float r0, float r1, float* rec, float* bounds, float* cen) {
+    v3 v = apex - base;
+    float height = length(v);
+    v = normalize(v);
+    v3 tmp = mk(0.0f, 1.0f, 0.0f);
+    if (1.0f - fabsf(dot(tmp, v)) < OBJ_RAY_EPS) tmp = mk(0.0f, 0.0f, 1.0f);
+    v3 u = normalize(cross(v, tmp));
+    v3 w = normalize(cross(u, v));
+    u = normalize(u);
+    v = normalize(v);
+    w = normalize(w);
+    float slope = (r0 - r1) / height;
+    float base_d = dot(base, v);
+    float min_d = dot(v, base), max_d = dot(v, apex);
+    if (max_d < min_d) {
+        float t = min_d;
+        min_d = max_d;
+        max_d = t;
+    }
+    float radius = (r0 > r1) ? r0 + 1e-6f : r1 + 1e-6f;
+    v3 l0 = mk(-radius, 0.0f, -radius), l1 = mk(radius, height, radius);
+    v3 corners[8] = {mk(l0.x, l1.y, l1.z), mk(l0.x, l0.y, l1.z), mk(l1.x, l0.y, l1.z), mk(l1.x, l1.y, l1.z),
+                     mk(l1.x, l1.y, l0.z), mk(l1.x, l0.y, l0.z), mk(l0.x, l0.y, l0.z), mk(l0.x, l1.y, l0.z)};
+    v3 bmin = mk(FLT_MAX, FLT_MAX, FLT_MAX), bmax = mk(-FLT_MAX, -FLT_MAX, -FLT_MAX);
+    for (int i = 0; i < 8; ++i) {
+        v3 q = corners[i];
+        v3 P = mk((u.x * q.x + v.x * q.y) + w.x * q.z, (u.y * q.x + v.y * q.y) + w.y * q.z,
+                  (u.z * q.x + v.z * q.y) + w.z * q.z) + base;
+        if (P.x < bmin.x) bmin.x = P.x;
+        if (P.x > bmax.x) bmax.x = P.x;
+        if (P.y < bmin.y) bmin.y = P.y;
+        if (P.y > bmax.y) bmax.y = P.y;
+        if (P.z < bmin.z) bmin.z = P.z;
+        if (P.z > bmax.z) bmax.z = P.z;
+    }
+    v3 ce = base + (apex - base) * 0.4f;  // Cylinder.cpp:50
+    rec[0] = base.x; rec[1] = base.y; rec[2] = base.z; rec[3] = r0;
+    rec[4] = u.x; rec[5] = u.y; rec[6] = u.z; rec[7] = slope;
+    rec[8] = v.x; rec[9] = v.y; rec[10] = v.z; rec[11] = min_d;
+    rec[12] = w.x; rec[13] = w.y; rec[14] = w.z; rec[15] = max_d;
+    bounds[0] = bmin.x; bounds[1] = bmin.y; bounds[2] = bmin.z;
+    bounds[3] = bmax.x; bounds[4] = bmax.y; bounds[5] = bmax.z;
+    cen[0] = ce.x; cen[1] = ce.y; cen[2] = ce.z;
+    return base_d;
+}
+
+// One fiber segment c (vertices c, c+1) -> cone: base pulled back by 0.8 % of
+// the segment, base radius shrunk 5 % (c <= 3) or 10 %.
+KHD void fiber_segment(const float* P, const float* R, uint32_t c, float* ob, float* oa) {
+    v3 basepos = ld3(P + 3 * c), apexpos = ld3(P + 3 * (c + 1));
+    float br = R[c];
+    basepos = basepos - (apexpos - basepos) * 0.008f;
+    br -= (c > 3) ? 0.1f * br : 0.05f * br;
+    ob[0] = basepos.x; ob[1] = basepos.y; ob[2] = basepos.z; ob[3] = br;
+    oa[0] = apexpos.x; oa[1] = apexpos.y; oa[2] = apexpos.z; oa[3] = R[c + 1];
+}
+
+// Strand s of the seeded hairball: root uniform on the sphere, the
+// addFurToFaces recurrence in the root's tangent frame.  lnt[i] = (float)ln(i).
+KHD void hairball_strand(uint32_t s, uint32_t verts, v3 C, float ball_r, float root_r, uint32_t key0,
+                         const float* lnt, float* P, float* R) {
+    uint32_t key = lowbias32(key0 ^ s);
+    float u0 = draw_u01(key, 0), u1 = draw_u01(key, 1), u2 = draw_u01(key, 2);
+    float z = 1.0f - 2.0f * u0;
+    float rxy = sqrtf(gmax(0.0f, 1.0f - z * z));
+    float phi = 2.0f * PIF * u1;
+    v3 nrm = mk(rxy * k_cosf(phi), z, rxy * k_sinf(phi));
+    v3 ref = fabsf(nrm.y) < 0.9f ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+    v3 t0 = normalize(cross(nrm, ref));
+    v3 b0 = cross(nrm, t0);
+    float psi = 2.0f * PIF * u2;
+    v3 tan = t0 * k_cosf(psi) + b0 * k_sinf(psi);
+    v3 pos = C + nrm * ball_r;
+    pos = pos - nrm * 0.003f;  // "move start position down" (Mesh.cpp:115)
+    float radius = root_r;
+    P[0] = pos.x; P[1] = pos.y; P[2] = pos.z;
+    R[0] = radius;
+    uint32_t k = 1;
+    for (int i = (int)verts; i > 1; --i, ++k) {
+        float off_y = lnt[i] / 90.0f;
+        v3 point = (pos + nrm * off_y) + tan * 0.06f;
+        radius -= radius / ((float)i + 5.0f);
+        P[3 * k] = point.x; P[3 * k + 1] = point.y; P[3 * k + 2] = point.z;
+        R[k] = radius;
+        pos = point;
+    }
+    R[verts - 1] = 0.001f;  // Mesh.cpp:142
+}
+
+}  // namespace khp

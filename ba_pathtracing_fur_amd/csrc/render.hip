@@ -1002,6 +1002,8 @@ struct khp_ctx {
     size_t cap = 0;
     DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
     // framebuffer + pixel list
+    DeviceObjects obj;        // device-flattened objects (device path)
+    bool scene_on_host = false;
     DeviceTree tree;          // device-built BVH (preorder nodes, ids), kept for khp_read_bvh
     bool tree_on_device = false;
     uint32_t n_dnodes = 0, n_slots = 0;
@@ -1081,15 +1083,71 @@ extern "C" void khp_destroy(khp_ctx* c) {
     delete c;
 }
 
-extern "C" khp_status khp_set_scene(khp_ctx* c, const khp_scene* s) {
+static bool host_path(const khp_ctx* c) { return (c->flags & KHP_CTX_HOST_BUILD) || getenv("KHP_HOST_BUILD"); }
+
+static khp_status set_scene_impl(khp_ctx* c, const khp_scene* s, bool device_ptrs) {
     if (!c) return fail(KHP_EINVAL, "ctx is null");
     auto t0 = std::chrono::steady_clock::now();
-    std::string err = flatten_scene(s, c->hs);
-    if (!err.empty()) return fail(KHP_EINVAL, err);
-    c->scene_set = true;
+    const bool host = host_path(c);
+    if (host && device_ptrs) return fail(KHP_EUNSUPPORTED, "device scene arrays need the device build path");
+    c->scene_set = false;
     c->built = false;
+    std::string err = flatten_scene(s, c->hs, host);
+    if (!err.empty()) return fail(KHP_EINVAL, err);
+    c->st.flatten_kernel_ms = 0.0;
+    if (host) {
+        c->obj.release();
+    } else {
+        HIPCHK(hipSetDevice(c->device));
+        err = device_flatten(s, device_ptrs, s->n_materials, c->obj, c->stream, &c->st.flatten_kernel_ms);
+        if (!err.empty()) {
+            if (err.rfind("EINVAL:", 0) == 0) return fail(KHP_EINVAL, err.substr(7));
+            return fail(KHP_EDEVICE, err);
+        }
+    }
+    c->scene_set = true;
+    c->scene_on_host = host;
     c->st.flatten_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->st.build_ms = c->st.flatten_ms;
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_set_scene(khp_ctx* c, const khp_scene* s) { return set_scene_impl(c, s, false); }
+
+extern "C" khp_status khp_set_scene_device(khp_ctx* c, const khp_scene* s) { return set_scene_impl(c, s, true); }
+
+extern "C" khp_status khp_gen_hairball_device(khp_ctx* c, uint32_t n, uint32_t verts, const float center[3],
+                                              float ball_r, float root_r, uint32_t seed, float* d_base_r0,
+                                              float* d_apex_r1) {
+    if (!c || !center || (n && (!d_base_r0 || !d_apex_r1)) || verts < 2 || verts > 64)
+        return fail(KHP_EINVAL, "bad hairball arguments");
+    HIPCHK(hipSetDevice(c->device));
+    std::string err = device_gen_hairball(n, verts, center, ball_r, root_r, seed, d_base_r0, d_apex_r1, c->stream);
+    if (!err.empty()) return fail(KHP_EDEVICE, err);
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_device_alloc(khp_ctx* c, size_t bytes, void** out) {
+    if (!c || !out) return fail(KHP_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    *out = nullptr;
+    hipError_t e = hipMalloc(out, bytes ? bytes : 16);
+    if (e != hipSuccess) return fail(KHP_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_device_free(khp_ctx* c, void* p) {
+    if (!c) return fail(KHP_EINVAL, "ctx is null");
+    if (p) HIPCHK(hipFree(p));
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_device_copy(khp_ctx* c, void* dst, const void* src, size_t bytes, int to_device) {
+    if (!c || (bytes && (!dst || !src))) return fail(KHP_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    if (bytes)
+        HIPCHK(hipMemcpyAsync(dst, src, bytes, to_device ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return KHP_OK;
 }
 
@@ -1106,7 +1164,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     if (!c->scene_set) return fail(KHP_ENOTREADY, "khp_set_scene first");
     HIPCHK(hipSetDevice(c->device));
     auto t0 = std::chrono::steady_clock::now();
-    const bool host_build = (c->flags & KHP_CTX_HOST_BUILD) || getenv("KHP_HOST_BUILD");
+    const bool host_build = c->scene_on_host;  // the path khp_set_scene flattened on
     HostScene& hs = c->hs;
     c->built = false;
     c->st.bvh_kernel_ms = 0.0;
@@ -1142,12 +1200,12 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         hs.dnodes.clear();
         hs.slot_rec.clear();
         hs.slot_aux.clear();
-        std::string err = device_build_bvh(hs, c->stream, c->tree, &c->st.bvh_kernel_ms);
+        std::string err = device_build_bvh(hs, c->obj, c->stream, c->tree, &c->st.bvh_kernel_ms);
         if (!err.empty()) return fail(KHP_EDEVICE, err);
         c->tree_on_device = true;
         tb = std::chrono::steady_clock::now();
         DeviceLayout lay;
-        err = device_layout(hs, c->tree, c->stream, c->nodes, c->prims, c->aux, lay, &lay_kernel_ms);
+        err = device_layout(c->obj, c->tree, c->stream, c->nodes, c->prims, c->aux, lay, &lay_kernel_ms);
         if (!err.empty()) return fail(KHP_EDEVICE, err);
         t1 = std::chrono::steady_clock::now();
         n_dnodes = lay.n_dnodes;
@@ -1158,14 +1216,14 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         root_cnt = lay.root_cnt;
         memcpy(root_box, lay.root_box, sizeof(root_box));
         c->st.n_nodes = c->tree.n_nodes;
-        c->st.bvh_kernel_ms += lay_kernel_ms;
+        c->st.layout_kernel_ms = lay_kernel_ms;
     }
     c->st.bvh_ms = std::chrono::duration<double, std::milli>(tb - t0).count();
     c->st.layout_ms = std::chrono::duration<double, std::milli>(t1 - tb).count();
     c->st.build_ms = c->st.flatten_ms + c->st.bvh_ms + c->st.layout_ms;
     if (hs.depth + 1 > (uint32_t)STACK_MAX)
         return fail(KHP_EUNSUPPORTED, "BVH deeper than the traversal stack (" + std::to_string(hs.depth) + ")");
-    HIPCHK(upload(c->trinrm, hs.tri_nrm.data(), hs.tri_nrm.size(), c->stream));
+    if (host_build) HIPCHK(upload(c->trinrm, hs.tri_nrm.data(), hs.tri_nrm.size(), c->stream));
     HIPCHK(upload(c->mats, hs.mats.data(), hs.mats.size(), c->stream));
     HIPCHK(upload(c->lights, hs.lights.data(), hs.lights.size(), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1173,7 +1231,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     DevScene& S = c->S;
     S.prims = c->prims.as<float4>();
     S.aux = c->aux.as<Aux>();
-    S.tri_nrm = c->trinrm.as<float>();
+    S.tri_nrm = host_build ? c->trinrm.as<float>() : c->obj.tri_nrm.as<float>();
     S.nodes = c->nodes.as<DevNode>();
     S.mats = c->mats.as<khp_material>();
     S.lights = c->lights.as<DevLight>();

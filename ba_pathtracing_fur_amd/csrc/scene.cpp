@@ -4,6 +4,7 @@
 // Built with -ffp-contract=off so every float matches the device and the
 // documented semantics bit-for-bit.
 #include "scene.h"
+#include "objects.h"
 
 #include <string.h>
 
@@ -13,13 +14,7 @@
 
 namespace khp {
 
-static constexpr float RAY_EPS = 1e-4f;  // KIRK::cRayEpsilon (Common/Ray.h:9)
 
-static void set_comp(v3& a, int i, float v) {
-    if (i == 0) a.x = v;
-    else if (i == 1) a.y = v;
-    else a.z = v;
-}
 
 // Light ctors + QuadLight::calcParams + Light::transform(identity)
 // (Common/Light.h ctors, Light.cpp:112-118, 216-220, 263-276).
@@ -62,88 +57,21 @@ void light_init(DevLight& L, const khp_light& in) {
     L.direction[2] = d.z;
 }
 
-// Triangle::Triangle (Common/Triangle.cpp:3-129), identity model matrix.
+// Triangle::Triangle / Cylinder::Cylinder (objects.h, shared with the device flatten).
 static void tri_ctor(HostScene& hs, uint32_t id, v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc, uint32_t mat) {
-    v3 bmin = vmin(vmin(a, b), c) - mk(RAY_EPS, RAY_EPS, RAY_EPS);
-    v3 bmax = vmax(vmax(a, b), c) + mk(RAY_EPS, RAY_EPS, RAY_EPS);
-    v3 diff = bmax - bmin;
-    int lA = 0;
-    float longest = diff.x;
-    if (diff.y > longest) { longest = diff.y; lA = 1; }
-    if (diff.z > longest) { longest = diff.z; lA = 2; }
-    v3 Na = normalize(na), Nb = normalize(nb), Nc = normalize(nc);
-    v3 A = a, B = b, C = c, nA = Na, nB = Nb, nC = Nc;
-    float ca = comp(a, lA), cb = comp(b, lA), cc = comp(c, lA);
-    // six orderings, later matches override earlier ones (ties)
-    if (ca <= cb && cb <= cc) { A = a; B = b; C = c; nA = Na; nB = Nb; nC = Nc; }
-    if (cb <= ca && ca <= cc) { A = b; B = a; C = c; nA = Nb; nB = Na; nC = Nc; }
-    if (ca <= cc && cc <= cb) { A = a; B = c; C = b; nA = Na; nB = Nc; nC = Nb; }
-    if (cc <= ca && ca <= cb) { A = c; B = a; C = b; nA = Nc; nB = Na; nC = Nb; }
-    if (cb <= cc && cc <= ca) { A = b; B = c; C = a; nA = Nb; nB = Nc; nC = Na; }
-    if (cc <= cb && cb <= ca) { A = c; B = b; C = a; nA = Nc; nB = Nb; nC = Na; }
-    v3 ab = B - A, ac = C - A, bc = C - B;
-    if (comp(ab, lA) == 0.0f) set_comp(ab, lA, 0.0001f);
-    if (comp(ac, lA) == 0.0f) set_comp(ac, lA, 0.0001f);
-    if (comp(bc, lA) == 0.0f) set_comp(bc, lA, 0.0001f);
-    v3 cen = ((A + B) + C) / 3.0f;
-    float* r = &hs.rec[16 * (size_t)id];
-    float rr[16] = {A.x, A.y, A.z, f_from_bits(TRI_TAG), ab.x, ab.y, ab.z, 0.0f,
-                    ac.x, ac.y, ac.z, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    memcpy(r, rr, sizeof(rr));
-    float* bb = &hs.bounds[6 * (size_t)id];
-    bb[0] = bmin.x; bb[1] = bmin.y; bb[2] = bmin.z; bb[3] = bmax.x; bb[4] = bmax.y; bb[5] = bmax.z;
-    float* ce = &hs.centroid[3 * (size_t)id];
-    ce[0] = cen.x; ce[1] = cen.y; ce[2] = cen.z;
-    float* tn = &hs.tri_nrm[9 * (size_t)id];
-    float nn[9] = {nA.x, nA.y, nA.z, nB.x, nB.y, nB.z, nC.x, nC.y, nC.z};
-    memcpy(tn, nn, sizeof(nn));
+    tri_object(a, b, c, na, nb, nc, &hs.rec[16 * (size_t)id], &hs.bounds[6 * (size_t)id],
+               &hs.centroid[3 * (size_t)id], &hs.tri_nrm[9 * (size_t)id]);
     hs.aux[id] = Aux{0.0f, mat, id, 0u};  // flags: triangle
 }
 
-// Cylinder::Cylinder + computeBounds (Common/Cylinder.cpp:5-67, 306-336).
 static void cone_ctor(HostScene& hs, uint32_t id, uint32_t ci, v3 base, v3 apex, float r0, float r1, uint32_t mat) {
-    v3 v = apex - base;
-    float height = length(v);
-    v = normalize(v);
-    v3 tmp = mk(0.0f, 1.0f, 0.0f);
-    if (1.0f - fabsf(dot(tmp, v)) < RAY_EPS) tmp = mk(0.0f, 0.0f, 1.0f);
-    v3 u = normalize(cross(v, tmp));
-    v3 w = normalize(cross(u, v));
-    u = normalize(u);
-    v = normalize(v);
-    w = normalize(w);
-    float slope = (r0 - r1) / height;
-    float base_d = dot(base, v);
-    float min_d = dot(v, base), max_d = dot(v, apex);
-    if (max_d < min_d) std::swap(min_d, max_d);
-    float radius = (r0 > r1) ? r0 + 1e-6f : r1 + 1e-6f;
-    v3 l0 = mk(-radius, 0.0f, -radius), l1 = mk(radius, height, radius);
-    v3 corners[8] = {mk(l0.x, l1.y, l1.z), mk(l0.x, l0.y, l1.z), mk(l1.x, l0.y, l1.z), mk(l1.x, l1.y, l1.z),
-                     mk(l1.x, l1.y, l0.z), mk(l1.x, l0.y, l0.z), mk(l0.x, l0.y, l0.z), mk(l0.x, l1.y, l0.z)};
-    v3 bmin = mk(FLT_MAX, FLT_MAX, FLT_MAX), bmax = mk(-FLT_MAX, -FLT_MAX, -FLT_MAX);
-    for (int i = 0; i < 8; ++i) {
-        v3 q = corners[i];
-        v3 P = mk((u.x * q.x + v.x * q.y) + w.x * q.z, (u.y * q.x + v.y * q.y) + w.y * q.z,
-                  (u.z * q.x + v.z * q.y) + w.z * q.z) + base;
-        if (P.x < bmin.x) bmin.x = P.x;
-        if (P.x > bmax.x) bmax.x = P.x;
-        if (P.y < bmin.y) bmin.y = P.y;
-        if (P.y > bmax.y) bmax.y = P.y;
-        if (P.z < bmin.z) bmin.z = P.z;
-        if (P.z > bmax.z) bmax.z = P.z;
-    }
-    v3 cen = base + (apex - base) * 0.4f;  // Cylinder.cpp:50
-    float rr[16] = {base.x, base.y, base.z, r0, u.x, u.y, u.z, slope, v.x, v.y, v.z, min_d, w.x, w.y, w.z, max_d};
-    memcpy(&hs.rec[16 * (size_t)id], rr, sizeof(rr));
-    float* bb = &hs.bounds[6 * (size_t)id];
-    bb[0] = bmin.x; bb[1] = bmin.y; bb[2] = bmin.z; bb[3] = bmax.x; bb[4] = bmax.y; bb[5] = bmax.z;
-    float* ce = &hs.centroid[3 * (size_t)id];
-    ce[0] = cen.x; ce[1] = cen.y; ce[2] = cen.z;
-    hs.cone_height[ci] = height;
+    const float base_d = cone_object(base, apex, r0, r1, &hs.rec[16 * (size_t)id], &hs.bounds[6 * (size_t)id],
+                                     &hs.centroid[3 * (size_t)id]);
+    (void)ci;
     hs.aux[id] = Aux{base_d, mat, id, 1u};  // flags: cone
 }
 
-std::string flatten_scene(const khp_scene* s, HostScene& hs) {
+std::string flatten_scene(const khp_scene* s, HostScene& hs, bool objects) {
     if (!s) return "scene is null";
     uint64_t n = (uint64_t)s->n_tris + s->n_cones;
     if (n == 0) return "Your scene is empty!";  // BoundingBox.cpp:121-122
@@ -163,12 +91,19 @@ std::string flatten_scene(const khp_scene* s, HostScene& hs) {
     hs.n_tris = s->n_tris;
     hs.n_cones = s->n_cones;
     hs.n_obj = (uint32_t)n;
+    if (!objects) {  // the device flattens the objects (flatten.hip)
+        hs.mats.assign(s->materials, s->materials + s->n_materials);
+        hs.lights.resize(s->n_lights);
+        for (uint32_t i = 0; i < s->n_lights; ++i) light_init(hs.lights[i], s->lights[i]);
+        hs.env = s->env;
+        hs.cam = s->camera;
+        return std::string();
+    }
     hs.rec.resize(16 * n);
     hs.aux.resize(n);
     hs.bounds.resize(6 * n);
     hs.centroid.resize(3 * n);
     hs.tri_nrm.resize(9 * (size_t)s->n_tris);
-    hs.cone_height.resize(s->n_cones);
     for (uint32_t i = 0; i < s->n_tris; ++i)
         if (s->tri_mat[i] >= s->n_materials) return "triangle material index out of range";
     for (uint32_t i = 0; i < s->n_cones; ++i)
@@ -577,16 +512,7 @@ extern "C" khp_status khp_fibers_to_cones(uint32_t n_fibers, uint32_t verts, con
     for (uint32_t f = 0; f < n_fibers; ++f) {
         const float* P = positions + (size_t)f * verts * 3;
         const float* R = radii + (size_t)f * verts;
-        for (uint32_t c = 0; c + 1 < verts; ++c, ++k) {
-            v3 basepos = ld3(P + 3 * c), apexpos = ld3(P + 3 * (c + 1));
-            float br = R[c];
-            basepos = basepos - (apexpos - basepos) * 0.008f;
-            br -= (c > 3) ? 0.1f * br : 0.05f * br;
-            float* ob = out_base_r0 + 4 * k;
-            float* oa = out_apex_r1 + 4 * k;
-            ob[0] = basepos.x; ob[1] = basepos.y; ob[2] = basepos.z; ob[3] = br;
-            oa[0] = apexpos.x; oa[1] = apexpos.y; oa[2] = apexpos.z; oa[3] = R[c + 1];
-        }
+        for (uint32_t c = 0; c + 1 < verts; ++c, ++k) fiber_segment(P, R, c, out_base_r0 + 4 * k, out_apex_r1 + 4 * k);
     }
     return KHP_OK;
 }
@@ -603,38 +529,11 @@ extern "C" khp_status khp_gen_hairball(uint32_t n, uint32_t verts, const float c
         for (int i = 1; i <= 64; ++i) lnt[i] = (float)log((double)i);
         init = true;
     }
-    v3 C = ld3(center);
-    uint32_t key0 = lowbias32(seed ^ 0x48414952u);
-    for (uint32_t s = 0; s < n; ++s) {
-        uint32_t key = lowbias32(key0 ^ s);
-        float u0 = draw_u01(key, 0), u1 = draw_u01(key, 1), u2 = draw_u01(key, 2);
-        float z = 1.0f - 2.0f * u0;
-        float rxy = sqrtf(gmax(0.0f, 1.0f - z * z));
-        float phi = 2.0f * PIF * u1;
-        v3 nrm = mk(rxy * k_cosf(phi), z, rxy * k_sinf(phi));
-        v3 ref = fabsf(nrm.y) < 0.9f ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
-        v3 t0 = normalize(cross(nrm, ref));
-        v3 b0 = cross(nrm, t0);
-        float psi = 2.0f * PIF * u2;
-        v3 tan = t0 * k_cosf(psi) + b0 * k_sinf(psi);
-        float* P = positions + (size_t)s * verts * 3;
-        float* R = radii + (size_t)s * verts;
-        v3 pos = C + nrm * ball_r;
-        pos = pos - nrm * 0.003f;  // "move start position down" (Mesh.cpp:115)
-        float radius = root_r;
-        P[0] = pos.x; P[1] = pos.y; P[2] = pos.z;
-        R[0] = radius;
-        uint32_t k = 1;
-        for (int i = (int)verts; i > 1; --i, ++k) {
-            float off_y = lnt[i] / 90.0f;
-            v3 point = (pos + nrm * off_y) + tan * 0.06f;
-            radius -= radius / ((float)i + 5.0f);
-            P[3 * k] = point.x; P[3 * k + 1] = point.y; P[3 * k + 2] = point.z;
-            R[k] = radius;
-            pos = point;
-        }
-        R[verts - 1] = 0.001f;  // Mesh.cpp:142
-    }
+    const v3 C = ld3(center);
+    const uint32_t key0 = lowbias32(seed ^ 0x48414952u);
+    for (uint32_t s = 0; s < n; ++s)
+        hairball_strand(s, verts, C, ball_r, root_r, key0, lnt, positions + (size_t)s * verts * 3,
+                        radii + (size_t)s * verts);
     return KHP_OK;
 }
 

@@ -61,7 +61,6 @@ struct HostScene {
     std::vector<float> bounds;     // n_obj * 6
     std::vector<float> centroid;   // n_obj * 3
     std::vector<float> tri_nrm;    // n_tris * 9 (na, nb, nc after ctor reordering)
-    std::vector<float> cone_height;// n_cones
     std::vector<khp_material> mats;
     std::vector<DevLight> lights;
     khp_environment env{};
@@ -80,7 +79,9 @@ struct HostScene {
 };
 
 // Returns an error string (empty on success).
-std::string flatten_scene(const khp_scene* s, HostScene& hs);
+// objects=false: validate and keep materials/lights/env/camera only (the
+// device flattens the objects).
+std::string flatten_scene(const khp_scene* s, HostScene& hs, bool objects = true);
 void build_bvh(HostScene& hs, int n_threads);
 void make_device_layout(HostScene& hs);
 void light_init(DevLight& L, const khp_light& in);

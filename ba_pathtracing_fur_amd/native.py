@@ -82,7 +82,8 @@ class Stats(ctypes.Structure):
                 ("bounce_wave_iters", c_uint64 * 16), ("bounce_lanes_busy", c_uint64 * 16),
                 ("bounce_shadow_wave_iters", c_uint64 * 16), ("bounce_shadow_lanes_busy", c_uint64 * 16),
                 ("step_cycles", c_uint64 * 4), ("bvh_on_device", c_uint32), ("pad0", c_uint32),
-                ("flatten_ms", c_double), ("bvh_ms", c_double), ("bvh_kernel_ms", c_double), ("layout_ms", c_double)]
+                ("flatten_ms", c_double), ("bvh_ms", c_double), ("bvh_kernel_ms", c_double), ("layout_ms", c_double),
+                ("flatten_kernel_ms", c_double), ("layout_kernel_ms", c_double)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if not isinstance(getattr(self, k), (int, float)) else getattr(self, k))
@@ -113,7 +114,8 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_bsdf_name", "khp_shader_kind_from_name", "khp_camera_setup", "khp_fibers_to_cones",
             "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus", "khp_host_build", "khp_debug_queue",
             "khp_read_rgba8", "khp_tonemap_defaults", "khp_read_bvh",
-            "khp_read_layout"]
+            "khp_read_layout", "khp_set_scene_device", "khp_gen_hairball_device", "khp_device_alloc",
+            "khp_device_free", "khp_device_copy"]
 
 _lib = None
 
@@ -147,6 +149,12 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
         "khp_read_rgba8": (c_int, [c_void_p, P(Tonemap), P(c_uint8)]),
         "khp_tonemap_defaults": (None, [P(Tonemap)]),
+        "khp_set_scene_device": (c_int, [c_void_p, P(SceneDesc)]),
+        "khp_gen_hairball_device": (c_int, [c_void_p, c_uint32, c_uint32, P(c_float), c_float, c_float, c_uint32,
+                                            c_void_p, c_void_p]),
+        "khp_device_alloc": (c_int, [c_void_p, ctypes.c_size_t, P(c_void_p)]),
+        "khp_device_free": (c_int, [c_void_p, c_void_p]),
+        "khp_device_copy": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_int]),
         "khp_read_layout": (c_int, [c_void_p, P(c_uint32), P(c_uint32), c_void_p, P(c_float), P(c_uint32)]),
         "khp_read_bvh": (c_int, [c_void_p, P(c_uint32), P(c_uint32), P(c_float), P(c_int32), P(c_int32), P(c_int32)]),
         "khp_trace_closest": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_int32),

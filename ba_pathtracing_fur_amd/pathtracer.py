@@ -46,6 +46,42 @@ class ShaderFactory:
         return k
 
 
+class DeviceBuffer:
+    """A device allocation on a context's GPU (khp_device_alloc); freed with the object."""
+
+    def __init__(self, ctx: "HipContext", nbytes: int):
+        self.ctx, self.nbytes = ctx, int(nbytes)
+        p = ctypes.c_void_p()
+        N.check(ctx.lib, ctx.lib.khp_device_alloc(ctx.ptr, self.nbytes, ctypes.byref(p)), "khp_device_alloc")
+        self.ptr = p.value
+
+    @classmethod
+    def from_array(cls, ctx: "HipContext", a: np.ndarray) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        b = cls(ctx, a.nbytes)
+        N.check(ctx.lib, ctx.lib.khp_device_copy(ctx.ptr, b.ptr, a.ctypes.data_as(ctypes.c_void_p), a.nbytes, 1),
+                "khp_device_copy")
+        return b
+
+    def to_array(self, shape, dtype) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        assert out.nbytes <= self.nbytes
+        N.check(self.ctx.lib, self.ctx.lib.khp_device_copy(self.ctx.ptr, out.ctypes.data_as(ctypes.c_void_p), self.ptr,
+                                                           out.nbytes, 0), "khp_device_copy")
+        return out
+
+    def free(self):
+        if self.ptr and self.ctx.ptr:
+            self.ctx.lib.khp_device_free(self.ctx.ptr, self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class HipContext:
     """One khp_ctx: one GPU, one stream (one process per GPU)."""
 
@@ -71,6 +107,52 @@ class HipContext:
         d = scene.desc()
         N.check(self.lib, self.lib.khp_set_scene(self.ptr, ctypes.byref(d)), "khp_set_scene")
         self._scene = scene
+        self._n_objects = scene.n_objects
+
+    def hairball_device(self, n_strands: int, center, ball_radius: float, root_radius: float = 0.004,
+                        verts: int = 10, seed: int = 0x4B49524B):
+        """Seeded hairball cones generated in HBM (khp_gen_hairball_device): (base_r0, apex_r1, n_cones)."""
+        nc = n_strands * (verts - 1)
+        base, apex = DeviceBuffer(self, 16 * nc), DeviceBuffer(self, 16 * nc)
+        c = np.asarray(center, np.float32)
+        N.check(self.lib, self.lib.khp_gen_hairball_device(self.ptr, n_strands, verts, N.fptr(c), ball_radius,
+                                                           root_radius, seed, base.ptr, apex.ptr),
+                "khp_gen_hairball_device")
+        return base, apex, nc
+
+    def set_scene_device(self, scene: SceneData, cones=None):
+        """khp_set_scene_device: the scene's geometry copied to HBM first, or, with
+        cones=(base_r0, apex_r1, n, material) from hairball_device, those cones in
+        place of the scene's own (which must then be empty)."""
+        d = scene.desc()
+        keep = []
+
+        def dev(a):
+            b = DeviceBuffer.from_array(self, a)
+            keep.append(b)
+            return b.ptr
+
+        if len(scene.tri_v):
+            d.tri_v = ctypes.cast(dev(scene.tri_v), ctypes.POINTER(ctypes.c_float))
+            d.tri_n = ctypes.cast(dev(scene.tri_n), ctypes.POINTER(ctypes.c_float))
+            d.tri_mat = ctypes.cast(dev(scene.tri_mat), ctypes.POINTER(ctypes.c_uint32))
+        if cones is not None:
+            if len(scene.cone_base_r0):
+                raise ValueError("scene already has cones")
+            base, apex, nc, mat = cones
+            d.n_cones = nc
+            d.cone_base_r0 = ctypes.cast(base.ptr, ctypes.POINTER(ctypes.c_float))
+            d.cone_apex_r1 = ctypes.cast(apex.ptr, ctypes.POINTER(ctypes.c_float))
+            d.cone_mat = ctypes.cast(dev(np.full(nc, mat, np.uint32)), ctypes.POINTER(ctypes.c_uint32))
+        elif len(scene.cone_base_r0):
+            d.cone_base_r0 = ctypes.cast(dev(scene.cone_base_r0), ctypes.POINTER(ctypes.c_float))
+            d.cone_apex_r1 = ctypes.cast(dev(scene.cone_apex_r1), ctypes.POINTER(ctypes.c_float))
+            d.cone_mat = ctypes.cast(dev(scene.cone_mat), ctypes.POINTER(ctypes.c_uint32))
+        N.check(self.lib, self.lib.khp_set_scene_device(self.ptr, ctypes.byref(d)), "khp_set_scene_device")
+        for b in keep:
+            b.free()
+        self._scene = scene
+        self._n_objects = d.n_tris + d.n_cones
 
     def build_accel(self):
         N.check(self.lib, self.lib.khp_build_accel(self.ptr), "khp_build_accel")
@@ -94,7 +176,7 @@ class HipContext:
         boxes = np.empty((n, 6), np.float32)
         first = np.empty(n, np.int32)
         count = np.empty(n, np.int32)
-        ids = np.empty(self._scene.n_objects, np.int32)
+        ids = np.empty(getattr(self, "_n_objects", None) or self._scene.n_objects, np.int32)
         ip = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
         N.check(self.lib, self.lib.khp_read_bvh(self.ptr, ctypes.byref(nn), ctypes.byref(dep), N.fptr(boxes), ip(first),
                                                 ip(count), ip(ids)), "khp_read_bvh")

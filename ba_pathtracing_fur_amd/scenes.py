@@ -312,6 +312,20 @@ def config3(width=1920, height=1080, n_strands=1_000_000, bsdf="MarschnerHairBSD
     return sd
 
 
+def config3_device(ctx, width=1920, height=1080, n_strands=1_000_000, bsdf="MarschnerHairBSDF") -> SceneData:
+    """config3 with the hairball generated and flattened on the GPU of `ctx`
+    (khp_gen_hairball_device + khp_set_scene_device).  The same
+    objects in the same order as config3, so the same tree and frames.  Returns
+    the host part (plane, materials, lights, camera); the cones live in HBM."""
+    sd = config3(width, height, 0, bsdf)
+    sd.name = f"plane_hairball_{n_strands}_device"
+    base, apex, nc = ctx.hairball_device(n_strands, (0.0, 1.0, 0.0), 1.0)
+    ctx.set_scene_device(sd, cones=(base, apex, nc, 1))
+    base.free()
+    apex.free()
+    return sd
+
+
 def config5(width=3840, height=2160, n_strands=1_000_000, torus_grid=500, glass_subdiv=5) -> SceneData:
     """Config 3 hairball + 500k-tri Lambert torus + glass icosphere (ior 1.52)."""
     sd = config3(width, height, n_strands)

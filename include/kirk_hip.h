@@ -180,10 +180,12 @@ typedef struct {
     uint64_t step_cycles[4];
     /* ABI 3: where khp_build_accel built the BVH and how long it took */
     uint32_t bvh_on_device, pad0;    /* 1: device build (default), 0: host   */
-    double flatten_ms;               /* khp_set_scene (host flatten)          */
+    double flatten_ms;               /* khp_set_scene (flatten, incl. copies) */
     double bvh_ms;                   /* BVH build wall time incl. transfers   */
     double bvh_kernel_ms;            /* device build: GPU time of its kernels  */
-    double layout_ms;                /* node pairing + leaf slots (host)      */
+    double layout_ms;                /* node pairing + leaf slots + slot records */
+    double flatten_kernel_ms;        /* device flatten: GPU time of its kernels */
+    double layout_kernel_ms;         /* device layout: GPU time of its kernels  */
 } khp_stats;
 #define KHP_MAX_BOUNCE_STATS 16
 
@@ -210,6 +212,25 @@ khp_status khp_build_accel(khp_ctx* ctx);
  * floats (host unless KHP_RENDER_OUT_DEVICE, ignored with NO_READBACK).
  * Pixels of tiles not owned by this rank are left untouched. */
 khp_status khp_render(khp_ctx* ctx, const khp_render_params* p, float* out_rgb);
+
+/* khp_set_scene with the geometry arrays (tri_v, tri_n, tri_mat, cone_*) in
+ * device memory of ctx's GPU (materials, lights, camera stay host structs).
+ * The objects are flattened on the device; the arrays are
+ * read during the call only.  Not with KHP_CTX_HOST_BUILD. */
+khp_status khp_set_scene_device(khp_ctx* ctx, const khp_scene* scene);
+
+/* khp_gen_hairball followed by khp_fibers_to_cones, on the device: writes
+ * n_strands * (verts - 1) cones (float4 base.xyz r0 / apex.xyz r1) into the
+ * device arrays d_base_r0 / d_apex_r1; bit-identical to the host pair. */
+khp_status khp_gen_hairball_device(khp_ctx* ctx, uint32_t n_strands, uint32_t verts, const float center[3],
+                                   float ball_radius, float root_radius, uint32_t seed, float* d_base_r0,
+                                   float* d_apex_r1);
+
+/* Device memory on ctx's GPU for the arrays above (plain hipMalloc / hipFree),
+ * and a synchronous copy (to_device 1: host -> device, 0: device -> host). */
+khp_status khp_device_alloc(khp_ctx* ctx, size_t bytes, void** out);
+khp_status khp_device_free(khp_ctx* ctx, void* p);
+khp_status khp_device_copy(khp_ctx* ctx, void* dst, const void* src, size_t bytes, int to_device);
 
 /* Copy the device framebuffer (running mean, W*H*3) to host. */
 khp_status khp_read_framebuffer(khp_ctx* ctx, float* out_rgb);
