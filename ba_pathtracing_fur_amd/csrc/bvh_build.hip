@@ -224,64 +224,107 @@ __device__ void spawn(uint32_t first, uint32_t count, const GBox& cb, uint32_t l
 
 // Per node: reduce the chunk bins, run the SAH sweep exactly as the host loop
 // (CPU_BVH.cpp:400-470), spawn the two children.
-__global__ __launch_bounds__(256) void k_pick(GNode* g, uint32_t b, const uint32_t* __restrict__ part, uint32_t gcap,
-                                              SRoot* sr, uint32_t scap, LLeaf* ll, uint32_t lcap, uint32_t* leafstart,
-                                              Ctr* ct) {
-    __shared__ uint32_t red[BW];
+// The SAH sweep of one axis over its 16 encoded bins (t: 16 x 7 words), in
+// the host loop's order and arithmetic (CPU_BVH.cpp:400-470, scene.cpp
+// Builder::partition): left prefix boxes, then planes 14 .. 0 with the right
+// suffix, strict <.  lbw: 15 x 7 words of scratch (LDS).
+struct AxisBest {
+    float best;
+    int plane;
+    uint32_t L;
+    GBox lcb, rcb;
+};
+__device__ __forceinline__ GBox bin_box(const uint32_t* t) {
+    return GBox{{fdec(t[1]), fdec(t[2]), fdec(t[3])}, {fdec(t[4]), fdec(t[5]), fdec(t[6])}};
+}
+__device__ AxisBest sweep_axis(const uint32_t* t, float* lbw) {
+    GBox acc = box_empty();
+    uint32_t cnt = 0;
+#pragma unroll 1
+    for (int p = 0; p < NP; ++p) {
+        GBox l = box_empty();
+        if (p > 0) grow(l, acc);
+        grow(l, bin_box(t + 7 * p));
+        acc = l;
+        cnt += t[7 * p];
+        float* o = lbw + 7 * p;
+        o[0] = __uint_as_float(cnt);
+        for (int a = 0; a < 3; ++a) {
+            o[1 + a] = acc.mn[a];
+            o[4 + a] = acc.mx[a];
+        }
+    }
+    AxisBest r{FLT_MAX, 0, 0u, box_empty(), box_empty()};
+    GBox rb_next = box_empty();
+    uint32_t rn_next = 0;
+#pragma unroll 1
+    for (int p = NP - 1; p >= 0; --p) {
+        GBox rb = box_empty();
+        grow(rb, bin_box(t + 7 * (p + 1)));
+        uint32_t rn = t[7 * (p + 1)];
+        if (p != NP - 1) {
+            grow(rb, rb_next);
+            rn += rn_next;
+        }
+        const float* o = lbw + 7 * p;
+        const GBox lb{{o[1], o[2], o[3]}, {o[4], o[5], o[6]}};
+        const uint32_t ln = __float_as_uint(o[0]);
+        const float cost = area(lb) * (float)ln + area(rb) * (float)rn;
+        if (cost < r.best) {
+            r.best = cost;
+            r.plane = p;
+            r.L = ln;
+            r.lcb = lb;
+            r.rcb = rb;
+        }
+        rb_next = rb;
+        rn_next = rn;
+    }
+    return r;
+}
+
+constexpr int PICK_GROUPS = 3;  // 3 x 336 threads reduce every 3rd chunk each
+
+__global__ __launch_bounds__(PICK_GROUPS * BW) void k_pick(GNode* g, uint32_t b, const uint32_t* __restrict__ part,
+                                                           uint32_t gcap, SRoot* sr, uint32_t scap, LLeaf* ll,
+                                                           uint32_t lcap, uint32_t* leafstart, Ctr* ct) {
+    __shared__ uint32_t red[PICK_GROUPS][BW];
     const uint32_t i = b + blockIdx.x;
     const uint32_t c0 = g[i].chunk0, nc = g[i].nchunk;
-    for (int w = threadIdx.x; w < BW; w += 256) {
+    {
+        const int w = (int)(threadIdx.x % BW), grp = (int)(threadIdx.x / BW);
         uint32_t v = bin_init(w);
-        for (uint32_t c = c0; c < c0 + nc; ++c) v = bin_comb(w, v, part[(size_t)c * BW + w]);
-        red[w] = v;
+        uint32_t c = c0 + grp;
+        for (; c + 3 * PICK_GROUPS < c0 + nc; c += 4 * PICK_GROUPS) {  // 4 independent loads in flight
+            const uint32_t a0 = part[(size_t)c * BW + w];
+            const uint32_t a1 = part[(size_t)(c + PICK_GROUPS) * BW + w];
+            const uint32_t a2 = part[(size_t)(c + 2 * PICK_GROUPS) * BW + w];
+            const uint32_t a3 = part[(size_t)(c + 3 * PICK_GROUPS) * BW + w];
+            v = bin_comb(w, bin_comb(w, v, a0), bin_comb(w, bin_comb(w, a1, a2), a3));
+        }
+        for (; c < c0 + nc; c += PICK_GROUPS) v = bin_comb(w, v, part[(size_t)c * BW + w]);
+        red[grp][w] = v;
     }
+    __syncthreads();
+    for (int w = threadIdx.x; w < BW; w += blockDim.x)
+        for (int q = 1; q < PICK_GROUPS; ++q) red[0][w] = bin_comb(w, red[0][w], red[q][w]);
     __syncthreads();
     if (threadIdx.x != 0) return;
     GNode nd = g[i];
+    __shared__ float lbw[NP * 7];
     float best = FLT_MAX;
     int best_axis = 0, best_plane = 0;
     uint32_t bestL = 0;
     GBox lcb = box_empty(), rcb = box_empty();
     for (int axis = 0; axis < 3; ++axis) {
-        GBox bb[NB];
-        uint32_t bn[NB];
-        for (int q = 0; q < NB; ++q) {
-            const uint32_t* t = &red[(axis * NB + q) * 7];
-            bn[q] = t[0];
-            bb[q] = GBox{{fdec(t[1]), fdec(t[2]), fdec(t[3])}, {fdec(t[4]), fdec(t[5]), fdec(t[6])}};
-        }
-        uint32_t ln[NP];
-        GBox lb[NP];
-        lb[0] = box_empty();
-        grow(lb[0], bb[0]);
-        ln[0] = bn[0];
-        for (int p = 1; p < NP; ++p) {
-            lb[p] = box_empty();
-            grow(lb[p], lb[p - 1]);
-            grow(lb[p], bb[p]);
-            ln[p] = ln[p - 1] + bn[p];
-        }
-        GBox rb_next = box_empty();
-        uint32_t rn_next = 0;
-        for (int p = NP - 1; p >= 0; --p) {
-            GBox rb = box_empty();
-            grow(rb, bb[p + 1]);
-            uint32_t rn = bn[p + 1];
-            if (p != NP - 1) {
-                grow(rb, rb_next);
-                rn += rn_next;
-            }
-            const float cost = area(lb[p]) * (float)ln[p] + area(rb) * (float)rn;
-            if (cost < best) {
-                best = cost;
-                best_axis = axis;
-                best_plane = p;
-                lcb = lb[p];
-                rcb = rb;
-                bestL = ln[p];
-            }
-            rb_next = rb;
-            rn_next = rn;
+        const AxisBest r = sweep_axis(&red[0][axis * NB * 7], lbw);
+        if (r.best < best) {
+            best = r.best;
+            best_axis = axis;
+            best_plane = r.plane;
+            bestL = r.L;
+            lcb = r.lcb;
+            rcb = r.rcb;
         }
     }
     nd.axis = best_axis;
@@ -409,178 +452,279 @@ struct Frame {
     int32_t side;
 };
 
+// Values every lane of the wave holds identically, made scalar for the compiler
+// so that the loops and branches on them stay wave-uniform (the subtree kernel
+// relies on the wave moving through its steps together).
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float uni(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+
+__device__ __forceinline__ float wave_min(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = smin(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = smax(v, __shfl_xor(v, o));
+    return v;
+}
+
+// One wave per subtree (persistent blocks pull subtrees from a counter): the
+// node range lives in LDS; per node the lanes reduce the box, fill the 3 x 16
+// bins with LDS atomics, three lanes sweep one axis each, and the Hoare pairs
+// of the partition are ranked with ballots and swapped in LDS.  The nodes come
+// out in the recursion's preorder (explicit stack, left child popped first).
 __global__ __launch_bounds__(64) void k_subtree(float4* rec, const float* __restrict__ bounds, SRoot* sr, uint32_t n,
-                                                BuildNode* T, uint32_t* leafstart, Ctr* ct) {
-    // per-thread bins in LDS: bb (16 x 7) + lb (15 x 7) words
-    __shared__ float lds[64][NB * 7 + NP * 7];
-    const uint32_t si = blockIdx.x * blockDim.x + threadIdx.x;
-    if (si >= n) return;
-    float* bbw = lds[threadIdx.x];
-    float* lbw = bbw + NB * 7;
-    SRoot root = sr[si];
-    BuildNode* out = T + 2 * (size_t)root.first;
-    Frame st[SUB_STACK];
-    int sp = 0;
-    st[sp].first = root.first;
-    st[sp].second = root.first + root.count - 1;
-    st[sp].depth = root.depth;
-    st[sp].parent = -1;
-    st[sp].side = 0;
-    for (int a = 0; a < 6; ++a) st[sp].cb[a] = root.cb[a];
-    ++sp;
-    int32_t local = 0;
-    uint32_t maxd = 0, maxl = 0;
-    while (sp > 0) {
-        const Frame f = st[--sp];
-        const int32_t ni = local++;
-        if (f.parent >= 0) {
-            if (f.side == 0) out[f.parent].left = ni;
-            else out[f.parent].right = ni;
+                                                uint32_t* next, BuildNode* T, uint32_t* leafstart, Ctr* ct,
+                                                Frame* fstack) {
+    __shared__ float4 srec[SMALL];
+    __shared__ float sb[6][SMALL];
+    __shared__ uint32_t bins[BW];
+    __shared__ uint32_t PL[SMALL / 2 + 1], PR[SMALL / 2 + 1];
+    __shared__ float s_lcb[1][6], s_rcb[1][6];
+    const uint32_t lane = threadIdx.x;
+    Frame* stk = fstack + (size_t)blockIdx.x * SUB_STACK;
+    // every lane runs the atomic (no branch), lane 0 adds the 1: its old value is
+    // the wave's ticket, made scalar so the loop below is wave-uniform
+    uint32_t si = uni(atomicAdd(next, lane == 0 ? 1u : 0u));
+    while (si < n) {
+        const SRoot root = sr[si];
+        const uint32_t base = uni(root.first), cnt = uni(root.count);
+        for (uint32_t i = lane; i < cnt; i += 64) {
+            const float4 e = rec[base + i];
+            srec[i] = e;
+            const float* bb = bounds + 6 * (size_t)__float_as_uint(e.w);
+            for (int q = 0; q < 6; ++q) sb[q][i] = bb[q];
         }
-        GBox bv = box_empty();
-        for (uint32_t id = f.first; id <= f.second; ++id) {
-            const float* bb = &bounds[6 * (size_t)__float_as_uint(rec[id].w)];
-            bv.mn[0] = smin(bv.mn[0], bb[0]); bv.mn[1] = smin(bv.mn[1], bb[1]); bv.mn[2] = smin(bv.mn[2], bb[2]);
-            bv.mx[0] = smax(bv.mx[0], bb[3]); bv.mx[1] = smax(bv.mx[1], bb[4]); bv.mx[2] = smax(bv.mx[2], bb[5]);
+        BuildNode* out = T + 2 * (size_t)base;
+        if (lane == 0) {
+            Frame f{};
+            for (int q = 0; q < 6; ++q) f.cb[q] = root.cb[q];
+            f.first = 0;
+            f.second = cnt - 1;
+            f.depth = root.depth;
+            f.parent = -1;
+            f.side = 0;
+            stk[0] = f;
         }
-        BuildNode node{};
-        node.mn = mk(bv.mn[0], bv.mn[1], bv.mn[2]);
-        node.mx = mk(bv.mx[0], bv.mx[1], bv.mx[2]);
-        maxd = max(maxd, f.depth);
-        const GBox cb = cb_of(f.cb);
-        if (f.second - f.first > 1u && worth(cb)) {
-            // BVHNode::partition (CPU_BVH.cpp:357-552), as scene.cpp Builder::partition
-            float best = FLT_MAX;
-            int best_axis = 0, best_plane = 0;
-            GBox lcb = box_empty(), rcb = box_empty();
-            float cbmins[3], ks[3];
-            for (int axis = 0; axis < 3; ++axis) {
-                const float cbmin = cb.mn[axis];
-                const float k = split_k(cb.mn[axis], cb.mx[axis]);
-                cbmins[axis] = cbmin;
-                ks[axis] = k;
-                for (int q = 0; q < NB; ++q) {
-                    float* t = bbw + 7 * q;
-                    t[0] = __uint_as_float(0u);
-                    t[1] = t[2] = t[3] = FLT_MAX;
-                    t[4] = t[5] = t[6] = -FLT_MAX;
-                }
-                for (uint32_t id = f.first; id <= f.second; ++id) {
-                    const float4 e = rec[id];
-                    const float cc = axis == 0 ? e.x : (axis == 1 ? e.y : e.z);
-                    const int bin = min(max((int)(k * (cc - cbmin)), 0), NB - 1);
-                    float* t = bbw + 7 * bin;
-                    t[1] = smin(t[1], e.x); t[2] = smin(t[2], e.y); t[3] = smin(t[3], e.z);
-                    t[4] = smax(t[4], e.x); t[5] = smax(t[5], e.y); t[6] = smax(t[6], e.z);
-                    t[0] = __uint_as_float(__float_as_uint(t[0]) + 1u);
-                }
-                // lb prefix
-                {
-                    GBox acc = box_empty();
-                    const float* t = bbw;
-                    GBox b0{{t[1], t[2], t[3]}, {t[4], t[5], t[6]}};
-                    grow(acc, b0);
-                    uint32_t cnt = __float_as_uint(t[0]);
-                    float* o = lbw;
-                    o[0] = __uint_as_float(cnt);
-                    for (int a = 0; a < 3; ++a) { o[1 + a] = acc.mn[a]; o[4 + a] = acc.mx[a]; }
-                    for (int p = 1; p < NP; ++p) {
-                        const float* tp = bbw + 7 * p;
-                        GBox lbp = box_empty();
-                        grow(lbp, acc);
-                        GBox bp{{tp[1], tp[2], tp[3]}, {tp[4], tp[5], tp[6]}};
-                        grow(lbp, bp);
-                        acc = lbp;
-                        cnt += __float_as_uint(tp[0]);
-                        float* op = lbw + 7 * p;
-                        op[0] = __uint_as_float(cnt);
-                        for (int a = 0; a < 3; ++a) { op[1 + a] = acc.mn[a]; op[4 + a] = acc.mx[a]; }
-                    }
-                }
-                GBox rb_next = box_empty();
-                uint32_t rn_next = 0;
-                for (int p = NP - 1; p >= 0; --p) {
-                    const float* tb = bbw + 7 * (p + 1);
-                    GBox rb = box_empty();
-                    GBox bq{{tb[1], tb[2], tb[3]}, {tb[4], tb[5], tb[6]}};
-                    grow(rb, bq);
-                    uint32_t rn = __float_as_uint(tb[0]);
-                    if (p != NP - 1) {
-                        grow(rb, rb_next);
-                        rn += rn_next;
-                    }
-                    const float* tl = lbw + 7 * p;
-                    GBox lbp{{tl[1], tl[2], tl[3]}, {tl[4], tl[5], tl[6]}};
-                    const float cost = area(lbp) * (float)__float_as_uint(tl[0]) + area(rb) * (float)rn;
-                    if (cost < best) {
-                        best = cost;
-                        best_axis = axis;
-                        best_plane = p;
-                        lcb = lbp;
-                        rcb = rb;
-                    }
-                    rb_next = rb;
-                    rn_next = rn;
-                }
-            }
-            const float cbmin = cbmins[best_axis], k = ks[best_axis];
-            auto bin_of = [&](uint32_t pos) {
-                const float4 e = rec[pos];
-                const float cc = best_axis == 0 ? e.x : (best_axis == 1 ? e.y : e.z);
-                return (int)(k * (cc - cbmin));
-            };
-            int left = (int)f.first, right = (int)f.second;
-            bool ls = false, rs = false;
-            while (left < right) {
-                if (!ls) {
-                    if (bin_of((uint32_t)left) > best_plane) ls = true;
-                    else ++left;
-                }
-                if (!rs) {
-                    if (bin_of((uint32_t)right) <= best_plane) rs = true;
-                    else --right;
-                }
-                if (ls && rs) {
-                    const float4 tmp = rec[left];
-                    rec[left] = rec[right];
-                    rec[right] = tmp;
-                    ls = rs = false;
-                    ++left;
-                    --right;
-                }
-            }
-            uint32_t lsec, rfirst;
-            if (left > right) { lsec = (uint32_t)right; rfirst = (uint32_t)left; }
-            else if (ls) { lsec = (uint32_t)(left - 1); rfirst = (uint32_t)left; }
-            else if (rs) { lsec = (uint32_t)right; rfirst = (uint32_t)(right + 1); }
-            else if (bin_of((uint32_t)left) > best_plane) { lsec = (uint32_t)(left - 1); rfirst = (uint32_t)left; }
-            else { lsec = (uint32_t)left; rfirst = (uint32_t)(left + 1); }
-            node.count = 0;
-            out[ni] = node;
-            if (sp + 2 > SUB_STACK || (int)lsec < (int)f.first || rfirst > f.second) {  // deeper than any subtree of SMALL objects can be
-                atomicOr(&ct->error, 16u);
+        int sp = 1;
+        int32_t local = 0;
+        uint32_t maxd = 0, maxl = 0;
+        bool failed = false;
+        while (sp > 0 && !failed) {
+            __syncthreads();
+            Frame f = stk[--sp];
+            for (int q = 0; q < 6; ++q) f.cb[q] = uni(f.cb[q]);
+            f.first = uni(f.first);
+            f.second = uni(f.second);
+            f.depth = uni(f.depth);
+            f.parent = uni(f.parent);
+            f.side = uni(f.side);
+            const int32_t ni = local++;
+            if (ni >= 2 * (int32_t)cnt) {  // a subtree of cnt objects has < 2 cnt nodes: never spin
+                if (lane == 0) atomicOr(&ct->error, 64u);
+                failed = true;
                 break;
             }
-            Frame r{};
-            cb_put(r.cb, rcb);
-            r.first = rfirst; r.second = f.second; r.depth = f.depth + 1; r.parent = ni; r.side = 1;
-            st[sp++] = r;
-            Frame l{};
-            cb_put(l.cb, lcb);
-            l.first = f.first; l.second = lsec; l.depth = f.depth + 1; l.parent = ni; l.side = 0;
-            st[sp++] = l;
-        } else {
-            node.first = (int32_t)f.first;
-            node.count = (int32_t)(f.second - f.first + 1);
-            node.left = node.right = -1;
-            out[ni] = node;
-            leafstart[f.first] = 1u;
-            maxl = max(maxl, f.second - f.first + 1);
+#ifdef KHP_BUILD_DEBUG
+            if (lane == 0)
+                printf("sub %u sp %d ni %d first %u second %u depth %u parent %d side %d cb %g %g %g %g %g %g\n", si, sp,
+                       ni, f.first, f.second, f.depth, f.parent, f.side, f.cb[0], f.cb[1], f.cb[2], f.cb[3], f.cb[4],
+                       f.cb[5]);
+#endif
+            if (lane == 0 && f.parent >= 0) {
+                if (f.side == 0) out[f.parent].left = ni;
+                else out[f.parent].right = ni;
+            }
+            float bmn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, bmx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+            for (uint32_t i = f.first + lane; i <= f.second; i += 64)
+                for (int a = 0; a < 3; ++a) {
+                    bmn[a] = smin(bmn[a], sb[a][i]);
+                    bmx[a] = smax(bmx[a], sb[3 + a][i]);
+                }
+            BuildNode node{};
+            node.mn = mk(wave_min(bmn[0]), wave_min(bmn[1]), wave_min(bmn[2]));
+            node.mx = mk(wave_max(bmx[0]), wave_max(bmx[1]), wave_max(bmx[2]));
+            maxd = max(maxd, f.depth);
+            const GBox cb = cb_of(f.cb);
+            const uint32_t c = f.second - f.first + 1;
+            if (c - 1u > 1u && worth(cb)) {
+                float k[3], cbmin[3];
+                for (int a = 0; a < 3; ++a) {
+                    cbmin[a] = cb.mn[a];
+                    k[a] = split_k(cb.mn[a], cb.mx[a]);
+                }
+                for (int w = lane; w < BW; w += 64) bins[w] = bin_init(w);
+                __syncthreads();
+                for (uint32_t i = f.first + lane; i <= f.second; i += 64) {
+                    const float4 e = srec[i];
+                    const float cc[3] = {e.x, e.y, e.z};
+                    const uint32_t ex = fenc(e.x), ey = fenc(e.y), ez = fenc(e.z);
+                    for (int a = 0; a < 3; ++a) {
+                        const int bin = min(max((int)(k[a] * (cc[a] - cbmin[a])), 0), NB - 1);
+                        uint32_t* t = &bins[(a * NB + bin) * 7];
+                        atomicAdd(&t[0], 1u);
+                        atomicMin(&t[1], ex);
+                        atomicMin(&t[2], ey);
+                        atomicMin(&t[3], ez);
+                        atomicMax(&t[4], ex);
+                        atomicMax(&t[5], ey);
+                        atomicMax(&t[6], ez);
+                    }
+                }
+                __syncthreads();
+                // SAH sweep on 48 lanes: lane = axis * 16 + bin.  Prefix (left) and
+                // suffix (right) unions by segmented shuffles, one (axis, plane)
+                // cost per lane, then the host loop's choice: the first strict
+                // minimum in the order axis 0..2, plane 14..0, below FLT_MAX.
+                const int sax = (int)(lane >> 4), sb16 = (int)(lane & 15);
+                GBox lb = box_empty(), rb = box_empty();
+                uint32_t ln = 0, rn = 0;
+                if (sax < 3) {
+                    const uint32_t* t = &bins[(sax * NB + sb16) * 7];
+                    lb = bin_box(t);
+                    rb = lb;
+                    ln = rn = t[0];
+                }
+                for (int d = 1; d < 16; d <<= 1) {
+                    GBox ol, orr;
+                    for (int q = 0; q < 3; ++q) {
+                        ol.mn[q] = __shfl_up(lb.mn[q], d, 16);
+                        ol.mx[q] = __shfl_up(lb.mx[q], d, 16);
+                        orr.mn[q] = __shfl_down(rb.mn[q], d, 16);
+                        orr.mx[q] = __shfl_down(rb.mx[q], d, 16);
+                    }
+                    const uint32_t oln = __shfl_up(ln, d, 16), orn = __shfl_down(rn, d, 16);
+                    if (sb16 >= d) {  // left prefix: bins 0..b (earlier bins first, as the host's grow chain)
+                        GBox m = box_empty();
+                        grow(m, ol);
+                        grow(m, lb);
+                        lb = m;
+                        ln += oln;
+                    }
+                    if (sb16 + d < 16) {  // right suffix: bins b..15
+                        GBox m = box_empty();
+                        grow(m, rb);
+                        grow(m, orr);
+                        rb = m;
+                        rn += orn;
+                    }
+                }
+                // plane p = b: left = bins 0..p, right = bins p+1..15
+                GBox rb1;
+                for (int q = 0; q < 3; ++q) {
+                    rb1.mn[q] = __shfl_down(rb.mn[q], 1, 16);
+                    rb1.mx[q] = __shfl_down(rb.mx[q], 1, 16);
+                }
+                const uint32_t rn1 = __shfl_down(rn, 1, 16);
+                float cost = area(lb) * (float)ln + area(rb1) * (float)rn1;
+                const bool valid = sax < 3 && sb16 < NP && cost < FLT_MAX;
+                uint32_t order = valid ? (uint32_t)(sax * NP + (NP - 1 - sb16)) : 0xffffffffu;
+                if (!valid) cost = FLT_MAX;
+                float bc = cost;
+                uint32_t bo = order;
+                for (int o = 32; o > 0; o >>= 1) {
+                    const float oc = __shfl_xor(bc, o);
+                    const uint32_t oo = __shfl_xor(bo, o);
+                    if (oc < bc || (oc == bc && oo < bo)) {
+                        bc = oc;
+                        bo = oo;
+                    }
+                }
+                bo = uni(bo);
+                const bool found = bo != 0xffffffffu;
+                const int ax = found ? (int)(bo / NP) : 0;
+                const int plane = found ? (NP - 1) - (int)(bo % NP) : 0;
+                const int win = ax * 16 + plane;
+                const uint32_t L = found ? uni((uint32_t)__shfl(ln, win)) : 0u;
+                if (lane == (uint32_t)win && found) {
+                    cb_put(s_lcb[0], lb);
+                    cb_put(s_rcb[0], rb1);
+                }
+                __syncthreads();
+                if (L == 0 || L >= c) {  // cannot happen for worth(cb) boxes; refuse rather than loop
+                    if (lane == 0) atomicOr(&ct->error, 32u);
+                    failed = true;
+                    break;
+                }
+                const uint32_t mid = f.first + L;
+#ifdef KHP_BUILD_DEBUG
+                if (lane == 0) printf("  split ax %d plane %d L %u cost %g\n", ax, plane, L, bc);
+#endif
+                uint32_t mL = 0, mR = 0;
+                for (uint32_t r0 = f.first; r0 <= f.second; r0 += 64) {
+                    const uint32_t i = r0 + lane;
+                    bool fl = false, fr = false;
+                    if (i <= f.second) {
+                        const float4 e = srec[i];
+                        const float cc = ax == 0 ? e.x : (ax == 1 ? e.y : e.z);
+                        const bool rs = (int)(k[ax] * (cc - cbmin[ax])) > plane;
+                        fl = i < mid && rs;
+                        fr = i >= mid && !rs;
+                    }
+                    const uint64_t bl = __ballot(fl), br = __ballot(fr);
+                    if (fl) PL[mL + lane_rank(bl)] = i;
+                    if (fr) PR[mR + lane_rank(br)] = i;
+                    mL += (uint32_t)__popcll(bl);
+                    mR += (uint32_t)__popcll(br);
+                }
+                __syncthreads();
+                // k-th misplaced of the left region <-> k-th misplaced of the right region from its end
+                for (uint32_t q = lane; q < mL; q += 64) {
+                    const uint32_t pa = PL[q], pb = PR[mR - 1u - q];
+                    const float4 ta = srec[pa];
+                    srec[pa] = srec[pb];
+                    srec[pb] = ta;
+                    for (int z = 0; z < 6; ++z) {
+                        const float tz = sb[z][pa];
+                        sb[z][pa] = sb[z][pb];
+                        sb[z][pb] = tz;
+                    }
+                }
+                if (lane == 0) {
+                    node.count = 0;
+                    out[ni] = node;
+                }
+                if (sp + 2 > SUB_STACK) {
+                    if (lane == 0) atomicOr(&ct->error, 16u);
+                    failed = true;
+                    break;
+                }
+                GBox lcb = box_empty(), rcb = box_empty();
+                if (found) {
+                    lcb = cb_of(s_lcb[0]);
+                    rcb = cb_of(s_rcb[0]);
+                }
+                if (lane == 0) {
+                    Frame r{};
+                    cb_put(r.cb, rcb);
+                    r.first = mid; r.second = f.second; r.depth = f.depth + 1; r.parent = ni; r.side = 1;
+                    stk[sp] = r;
+                    Frame l{};
+                    cb_put(l.cb, lcb);
+                    l.first = f.first; l.second = mid - 1; l.depth = f.depth + 1; l.parent = ni; l.side = 0;
+                    stk[sp + 1] = l;
+                }
+                sp += 2;
+            } else {
+                node.first = (int32_t)(base + f.first);
+                node.count = (int32_t)c;
+                node.left = node.right = -1;
+                if (lane == 0) {
+                    out[ni] = node;
+                    leafstart[base + f.first] = 1u;
+                }
+                maxl = max(maxl, c);
+            }
         }
+        __syncthreads();
+        for (uint32_t i = lane; i < cnt; i += 64) rec[base + i] = srec[i];
+        if (lane == 0) {
+            sr[si].n_local = (uint32_t)local;
+            atomicMax(&ct->max_depth, maxd);
+            atomicMax(&ct->max_leaf, maxl);
+        }
+        si = uni(atomicAdd(next, lane == 0 ? 1u : 0u));
     }
-    sr[si].n_local = (uint32_t)local;
-    atomicMax(&ct->max_depth, maxd);
-    atomicMax(&ct->max_leaf, maxl);
 }
 
 // ---- assembly into DFS preorder ---------------------------------------------
@@ -811,7 +955,7 @@ std::string device_build_bvh(HostScene& hs, const DeviceObjects& o, hipStream_t 
                            chunk_node.as<uint32_t>());
         hipLaunchKernelGGL(k_bin, dim3(nch), dim3(256), 0, st, rec.as<float4>(), gn.as<GNode>(),
                            chunk_node.as<uint32_t>(), part.as<uint32_t>());
-        hipLaunchKernelGGL(k_pick, dim3(n), dim3(256), 0, st, gn.as<GNode>(), lb, part.as<uint32_t>(), (uint32_t)gcap,
+        hipLaunchKernelGGL(k_pick, dim3(n), dim3(PICK_GROUPS * BW), 0, st, gn.as<GNode>(), lb, part.as<uint32_t>(), (uint32_t)gcap,
                            srb.as<SRoot>(), (uint32_t)scap, llb.as<LLeaf>(), (uint32_t)lcap,
                            leafstart.as<uint32_t>(), ctr.as<Ctr>());
         hipLaunchKernelGGL(k_classify, dim3(nch), dim3(256), 0, st, rec.as<float4>(), gn.as<GNode>(),
@@ -834,10 +978,19 @@ std::string device_build_bvh(HostScene& hs, const DeviceObjects& o, hipStream_t 
     // small subtrees
     Buf T;
     GBCHK(T.ensure(2 * (size_t)N * sizeof(BuildNode)));
-    if (hc.n_sroot)
-        hipLaunchKernelGGL(k_subtree, dim3(blocks(hc.n_sroot, 64)), dim3(64), 0, st, rec.as<float4>(),
-                           bnd, srb.as<SRoot>(), hc.n_sroot, T.as<BuildNode>(), leafstart.as<uint32_t>(),
-                           ctr.as<Ctr>());
+    Buf fst, nxt;
+    if (hc.n_sroot) {
+        int dev = 0, n_cu = 256;
+        GBCHK(hipGetDevice(&dev));
+        GBCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+        const uint32_t grid = std::min<uint32_t>(hc.n_sroot, (uint32_t)n_cu * 12u);
+        GBCHK(fst.ensure((size_t)grid * SUB_STACK * sizeof(Frame)));
+        GBCHK(nxt.ensure(4));
+        GBCHK(hipMemsetAsync(nxt.p, 0, 4, st));
+        hipLaunchKernelGGL(k_subtree, dim3(grid), dim3(64), 0, st, rec.as<float4>(), bnd, srb.as<SRoot>(), hc.n_sroot,
+                           nxt.as<uint32_t>(), T.as<BuildNode>(), leafstart.as<uint32_t>(), ctr.as<Ctr>(),
+                           fst.as<Frame>());
+    }
     GBCHK(hipGetLastError());
     // leaf starts -> P (exclusive), P[N] = leaves
     GBCHK(t.P.ensure(4 * ((size_t)N + 1)));
