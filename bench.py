@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-scene", action="store_true",
+                    help="generate + flatten + build on the host (the pre-(f)1/(f)2 path) instead of in HBM")
     return ap.parse_args()
 
 
@@ -125,18 +127,28 @@ def main():
     from ba_pathtracing_fur_amd import HipContext, scenes
 
     W, H, spp, depth = args.width, args.height, args.spp, args.depth
+    ctx = HipContext(device=local_rank, host_build=args.host_scene)
     t0 = time.time()
-    sd = scenes.config3(W, H, n_strands=args.strands)
-    gen_s = time.time() - t0
-    ctx = HipContext(device=local_rank)
-    t0 = time.time()
-    ctx.set_scene(sd)
+    if args.host_scene:
+        sd = scenes.config3(W, H, n_strands=args.strands)
+        gen_s = time.time() - t0
+        t0 = time.time()
+        ctx.set_scene(sd)
+    else:  # hairball generated and flattened in HBM
+        sd = scenes.config3_device(ctx, W, H, n_strands=args.strands)
+        gen_s = time.time() - t0
+        t0 = time.time()
     ctx.build_accel()
     build_s = time.time() - t0
     st0 = ctx.stats()
+    n_objects = st0["n_objects"]
+    setup = {"path": "host" if args.host_scene else "device", "gen_s": round(gen_s, 4),
+             "flatten_ms": round(st0["flatten_ms"], 2), "bvh_ms": round(st0["bvh_ms"], 2),
+             "bvh_kernel_ms": round(st0["bvh_kernel_ms"], 2), "layout_ms": round(st0["layout_ms"], 2),
+             "upload_ms": round(st0["upload_ms"], 2), "build_accel_s": round(build_s, 4)}
     if rank == 0:
-        log(f"scene: {sd.n_objects} objects, gen {gen_s:.1f}s, flatten+BVH+upload {build_s:.1f}s, "
-            f"depth {st0['bvh_depth']}, nodes {st0['n_nodes']}, HBM {st0['device_bytes'] / 1e9:.2f} GB")
+        log(f"scene: {n_objects} objects, gen+flatten {gen_s:.3f}s, BVH+layout {build_s:.3f}s "
+            f"({setup}), depth {st0['bvh_depth']}, nodes {st0['n_nodes']}, HBM {st0['device_bytes'] / 1e9:.2f} GB")
     frame = ShardedFrame(ctx, rank, world, dist, tile=args.tile)
 
     def step(stats=False):
@@ -182,12 +194,12 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: seeded hairball (khp_gen_hairball, seed 0x4B49524B), scene built in-process",
+        "data": "synthetic: seeded hairball (khp_gen_hairball[_device], seed 0x4B49524B), scene built in-process",
         "config": {
-            "workload": f"config3 scene at the metric row: {args.strands} strands ({sd.n_objects - 2} cone frusta) "
+            "workload": f"config3 scene at the metric row: {args.strands} strands ({n_objects - 2} cone frusta) "
                         f"on a 2-tri plane + 2x2 quad light, {W}x{H}, {spp} spp, depth {depth}",
             "width": W, "height": H, "spp": spp, "depth": depth, "strands": args.strands,
-            "objects": sd.n_objects, "parallelism": f"tile-sharded {args.tile}px tiles x{world}, RCCL gather",
+            "objects": n_objects, "parallelism": f"tile-sharded {args.tile}px tiles x{world}, RCCL gather",
         },
         "roofline": {
             "bound": "hbm",
@@ -209,7 +221,8 @@ def main():
             "device_ms": round(last["render_ms"], 3),
             "shadow_nodes_per_ray": round(cnt["shadow_node_visits"] / max(1, cnt["shadow_rays"]), 2),
             "stack_spills_per_ray": round(cnt["stack_spills"] / max(1, rays + cnt["shadow_rays"]), 4),
-            "build_s": round(build_s, 2),
+            "build_s": round(build_s, 3),
+            "setup": setup,
             "per_bounce": [
                 {"bounce": b, "rays": cnt["bounce_rays"][b],
                  "nodes_per_ray": round(cnt["bounce_nodes"][b] / max(1, cnt["bounce_rays"][b]), 2),
@@ -241,7 +254,9 @@ def main():
         out["output_stage"] = o
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(sd, args, args.cpu_seconds)
+            # the oracle reads host arrays: the same scene generated on the host
+            host_sd = sd if args.host_scene else scenes.config3(W, H, n_strands=args.strands)
+            out["cpu_baseline"] = cpu_baseline(host_sd, args, args.cpu_seconds)
         except Exception as e:  # reported, never silently replaced
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
