@@ -22,6 +22,7 @@ struct DevScene {
     const float4* __restrict__ prims;    // slot order, 4 x float4 per object
     const Aux* __restrict__ aux;         // slot order
     const float* __restrict__ tri_nrm;   // object-id order, 9 floats per triangle
+    const float* __restrict__ tri_frame; // object-id order, 9 floats per triangle: hair frame u v w
     const DevNode* __restrict__ nodes;   // interior nodes
     const khp_material* __restrict__ mats;
     const DevLight* __restrict__ lights;
@@ -412,7 +413,7 @@ __device__ __forceinline__ float normal_gauss_pdf(float x, float mean, float sd)
 struct ShadeCtx {
     const khp_material* m;
     v3 n;
-    v3 U, V, W;   // hair frame (Object::getU/V/W), cones only
+    v3 U, V, W;   // hair frame (Object::getU/V/W): the cone's, or the fiber's for fur triangles
 };
 
 // BSDF::evaluateLight dispatch (Bsdf.cpp:197-202, 310-318, 771-776; others 0)

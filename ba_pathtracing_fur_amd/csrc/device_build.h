@@ -46,6 +46,7 @@ struct DeviceObjects {
     DevMem bounds;    // float[6 * n_obj]
     DevMem centroid;  // float[3 * n_obj]
     DevMem tri_nrm;   // float[9 * n_tris]
+    DevMem tri_frame; // float[9 * n_tris] hair frame (zeros unless fiberToTriangles)
     uint32_t n_obj = 0, n_tris = 0, n_cones = 0;
     void release() {
         rec.release();
@@ -53,6 +54,7 @@ struct DeviceObjects {
         bounds.release();
         centroid.release();
         tri_nrm.release();
+        tri_frame.release();
         n_obj = n_tris = n_cones = 0;
     }
 };
@@ -87,6 +89,11 @@ std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_mate
 // n * (verts - 1) float4 each.
 std::string device_gen_hairball(uint32_t n, uint32_t verts, const float center[3], float ball_r, float root_r,
                                 uint32_t seed, float* d_base_r0, float* d_apex_r1, hipStream_t st);
+
+// khp_gen_hairball followed by khp_fibers_to_triangles, on the device.
+std::string device_gen_hairball_tris(uint32_t n, uint32_t verts, const float center[3], float ball_r, float root_r,
+                                     uint32_t seed, uint32_t res, float* d_v, float* d_n, float* d_frame,
+                                     hipStream_t st);
 
 // BVH::addBaseDataStructure on the device from o.centroid / o.bounds: the host
 // builder's tree (build_bvh), node for node.  Sets hs.depth / hs.max_leaf.

@@ -75,6 +75,20 @@ __global__ void k_gen_hairball(uint32_t n, uint32_t verts, float cx, float cy, f
     }
 }
 
+// one triangle per thread: strand s = t / (segs * per_seg) regenerated per
+// thread (cheap next to the tube math), then fiber_tube_triangle
+__global__ void k_gen_hairball_tris(uint32_t n, uint32_t verts, float cx, float cy, float cz, float ball_r,
+                                    float root_r, uint32_t key0, LnTable lnt, uint32_t res, float* ov, float* on,
+                                    float* of) {
+    const uint32_t per_seg = 2 * res * res, per_strand = (verts - 1) * per_seg;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)n * per_strand) return;
+    const uint32_t s = (uint32_t)(t / per_strand), r = (uint32_t)(t % per_strand);
+    float P[3 * 64], R[64];
+    hairball_strand(s, verts, mk(cx, cy, cz), ball_r, root_r, key0, lnt.v, P, R);
+    fiber_tube_triangle(P, R, r / per_seg, res, r % per_seg, ov + 9 * t, on + 9 * t, of + 9 * t);
+}
+
 #define FLCHK(expr)                                                                  \
     do {                                                                             \
         hipError_t e_ = (expr);                                                      \
@@ -97,6 +111,12 @@ std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_mate
     FLCHK(o.bounds.ensure(24 * (size_t)N));
     FLCHK(o.centroid.ensure(12 * (size_t)N));
     FLCHK(o.tri_nrm.ensure(36 * (size_t)std::max(nt, 1u)));
+    FLCHK(o.tri_frame.ensure(36 * (size_t)std::max(nt, 1u)));
+    if (s->tri_frame && nt)
+        FLCHK(hipMemcpyAsync(o.tri_frame.p, s->tri_frame, 36 * (size_t)nt,
+                             device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    else
+        FLCHK(hipMemsetAsync(o.tri_frame.p, 0, 36 * (size_t)std::max(nt, 1u), st));
     DevMem tv, tn, tm, cb, ca, cm, err;
     const float *dtv = s->tri_v, *dtn = s->tri_n, *dcb = s->cone_base_r0, *dca = s->cone_apex_r1;
     const uint32_t *dtm = s->tri_mat, *dcm = s->cone_mat;
@@ -162,6 +182,22 @@ std::string device_gen_hairball(uint32_t n, uint32_t verts, const float center[3
     if (n)
         hipLaunchKernelGGL(k_gen_hairball, dim3(blocks(n, 128)), dim3(128), 0, st, n, verts, center[0], center[1],
                            center[2], ball_r, root_r, key0, t, (float4*)d_base_r0, (float4*)d_apex_r1);
+    FLCHK(hipGetLastError());
+    FLCHK(hipStreamSynchronize(st));
+    return std::string();
+}
+
+std::string device_gen_hairball_tris(uint32_t n, uint32_t verts, const float center[3], float ball_r, float root_r,
+                                     uint32_t seed, uint32_t res, float* d_v, float* d_n, float* d_frame,
+                                     hipStream_t st) {
+    using namespace fl;
+    LnTable t{};
+    for (int i = 1; i <= 64; ++i) t.v[i] = (float)std::log((double)i);
+    const uint32_t key0 = lowbias32(seed ^ 0x48414952u);
+    const size_t nt = (size_t)n * (verts - 1) * 2 * res * res;
+    if (nt)
+        hipLaunchKernelGGL(k_gen_hairball_tris, dim3((uint32_t)((nt + 127) / 128)), dim3(128), 0, st, n, verts,
+                           center[0], center[1], center[2], ball_r, root_r, key0, t, res, d_v, d_n, d_frame);
     FLCHK(hipGetLastError());
     FLCHK(hipStreamSynchronize(st));
     return std::string();

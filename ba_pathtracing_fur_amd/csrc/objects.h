@@ -120,6 +120,56 @@ KHD void fiber_segment(const float* P, const float* R, uint32_t c, float* ob, fl
     oa[0] = apexpos.x; oa[1] = apexpos.y; oa[2] = apexpos.z; oa[3] = R[c + 1];
 }
 
+// glm::mat4(1) * vec4(p, w), in glm's operation order ((m0 x + m1 y) + (m2 z + m3 w)):
+// exact, up to the sign of zero components (the identity mesh transform of
+// fiberToTriangles; the inverse-transpose for normals is the same matrix).
+KHD v3 ident_apply(v3 p, float w) {
+    const float x = (1.0f * p.x + 0.0f * p.y) + (0.0f * p.z + 0.0f * w);
+    const float y = (0.0f * p.x + 1.0f * p.y) + (0.0f * p.z + 0.0f * w);
+    const float z = (0.0f * p.x + 0.0f * p.y) + (1.0f * p.z + 0.0f * w);
+    return mk(x, y, z);
+}
+
+// fiberToTriangles (CPU_Scene.cpp:232-345) for segment c of one fiber: its
+// frame (no base pull-back / radius shrink on this path), then triangle t of
+// the 2 res^2 triangles: cells (i, j) row by row, two triangles per cell.
+// ov / on / of: 9 floats each (3 vertices, 3 normals, frame u v w).
+KHD void fiber_tube_triangle(const float* P, const float* R, uint32_t c, uint32_t res, uint32_t t, float* ov,
+                             float* on, float* of) {
+    const v3 base = ld3(P + 3 * c), apex = ld3(P + 3 * (c + 1));
+    v3 v = apex - base;
+    const float height = length(v);
+    v = normalize(v);
+    v3 tmp = mk(0.0f, 1.0f, 0.0f);
+    if (1.0f - fabsf(dot(tmp, v)) < OBJ_RAY_EPS) tmp = mk(0.0f, 0.0f, 1.0f);
+    const v3 u = normalize(cross(v, tmp));
+    const v3 w = normalize(cross(u, v));
+    const float slope = (R[c] - R[c + 1]) / height;
+    const uint32_t cell = t >> 1, j = cell / res, i = cell % res;
+    // tri1: (i, j+1) (i, j) (i+1, j); tri2: (i+1, j) (i+1, j+1) (i, j+1)
+    const uint32_t gi[2][3] = {{i, i, i + 1}, {i + 1, i + 1, i}};
+    const uint32_t gj[2][3] = {{j + 1, j, j}, {j, j + 1, j + 1}};
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t ii = gi[t & 1][k], jj = gj[t & 1][k];
+        const float uu = (float)ii / (float)res;
+        const float phi = 2.0f * PIF * uu;
+        const float vv = height * ((float)jj / (float)res);
+        const float radius = R[c] - slope * vv;
+        const v3 q = ((base + u * (radius * k_sinf(phi))) + v * vv) + w * (radius * k_cosf(phi));
+        const float tt = dot(q, v) - dot(base, v);
+        const v3 q1 = q - v * tt;
+        v3 n = normalize(q1 - base);
+        n = normalize(n + v * slope);
+        const v3 qv = ident_apply(q, 1.0f);
+        const v3 nv = normalize(ident_apply(n, 0.0f));
+        ov[3 * k] = qv.x; ov[3 * k + 1] = qv.y; ov[3 * k + 2] = qv.z;
+        on[3 * k] = nv.x; on[3 * k + 1] = nv.y; on[3 * k + 2] = nv.z;
+    }
+    of[0] = u.x; of[1] = u.y; of[2] = u.z;
+    of[3] = v.x; of[4] = v.y; of[5] = v.z;
+    of[6] = w.x; of[7] = w.y; of[8] = w.z;
+}
+
 // Strand s of the seeded hairball: root uniform on the sphere, the
 // addFurToFaces recurrence in the root's tangent frame.  lnt[i] = (float)ln(i).
 KHD void hairball_strand(uint32_t s, uint32_t verts, v3 C, float ball_r, float root_r, uint32_t key0,

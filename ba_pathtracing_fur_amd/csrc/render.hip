@@ -517,7 +517,10 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
                     float bu = Wv.hu[i], bv = Wv.hv[i];
                     float bx = (1.0f - bu) - bv;
                     nrm = normalize((ld3(tn) * bx + ld3(tn + 3) * bu) + ld3(tn + 6) * bv);
-                    s.U = s.V = s.W = mk(0, 0, 0);
+                    const float* tf = S.tri_frame + 9 * (size_t)ax.obj;  // fiberToTriangles frame (else 0)
+                    s.U = ld3(tf);
+                    s.V = ld3(tf + 3);
+                    s.W = ld3(tf + 6);
                 }
                 s.n = nrm;
                 const khp_material* m = s.m;
@@ -996,7 +999,7 @@ struct khp_ctx {
     int n_cu = 256;
     HostScene hs;
     bool scene_set = false, built = false;
-    DevMem prims, aux, trinrm, nodes, mats, lights;
+    DevMem prims, aux, trinrm, trifrm, nodes, mats, lights;
     DevScene S{};
     // wavefront
     size_t cap = 0;
@@ -1127,6 +1130,17 @@ extern "C" khp_status khp_gen_hairball_device(khp_ctx* c, uint32_t n, uint32_t v
     return KHP_OK;
 }
 
+extern "C" khp_status khp_gen_hairball_tris_device(khp_ctx* c, uint32_t n, uint32_t verts, const float center[3],
+                                                   float ball_r, float root_r, uint32_t seed, uint32_t res,
+                                                   float* d_v, float* d_n, float* d_frame) {
+    if (!c || !center || (n && (!d_v || !d_n || !d_frame)) || verts < 2 || verts > 64 || res == 0)
+        return fail(KHP_EINVAL, "bad hairball arguments");
+    HIPCHK(hipSetDevice(c->device));
+    std::string err = device_gen_hairball_tris(n, verts, center, ball_r, root_r, seed, res, d_v, d_n, d_frame, c->stream);
+    if (!err.empty()) return fail(KHP_EDEVICE, err);
+    return KHP_OK;
+}
+
 extern "C" khp_status khp_device_alloc(khp_ctx* c, size_t bytes, void** out) {
     if (!c || !out) return fail(KHP_EINVAL, "null argument");
     HIPCHK(hipSetDevice(c->device));
@@ -1223,7 +1237,10 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     c->st.build_ms = c->st.flatten_ms + c->st.bvh_ms + c->st.layout_ms;
     if (hs.depth + 1 > (uint32_t)STACK_MAX)
         return fail(KHP_EUNSUPPORTED, "BVH deeper than the traversal stack (" + std::to_string(hs.depth) + ")");
-    if (host_build) HIPCHK(upload(c->trinrm, hs.tri_nrm.data(), hs.tri_nrm.size(), c->stream));
+    if (host_build) {
+        HIPCHK(upload(c->trinrm, hs.tri_nrm.data(), hs.tri_nrm.size(), c->stream));
+        HIPCHK(upload(c->trifrm, hs.tri_frame.data(), hs.tri_frame.size(), c->stream));
+    }
     HIPCHK(upload(c->mats, hs.mats.data(), hs.mats.size(), c->stream));
     HIPCHK(upload(c->lights, hs.lights.data(), hs.lights.size(), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1232,6 +1249,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     S.prims = c->prims.as<float4>();
     S.aux = c->aux.as<Aux>();
     S.tri_nrm = host_build ? c->trinrm.as<float>() : c->obj.tri_nrm.as<float>();
+    S.tri_frame = host_build ? c->trifrm.as<float>() : c->obj.tri_frame.as<float>();
     S.nodes = c->nodes.as<DevNode>();
     S.mats = c->mats.as<khp_material>();
     S.lights = c->lights.as<DevLight>();
@@ -1247,7 +1265,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     c->st.n_leaves = (c->st.n_nodes + 1) / 2;
     c->st.bvh_depth = hs.depth;
     c->st.max_leaf_size = hs.max_leaf;
-    c->st.device_bytes = c->prims.bytes + c->aux.bytes + c->trinrm.bytes + c->nodes.bytes + c->mats.bytes +
+    c->st.device_bytes = c->prims.bytes + c->aux.bytes + c->trinrm.bytes + c->trifrm.bytes + c->nodes.bytes + c->mats.bytes +
                          c->lights.bytes;
     // persistent grid sizes
     int nb = 0;

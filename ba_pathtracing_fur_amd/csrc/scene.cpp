@@ -104,6 +104,8 @@ std::string flatten_scene(const khp_scene* s, HostScene& hs, bool objects) {
     hs.bounds.resize(6 * n);
     hs.centroid.resize(3 * n);
     hs.tri_nrm.resize(9 * (size_t)s->n_tris);
+    if (s->tri_frame) hs.tri_frame.assign(s->tri_frame, s->tri_frame + 9 * (size_t)s->n_tris);
+    else hs.tri_frame.assign(9 * (size_t)s->n_tris, 0.0f);
     for (uint32_t i = 0; i < s->n_tris; ++i)
         if (s->tri_mat[i] >= s->n_materials) return "triangle material index out of range";
     for (uint32_t i = 0; i < s->n_cones; ++i)
@@ -513,6 +515,22 @@ extern "C" khp_status khp_fibers_to_cones(uint32_t n_fibers, uint32_t verts, con
         const float* P = positions + (size_t)f * verts * 3;
         const float* R = radii + (size_t)f * verts;
         for (uint32_t c = 0; c + 1 < verts; ++c, ++k) fiber_segment(P, R, c, out_base_r0 + 4 * k, out_apex_r1 + 4 * k);
+    }
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_fibers_to_triangles(uint32_t n_fibers, uint32_t verts, const float* positions,
+                                              const float* radii, uint32_t res, float* out_v, float* out_n,
+                                              float* out_frame) {
+    if (verts < 2 || res == 0 || !positions || !radii || !out_v || !out_n || !out_frame) return KHP_EINVAL;
+    const uint32_t per_seg = 2 * res * res;
+    size_t k = 0;
+    for (uint32_t f = 0; f < n_fibers; ++f) {
+        const float* P = positions + (size_t)f * verts * 3;
+        const float* R = radii + (size_t)f * verts;
+        for (uint32_t c = 0; c + 1 < verts; ++c)
+            for (uint32_t t = 0; t < per_seg; ++t, ++k)
+                fiber_tube_triangle(P, R, c, res, t, out_v + 9 * k, out_n + 9 * k, out_frame + 9 * k);
     }
     return KHP_OK;
 }

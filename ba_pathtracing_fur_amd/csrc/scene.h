@@ -61,6 +61,7 @@ struct HostScene {
     std::vector<float> bounds;     // n_obj * 6
     std::vector<float> centroid;   // n_obj * 3
     std::vector<float> tri_nrm;    // n_tris * 9 (na, nb, nc after ctor reordering)
+    std::vector<float> tri_frame;  // n_tris * 9 (hair frame u, v, w; fiberToTriangles) or zeros
     std::vector<khp_material> mats;
     std::vector<DevLight> lights;
     khp_environment env{};

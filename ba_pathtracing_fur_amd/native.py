@@ -59,7 +59,7 @@ class SceneDesc(ctypes.Structure):
                 ("tri_mat", POINTER(c_uint32)), ("n_cones", c_uint32), ("cone_base_r0", POINTER(c_float)),
                 ("cone_apex_r1", POINTER(c_float)), ("cone_mat", POINTER(c_uint32)), ("n_materials", c_uint32),
                 ("materials", POINTER(Material)), ("n_lights", c_uint32), ("lights", POINTER(Light)),
-                ("env", Environment), ("camera", Camera)]
+                ("env", Environment), ("camera", Camera), ("tri_frame", POINTER(c_float))]
 
 
 class RenderParams(ctypes.Structure):
@@ -115,7 +115,7 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus", "khp_host_build", "khp_debug_queue",
             "khp_read_rgba8", "khp_tonemap_defaults", "khp_read_bvh",
             "khp_read_layout", "khp_set_scene_device", "khp_gen_hairball_device", "khp_device_alloc",
-            "khp_device_free", "khp_device_copy"]
+            "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device"]
 
 _lib = None
 
@@ -152,6 +152,10 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_set_scene_device": (c_int, [c_void_p, P(SceneDesc)]),
         "khp_gen_hairball_device": (c_int, [c_void_p, c_uint32, c_uint32, P(c_float), c_float, c_float, c_uint32,
                                             c_void_p, c_void_p]),
+        "khp_fibers_to_triangles": (c_int, [c_uint32, c_uint32, P(c_float), P(c_float), c_uint32, P(c_float),
+                                            P(c_float), P(c_float)]),
+        "khp_gen_hairball_tris_device": (c_int, [c_void_p, c_uint32, c_uint32, P(c_float), c_float, c_float,
+                                                 c_uint32, c_uint32, c_void_p, c_void_p, c_void_p]),
         "khp_device_alloc": (c_int, [c_void_p, ctypes.c_size_t, P(c_void_p)]),
         "khp_device_free": (c_int, [c_void_p, c_void_p]),
         "khp_device_copy": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_int]),

@@ -136,6 +136,7 @@ class HipContext:
             d.tri_v = ctypes.cast(dev(scene.tri_v), ctypes.POINTER(ctypes.c_float))
             d.tri_n = ctypes.cast(dev(scene.tri_n), ctypes.POINTER(ctypes.c_float))
             d.tri_mat = ctypes.cast(dev(scene.tri_mat), ctypes.POINTER(ctypes.c_uint32))
+            d.tri_frame = ctypes.cast(dev(scene.frames()), ctypes.POINTER(ctypes.c_float))
         if cones is not None:
             if len(scene.cone_base_r0):
                 raise ValueError("scene already has cones")

@@ -113,6 +113,8 @@ class SceneData:
     tri_v: np.ndarray = field(default_factory=lambda: np.zeros((0, 3, 3), np.float32))
     tri_n: np.ndarray = field(default_factory=lambda: np.zeros((0, 3, 3), np.float32))
     tri_mat: np.ndarray = field(default_factory=lambda: np.zeros((0,), np.uint32))
+    # hair frame (u, v, w) per triangle: set by fiberToTriangles fur, zero otherwise
+    tri_frame: np.ndarray = field(default_factory=lambda: np.zeros((0, 3, 3), np.float32))
     cone_base_r0: np.ndarray = field(default_factory=lambda: np.zeros((0, 4), np.float32))
     cone_apex_r1: np.ndarray = field(default_factory=lambda: np.zeros((0, 4), np.float32))
     cone_mat: np.ndarray = field(default_factory=lambda: np.zeros((0,), np.uint32))
@@ -128,19 +130,43 @@ class SceneData:
         self.materials.append(m)
         return len(self.materials) - 1
 
-    def add_triangles(self, v: np.ndarray, n: np.ndarray, mat: int):
+    def add_triangles(self, v: np.ndarray, n: np.ndarray, mat: int, frame: np.ndarray | None = None):
+        """Triangles (a, b, c) with vertex normals; frame: optional hair frame u, v, w per
+        triangle (Object::setU/V/W, fiberToTriangles fur), zero otherwise."""
         v = np.ascontiguousarray(v, np.float32).reshape(-1, 3, 3)
         n = np.ascontiguousarray(n, np.float32).reshape(-1, 3, 3)
+        old = self.frames()
         self.tri_v = np.concatenate([self.tri_v, v])
         self.tri_n = np.concatenate([self.tri_n, n])
         self.tri_mat = np.concatenate([self.tri_mat, np.full(len(v), mat, np.uint32)])
+        f = np.zeros((len(v), 3, 3), np.float32) if frame is None else np.asarray(frame, np.float32).reshape(-1, 3, 3)
+        self.tri_frame = np.concatenate([old, f])
 
-    def add_fibers(self, positions: np.ndarray, radii: np.ndarray, mat: int):
-        """Fur fibers -> cones exactly as CPU_Scene::flattenNode (khp_fibers_to_cones)."""
+    def frames(self) -> np.ndarray:
+        """tri_frame padded with zero frames to one per triangle."""
+        f = np.asarray(self.tri_frame, np.float32).reshape(-1, 3, 3)
+        if len(f) < len(self.tri_v):
+            f = np.concatenate([f, np.zeros((len(self.tri_v) - len(f), 3, 3), np.float32)])
+        return f
+
+    def add_fibers(self, positions: np.ndarray, radii: np.ndarray, mat: int, as_triangles: bool = False,
+                   resolution: int = 5):
+        """Fur fibers -> cones exactly as CPU_Scene::flattenNode (khp_fibers_to_cones), or, with
+        as_triangles (m_fiberAsCylinder = false), -> triangle tubes as fiberToTriangles
+        (khp_fibers_to_triangles, CPU_Scene.cpp:232-345)."""
         lib = N.load_library()
         positions = np.ascontiguousarray(positions, np.float32)
         radii = np.ascontiguousarray(radii, np.float32)
         nf, nv = radii.shape
+        if as_triangles:
+            nt = nf * (nv - 1) * 2 * resolution * resolution
+            v = np.empty((nt, 3, 3), np.float32)
+            n = np.empty((nt, 3, 3), np.float32)
+            fr = np.empty((nt, 3, 3), np.float32)
+            N.check(lib, lib.khp_fibers_to_triangles(nf, nv, N.fptr(positions), N.fptr(radii), resolution, N.fptr(v),
+                                                     N.fptr(n), N.fptr(fr)), "khp_fibers_to_triangles")
+            self.add_triangles(v, n, mat, frame=fr)
+            return
         base = np.empty((nf * (nv - 1), 4), np.float32)
         apex = np.empty((nf * (nv - 1), 4), np.float32)
         N.check(lib, lib.khp_fibers_to_cones(nf, nv, N.fptr(positions), N.fptr(radii), N.fptr(base), N.fptr(apex)),
@@ -162,6 +188,7 @@ class SceneData:
         self.tri_v = np.ascontiguousarray(self.tri_v, np.float32)
         self.tri_n = np.ascontiguousarray(self.tri_n, np.float32)
         self.tri_mat = np.ascontiguousarray(self.tri_mat, np.uint32)
+        self.tri_frame = np.ascontiguousarray(self.frames(), np.float32)
         self.cone_base_r0 = np.ascontiguousarray(self.cone_base_r0, np.float32)
         self.cone_apex_r1 = np.ascontiguousarray(self.cone_apex_r1, np.float32)
         self.cone_mat = np.ascontiguousarray(self.cone_mat, np.uint32)
@@ -172,6 +199,7 @@ class SceneData:
         d.tri_v = N.fptr(self.tri_v)
         d.tri_n = N.fptr(self.tri_n)
         d.tri_mat = N.uptr(self.tri_mat)
+        d.tri_frame = N.fptr(self.tri_frame)
         d.n_cones = len(self.cone_base_r0)
         d.cone_base_r0 = N.fptr(self.cone_base_r0)
         d.cone_apex_r1 = N.fptr(self.cone_apex_r1)
@@ -192,7 +220,7 @@ class SceneData:
     def to_arrays(self) -> dict:
         """Arrays for np.savez; materials/lights/camera are their khp_* struct bytes."""
         raw = lambda objs, T: np.frombuffer(bytes((T * len(objs))(*objs)), np.uint8).copy()
-        return {"tri_v": self.tri_v, "tri_n": self.tri_n, "tri_mat": self.tri_mat,
+        return {"tri_v": self.tri_v, "tri_n": self.tri_n, "tri_mat": self.tri_mat, "tri_frame": self.frames(),
                 "cone_base_r0": self.cone_base_r0, "cone_apex_r1": self.cone_apex_r1, "cone_mat": self.cone_mat,
                 "materials": raw(self.materials, N.Material), "lights": raw(self.lights, N.Light),
                 "env": np.float32([*self.env_color, *self.env_ambient]),
@@ -207,6 +235,8 @@ class SceneData:
         env = np.asarray(a["env"], np.float32)
         return cls(tri_v=np.asarray(a["tri_v"], np.float32), tri_n=np.asarray(a["tri_n"], np.float32),
                    tri_mat=np.asarray(a["tri_mat"], np.uint32),
+                   tri_frame=np.asarray(a["tri_frame"], np.float32) if "tri_frame" in getattr(a, "files", a)
+                   else np.zeros((0, 3, 3), np.float32),
                    cone_base_r0=np.asarray(a["cone_base_r0"], np.float32),
                    cone_apex_r1=np.asarray(a["cone_apex_r1"], np.float32),
                    cone_mat=np.asarray(a["cone_mat"], np.uint32),

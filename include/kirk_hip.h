@@ -23,13 +23,14 @@
 #ifndef KIRK_HIP_H
 #define KIRK_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 3
+#define KHP_ABI_VERSION 4
 
 typedef struct khp_ctx khp_ctx;
 
@@ -135,6 +136,11 @@ typedef struct {
     const khp_light* lights;
     khp_environment env;
     khp_camera camera;
+    /* ABI 4: optional [n_tris][3][3] hair frame u, v, w per triangle
+     * (Object::setU/V/W, set by CPU_Scene::fiberToTriangles, CPU_Scene.cpp:
+     * 232-345, for fur drawn as triangle tubes; read by the hair BSDFs).
+     * NULL: zero frames (KIRK leaves them uninitialised on plain triangles). */
+    const float* tri_frame;
 } khp_scene;
 
 #define KHP_RENDER_OUT_DEVICE   (1u << 0)  /* out_rgb is a device pointer        */
@@ -225,6 +231,12 @@ khp_status khp_set_scene_device(khp_ctx* ctx, const khp_scene* scene);
 khp_status khp_gen_hairball_device(khp_ctx* ctx, uint32_t n_strands, uint32_t verts, const float center[3],
                                    float ball_radius, float root_radius, uint32_t seed, float* d_base_r0,
                                    float* d_apex_r1);
+
+/* khp_gen_hairball followed by khp_fibers_to_triangles, on the device, into
+ * device arrays of n_strands*(verts-1)*2*res*res triangles (9 floats each). */
+khp_status khp_gen_hairball_tris_device(khp_ctx* ctx, uint32_t n_strands, uint32_t verts, const float center[3],
+                                        float ball_radius, float root_radius, uint32_t seed, uint32_t resolution,
+                                        float* d_v, float* d_n, float* d_frame);
 
 /* Device memory on ctx's GPU for the arrays above (plain hipMalloc / hipFree),
  * and a synchronous copy (to_device 1: host -> device, 0: device -> host). */
@@ -334,6 +346,15 @@ khp_status khp_camera_setup(const float position[3], const float look_at[3], con
 khp_status khp_fibers_to_cones(uint32_t n_fibers, uint32_t verts_per_fiber,
                                const float* positions, const float* radii,
                                float* out_base_r0, float* out_apex_r1);
+
+/* Fur fibers -> triangle tubes exactly as CPU_Scene::fiberToTriangles
+ * (CPU_Scene.cpp:232-345, identity mesh transform), the flatten path KIRK
+ * takes with m_fiberAsCylinder = false: per segment a (res+1)^2 vertex grid
+ * and 2 res^2 triangles, each carrying the segment's frame.
+ * out_v / out_n / out_frame: [n_fibers*(verts-1)*2*res*res][3][3]. */
+khp_status khp_fibers_to_triangles(uint32_t n_fibers, uint32_t verts_per_fiber, const float* positions,
+                                   const float* radii, uint32_t resolution, float* out_v, float* out_n,
+                                   float* out_frame);
 
 /* Seeded synthetic inputs (stand-ins for SceneGraph + Mesh::addFurToFaces,
  * Mesh.cpp:82-148).  Bit-reproducible on any host.

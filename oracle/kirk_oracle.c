@@ -1362,6 +1362,12 @@ int ko_create(ko_ctx** out, const khp_scene* s) {
         const float* n = s->tri_n + 9 * (size_t)i;
         tri_ctor(&c->obj[i], ld3(v), ld3(v + 3), ld3(v + 6), ld3(n), ld3(n + 3), ld3(n + 6));
         c->obj[i].mat = s->tri_mat[i];
+        /* Object::setU/V/W: the fiber's frame for fiberToTriangles fur (CPU_Scene.cpp:297-319),
+         * zero for plain triangles (uninitialised glm::vec3 in KIRK) */
+        const float* f = s->tri_frame ? s->tri_frame + 9 * (size_t)i : NULL;
+        c->obj[i].u = f ? ld3(f) : V(0.0f, 0.0f, 0.0f);
+        c->obj[i].v = f ? ld3(f + 3) : V(0.0f, 0.0f, 0.0f);
+        c->obj[i].w = f ? ld3(f + 6) : V(0.0f, 0.0f, 0.0f);
     }
     for (uint32_t i = 0; i < s->n_cones; ++i) {
         const float* b = s->cone_base_r0 + 4 * (size_t)i;

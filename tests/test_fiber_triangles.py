@@ -1,0 +1,107 @@
+"""Fibers as triangle tubes: CPU_Scene::fiberToTriangles (CPU_Scene.cpp:232-345),
+KIRK's flatten path with m_fiberAsCylinder = false (CPU_Scene.cpp:146-162).
+
+khp_fibers_to_triangles (objects.h, shared by host and device) is checked here
+against an independent float64 restatement of the reference loop (tolerance
+1e-5 absolute on unit-scale geometry, since kmath's sinf/cosf and float
+rounding differ from float64), and the oracle renders scenes built from it;
+tests/test_gpu_flatten.py checks the device generator and GPU frames bit for bit.
+"""
+import numpy as np
+import pytest
+
+import oracle_ffi
+from ba_pathtracing_fur_amd import native as N
+from ba_pathtracing_fur_amd import scenes as S
+
+
+def _ref_tubes(P, R, res):
+    """float64 fiberToTriangles for one fiber: (tris, 3, 3) vertices, normals, and frames."""
+    V, Nn, F = [], [], []
+    for c in range(len(P) - 1):
+        base, apex = P[c].astype(np.float64), P[c + 1].astype(np.float64)
+        v = apex - base
+        h = np.linalg.norm(v)
+        v = v / h
+        tmp = np.array([0.0, 1.0, 0.0])
+        if 1.0 - abs(tmp @ v) < 1e-4:
+            tmp = np.array([0.0, 0.0, 1.0])
+        u = np.cross(v, tmp)
+        u /= np.linalg.norm(u)
+        w = np.cross(u, v)
+        w /= np.linalg.norm(w)
+        slope = (R[c] - R[c + 1]) / h
+        grid_q, grid_n = {}, {}
+        for j in range(res + 1):
+            for i in range(res + 1):
+                phi = 2 * np.pi * i / res
+                vv = h * j / res
+                rad = R[c] - slope * vv
+                q = base + rad * np.sin(phi) * u + vv * v + rad * np.cos(phi) * w
+                t = q @ v - base @ v
+                n = q - t * v - base
+                n /= np.linalg.norm(n)
+                n = n + slope * v
+                n /= np.linalg.norm(n)
+                grid_q[i, j], grid_n[i, j] = q, n
+        for j in range(res):
+            for i in range(res):
+                for tri in ([(i, j + 1), (i, j), (i + 1, j)], [(i + 1, j), (i + 1, j + 1), (i, j + 1)]):
+                    V.append([grid_q[k] for k in tri])
+                    Nn.append([grid_n[k] for k in tri])
+                    F.append([u, v, w])
+    return np.array(V), np.array(Nn), np.array(F)
+
+
+def test_fibers_to_triangles_matches_float64():
+    pos, rad = S.hairball(3, (0.0, 0.5, 0.0), 0.25, verts=6, seed=11)
+    sd = S.SceneData()
+    sd.add_fibers(pos, rad, 0, as_triangles=True, resolution=5)
+    assert len(sd.tri_v) == 3 * 5 * 50 and len(sd.cone_base_r0) == 0
+    want_v, want_n, want_f = zip(*[_ref_tubes(pos[f], rad[f], 5) for f in range(3)])
+    np.testing.assert_allclose(sd.tri_v, np.concatenate(want_v), atol=1e-5)
+    # normals come from q - t v - base with |q| ~ 1 and r = 0.004: float cancellation
+    # leaves ~eps |q| / r ~ 5e-5 of error, in KIRK's float code as here
+    np.testing.assert_allclose(sd.tri_n, np.concatenate(want_n), atol=2e-4)
+    np.testing.assert_allclose(sd.frames(), np.concatenate(want_f), atol=1e-6)
+
+
+def test_straight_fiber_tube_known_answer():
+    """A vertical fiber of constant radius r: every vertex lies at distance r from
+    the axis, heights j/res of the segment, normals horizontal and unit."""
+    P = np.array([[[0.2, 0.0, -0.1], [0.2, 1.0, -0.1]]], np.float32)
+    R = np.array([[0.05, 0.05]], np.float32)
+    sd = S.SceneData()
+    sd.add_fibers(P, R, 0, as_triangles=True, resolution=4)
+    v = sd.tri_v.reshape(-1, 3).astype(np.float64)
+    r = np.hypot(v[:, 0] - 0.2, v[:, 2] + 0.1)
+    np.testing.assert_allclose(r, 0.05, atol=1e-6)
+    assert set(np.round(v[:, 1] * 4).astype(int)) == {0, 1, 2, 3, 4}
+    n = sd.tri_n.reshape(-1, 3)
+    np.testing.assert_allclose(np.linalg.norm(n, axis=1), 1.0, atol=1e-6)
+    np.testing.assert_allclose(n[:, 1], 0.0, atol=1e-6)
+    # the frame of a vertical fiber: v = +y, and (KIRK's tmp swap) u = v x z
+    f = sd.frames()[0]
+    np.testing.assert_allclose(f[1], [0, 1, 0], atol=1e-7)
+    np.testing.assert_allclose(f[0], np.cross([0, 1, 0], [0, 0, 1]), atol=1e-7)
+
+
+def test_triangle_fur_scene_renders_in_oracle():
+    """config2's box with the hairball drawn as triangle tubes (Marschner on triangles
+    uses the fiber frame): a finite image that differs from the cylinder version."""
+    sd = S.config2(24, 16, n_strands=60)
+    tri = S.config2(24, 16, n_strands=0)
+    pos, rad = S.hairball(60, (0.0, 0.5, 0.0), 0.25)
+    tri.add_fibers(pos, rad, len(tri.materials) - 1, as_triangles=True)
+    a = oracle_ffi.Oracle(sd).render(24, 16, 2, 4, threads=4)
+    b = oracle_ffi.Oracle(tri).render(24, 16, 2, 4, threads=4)
+    assert np.isfinite(b).mean() > 0.95
+    assert not np.array_equal(a, b)
+
+
+def test_scene_arrays_round_trip_frames():
+    tri = S.config2(8, 8, n_strands=0)
+    pos, rad = S.hairball(4, (0.0, 0.5, 0.0), 0.25)
+    tri.add_fibers(pos, rad, 0, as_triangles=True, resolution=2)
+    back = S.SceneData.from_arrays(tri.to_arrays())
+    assert np.array_equal(back.frames(), tri.frames())
