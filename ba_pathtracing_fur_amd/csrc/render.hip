@@ -39,6 +39,7 @@ struct alignas(128) Counters {
     uint32_t fetch_ext[KHP_MAX_SEG * 32];  // queue-segment claim cursors, one 128-B line each
     unsigned long long ext_rays, sh_rays;
     unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests, spills;
+    unsigned long long pruned, sh_pruned;  // entries popped only to fail the prune test
     unsigned long long iters, lanes_busy, sh_iters, sh_lanes_busy;  // wave iterations, lanes with work
     unsigned long long step_cycles[4];  // KHP_PROFILE_STEPS: resolve, fetch, compute, loop/refill (extend)
 };
@@ -380,9 +381,11 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
     }
     if (STATS) {
         unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
+        unsigned long long pr = wave_sum((unsigned long long)st.pruned);
         if (lane_id() == 0) {
             atomicAdd(&Wv.cnt->node_visits, a);
             atomicAdd(&Wv.cnt->prim_tests, b);
+            atomicAdd(&Wv.cnt->pruned, pr);
         }
         unsigned long long sp_ = wave_sum((unsigned long long)stk.spills);
         if (lane_id() == 0) {
@@ -748,9 +751,11 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
     }
     if (STATS) {
         unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
+        unsigned long long pr = wave_sum((unsigned long long)st.pruned);
         if (lane_id() == 0) {
             atomicAdd(&Wv.cnt->sh_node_visits, a);
             atomicAdd(&Wv.cnt->sh_prim_tests, b);
+            atomicAdd(&Wv.cnt->sh_pruned, pr);
         }
         unsigned long long sp_ = wave_sum((unsigned long long)stk.spills);
         if (lane_id() == 0) {
@@ -1569,6 +1574,8 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     c->st.shadow_node_visits = hc.sh_node_visits;
     c->st.shadow_prim_tests = hc.sh_prim_tests;
     c->st.stack_spills = hc.spills;
+    c->st.extend_pruned_pops = hc.pruned;
+    c->st.shadow_pruned_pops = hc.sh_pruned;
     for (int k = 0; k < 4; ++k) c->st.step_cycles[k] = hc.step_cycles[k];
     if (n_snap) {
         std::vector<Counters> sn(n_snap);

@@ -24,7 +24,7 @@ struct Hit {
 };
 
 struct TravStats {
-    uint32_t nodes, prims;
+    uint32_t nodes, prims, pruned;  // pruned: entries popped only to fail the prune test
 };
 
 struct TravRay {
@@ -514,6 +514,7 @@ __device__ __forceinline__ bool resolve(const DevScene& S, float tlimit, Stack& 
     if (lf.left > 0) return true;
     while (c.valid) {
         if (c.t1 < 0.0f || c.t0 > tlimit) {  // pruned at pop time
+            if (STATS) st.pruned++;
             cur_next(stk, c);
             continue;
         }
@@ -532,9 +533,16 @@ __device__ __forceinline__ const float4* work_record(const DevScene& S, const Cu
 }
 
 // Interior work on a fetched record (prune test already done in resolve).
+#ifndef KHP_PUSH_PRUNE
+#define KHP_PUSH_PRUNE 1   // apply the pop-time prune test to children before they are pushed
+#endif
+// PUSH_PRUNE: a child that would fail the prune test `t1 < 0 || t0 > tlimit`
+// when popped is dropped now.  tlimit only ever decreases (closest hit) or is
+// fixed (any hit), so such a child is certain to be pruned later; the live
+// entries, their order and every visit (the counts included) are unchanged.
 template <bool STATS, class Stack>
 __device__ __forceinline__ void interior_apply(const TravRay& tr, float4 a, float4 b, float4 cc, int4 rf, Stack& stk,
-                                               Cur& c, TravStats& st) {
+                                               Cur& c, TravStats& st, float tlimit) {
     if (STATS) st.nodes++;
     float l0, l1, r0, r1;
 #if KHP_EXP_DOUBLE_SLAB
@@ -548,6 +556,12 @@ __device__ __forceinline__ void interior_apply(const TravRay& tr, float4 a, floa
 #endif
     bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, l0, l1);
     bool rh = slab(b.z, b.w, cc.x, cc.y, cc.z, cc.w, tr.r, tr.inv, r0, r1);
+#if KHP_PUSH_PRUNE
+    lh = lh && !(l1 < 0.0f || l0 > tlimit);
+    rh = rh && !(r1 < 0.0f || r0 > tlimit);
+#else
+    (void)tlimit;
+#endif
     if (lh && rh) {
         if (l0 < r0) {
             stk.push((uint32_t)rf.y, r0, r1);
@@ -621,7 +635,7 @@ __device__ __forceinline__ void step1_closest(const DevScene& S, const TravRay& 
     } else {
         int4 rf = make_int4(__float_as_int(q3.x), __float_as_int(q3.y), __float_as_int(q3.z), __float_as_int(q3.w));
         prefetch_children(S, rf, pf);
-        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st);
+        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st, h.t);
     }
 }
 
@@ -644,7 +658,7 @@ __device__ __forceinline__ void step1_closest_rec(const TravRay& tr, Hit& h, Sta
         }
     } else {
         int4 rf = make_int4(__float_as_int(q3.x), __float_as_int(q3.y), __float_as_int(q3.z), __float_as_int(q3.w));
-        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st);
+        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st, h.t);
     }
 }
 
@@ -666,7 +680,7 @@ __device__ __forceinline__ bool step1_any(const DevScene& S, const TravRay& tr, 
     } else {
         int4 rf = make_int4(__float_as_int(q3.x), __float_as_int(q3.y), __float_as_int(q3.z), __float_as_int(q3.w));
         prefetch_children(S, rf, pf);
-        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st);
+        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st, tMaxRay);
     }
     return false;
 }

@@ -83,7 +83,8 @@ class Stats(ctypes.Structure):
                 ("bounce_shadow_wave_iters", c_uint64 * 16), ("bounce_shadow_lanes_busy", c_uint64 * 16),
                 ("step_cycles", c_uint64 * 4), ("bvh_on_device", c_uint32), ("pad0", c_uint32),
                 ("flatten_ms", c_double), ("bvh_ms", c_double), ("bvh_kernel_ms", c_double), ("layout_ms", c_double),
-                ("flatten_kernel_ms", c_double), ("layout_kernel_ms", c_double)]
+                ("flatten_kernel_ms", c_double), ("layout_kernel_ms", c_double),
+                ("extend_pruned_pops", c_uint64), ("shadow_pruned_pops", c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if not isinstance(getattr(self, k), (int, float)) else getattr(self, k))

@@ -221,6 +221,8 @@ def main():
             "device_ms": round(last["render_ms"], 3),
             "shadow_nodes_per_ray": round(cnt["shadow_node_visits"] / max(1, cnt["shadow_rays"]), 2),
             "stack_spills_per_ray": round(cnt["stack_spills"] / max(1, rays + cnt["shadow_rays"]), 4),
+            "pruned_pops_per_ray": round(cnt["extend_pruned_pops"] / max(1, rays), 3),
+            "shadow_pruned_pops_per_ray": round(cnt["shadow_pruned_pops"] / max(1, cnt["shadow_rays"]), 3),
             "build_s": round(build_s, 3),
             "setup": setup,
             "per_bounce": [

@@ -192,6 +192,8 @@ typedef struct {
     double layout_ms;                /* node pairing + leaf slots + slot records */
     double flatten_kernel_ms;        /* device flatten: GPU time of its kernels */
     double layout_kernel_ms;         /* device layout: GPU time of its kernels  */
+    /* stack entries popped only to fail the prune test (instrumented renders) */
+    uint64_t extend_pruned_pops, shadow_pruned_pops;
 } khp_stats;
 #define KHP_MAX_BOUNCE_STATS 16
 
