@@ -289,9 +289,9 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
     Hit h;
     Cur c{0u, 0.0f, 0.0f, false};
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
-    Prefetch pf{0.0f, 0.0f};
+    [[maybe_unused]] Prefetch pf{0.0f, 0.0f};
     bool has = false, exhausted = false;
-    uint32_t idx = 0;
+    uint32_t idx = 0, mode = 0u;
     unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
 #if KHP_PROFILE_STEPS
     uint64_t prof[4] = {0, 0, 0, 0}, prof_last = __builtin_amdgcn_s_memtime(), prof_t0 = prof_last;
@@ -313,7 +313,11 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
                 h.slot = -1;
                 h.u = h.v = 0.0f;
                 lf.left = 0;
+#if KHP_LOOP2
+                has = trav2_begin<STATS>(S, tr, h.t, stk, mode, c, lf, st);
+#else
                 has = trav_begin(S, tr, stk, c);
+#endif
                 if (!has) {  // missed the root box
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = -1;
@@ -328,7 +332,23 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
             continue;
         }
         for (;;) {
-#if KHP_ONEFETCH
+#if KHP_LOOP2
+            if (STATS) {
+                unsigned long long wm = __ballot(has && (mode == M_NODE || mode == M_LEAF));
+                ++wit;
+                wbusy += (uint32_t)__popcll(wm);
+            }
+            if (has) {
+                bool occ_unused;
+                if (iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused)) {
+                    Wv.ht[idx] = h.t;
+                    Wv.hslot[idx] = h.slot;
+                    Wv.hu[idx] = h.u;
+                    Wv.hv[idx] = h.v;
+                    has = false;
+                }
+            }
+#elif KHP_ONEFETCH
 #if KHP_PROFILE_STEPS
             uint64_t tp0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
 #endif
@@ -684,9 +704,10 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
     TravRay tr;
     Cur c{0u, 0.0f, 0.0f, false};
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
-    Prefetch pf{0.0f, 0.0f};
+    [[maybe_unused]] Prefetch pf{0.0f, 0.0f};
     unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
     float tmax = 0.0f;
+    uint32_t mode = 0u;
     bool has = false, exhausted = false;
 #if !KHP_ONEFETCH
     bool found = false;
@@ -712,7 +733,11 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
                 found = false;
 #endif
                 lf.left = 0;
+#if KHP_LOOP2
+                has = trav2_begin<STATS>(S, tr, tmax, stk, mode, c, lf, st);
+#else
                 has = trav_begin(S, tr, stk, c);
+#endif
                 if (!has) Wv.vis[idx] = 0;
             }
         }
@@ -722,7 +747,21 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
             continue;
         }
         for (;;) {
-#if KHP_ONEFETCH
+#if KHP_LOOP2
+            if (STATS) {
+                unsigned long long wm = __ballot(has && (mode == M_NODE || mode == M_LEAF));
+                ++wit;
+                wbusy += (uint32_t)__popcll(wm);
+            }
+            if (has) {
+                bool occ = false;
+                Hit hu_{0.0f, -1, 0.0f, 0.0f};
+                if (iter2<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ)) {
+                    Wv.vis[idx] = occ ? 1 : 0;
+                    has = false;
+                }
+            }
+#elif KHP_ONEFETCH
             const bool work = has && resolve<STATS>(S, tmax, stk, c, lf, st);
             if (has && !work) {
                 Wv.vis[idx] = 0;

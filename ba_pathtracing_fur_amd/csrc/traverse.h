@@ -685,6 +685,188 @@ __device__ __forceinline__ bool step1_any(const DevScene& S, const TravRay& tr, 
     return false;
 }
 
+// ---- select-based one-fetch loop (the production kernels) -------------------------------
+// The same visit order and arithmetic as resolve + step1_*, restructured so
+// that a wave iteration has one fetch site, one push site and one pop site
+// instead of a pop inside every branch (interior miss, leaf done, pruned
+// entry) and a pop loop in resolve.  The compiler turns each divergent
+// branch into exec-mask bookkeeping on the scalar unit, and the old shape
+// cost ~185 SALU instructions per wave iteration -- the scalar unit, which
+// the 4 SIMDs of a CU share, was ~75 % busy (profiles/r01g, `mix` pass).
+// A lane is in one of four modes:
+//   M_NODE  the cursor (c) is an interior entry that passed its prune test;
+//   M_LEAF  the lane is testing the candidates of an opened leaf (lf);
+//   M_POP   the lane must pop its next entry (set when a popped entry failed
+//           its prune test: instead of looping, the lane pops again in the
+//           next iteration -- 1.2 such pops per ray against ~110 iterations);
+//   M_IDLE  no ray.
+// Entries are prune-tested exactly when KIRK would pop them, and
+// push-time pruning (KHP_PUSH_PRUNE) applies as in interior_apply.
+#ifndef KHP_LOOP2
+#define KHP_LOOP2 1
+#endif
+enum : uint32_t { M_IDLE = 0u, M_NODE = 1u, M_LEAF = 2u, M_POP = 3u };
+
+// BoundingVolume::intersects as selects: every IEEE operation of slab() is
+// evaluated, the early-out tests are and-ed; t0/t1 are those of slab()
+// whenever the result is true.
+__device__ __forceinline__ bool slab_sel(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                         const TravRay& tr, float& t0, float& t1) {
+    const bool sx = tr.r.d.x < 0.0f, sy = tr.r.d.y < 0.0f, sz = tr.r.d.z < 0.0f;
+    float tmin = ((sx ? mxx : mnx) - tr.r.o.x) * tr.inv.x;
+    float tmax = ((sx ? mnx : mxx) - tr.r.o.x) * tr.inv.x;
+    const float tymin = ((sy ? mxy : mny) - tr.r.o.y) * tr.inv.y;
+    const float tymax = ((sy ? mny : mxy) - tr.r.o.y) * tr.inv.y;
+    bool ok = !((tmin > tymax) || (tymin > tmax));
+    tmin = (tymin > tmin) ? tymin : tmin;
+    tmax = (tymax < tmax) ? tymax : tmax;
+    const float tzmin = ((sz ? mxz : mnz) - tr.r.o.z) * tr.inv.z;
+    const float tzmax = ((sz ? mnz : mxz) - tr.r.o.z) * tr.inv.z;
+    ok = ok && !((tmin > tzmax) || (tzmin > tmax));
+    t0 = (tzmin > tmin) ? tzmin : tmin;
+    t1 = (tzmax < tmax) ? tzmax : tmax;
+    return ok;
+}
+
+#ifndef KHP_SLAB_SEL
+#define KHP_SLAB_SEL 1
+#endif
+__device__ __forceinline__ bool slab2(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                      const TravRay& tr, float& t0, float& t1) {
+#if KHP_SLAB_SEL
+    return slab_sel(mnx, mny, mnz, mxx, mxy, mxz, tr, t0, t1);
+#else
+    return slab(mnx, mny, mnz, mxx, mxy, mxz, tr.r, tr.inv, t0, t1);
+#endif
+}
+
+// A new entry that passed its prune test becomes the lane's work: an interior
+// node is fetched next iteration, a leaf is opened (KIRK's leaf prologue,
+// CPU_BVH.cpp:155-159).
+template <bool STATS>
+__device__ __forceinline__ void take_entry(const DevScene& S, uint32_t ref, float t0, float t1, uint32_t& mode, Cur& c,
+                                           LeafCur& lf, TravStats& st) {
+    const bool leaf = ref_leaf(ref);
+    c.ref = ref;
+    c.t0 = t0;
+    c.t1 = t1;
+    mode = leaf ? M_LEAF : M_NODE;
+    uint32_t cnt = (ref >> 24) & 0x7Fu;
+    if (leaf && cnt == LEAF_CNT_ESC) cnt = S.aux[ref & 0x00FFFFFFu].flags >> 8;
+    lf.slot = leaf ? (ref & 0x00FFFFFFu) : lf.slot;
+    lf.left = leaf ? cnt : 0u;
+    lf.tmax = t1;
+    lf.tl = FLT_MAX_;
+    lf.lu = 0.0f;
+    lf.lv = 0.0f;
+    lf.sl = -1;
+    if (STATS && leaf) st.nodes++;
+}
+
+// Start a ray: root box pre-test (BVH::closestIntersection / isIntersection).
+// Returns false when the ray misses the root box (finished at once).
+template <bool STATS, class Stack>
+__device__ __forceinline__ bool trav2_begin(const DevScene& S, const TravRay& tr, float tlimit, Stack& stk,
+                                            uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st) {
+    stk.clear();
+    float t0, t1;
+    if (!slab(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4], S.root_box[5], tr.r,
+              tr.inv, t0, t1))
+        return false;
+    if (t1 < 0.0f || t0 > tlimit) {  // pruned at pop time: the next pop finds the stack empty
+        if (STATS) st.pruned++;
+        mode = M_POP;
+        return true;
+    }
+    take_entry<STATS>(S, (uint32_t)S.root_ref, t0, t1, mode, c, lf, st);
+    return true;
+}
+
+// One wave iteration of one lane (mode != M_IDLE).  ANY: any-hit with the
+// fixed limit tlimit = the ray's tMax; else closest hit, tlimit = h.t.
+// Returns true when the ray is finished; for ANY, `occluded` tells the result.
+template <bool ANY, bool STATS, class Stack>
+__device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
+                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
+    const bool in_leaf = mode == M_LEAF;
+    const bool fetch = in_leaf || mode == M_NODE;
+    const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
+    float4 q0, q1, q2, q3;
+    if (fetch) {
+        q0 = p[0];
+        q1 = p[1];
+        q2 = p[2];
+        q3 = p[3];
+        pin(q0); pin(q1); pin(q2); pin(q3);
+    }
+    bool need_pop = mode == M_POP;
+    bool have = false;  // a new entry (ref, t0, t1) for take_entry
+    uint32_t eref = 0u;
+    float et0 = 0.0f, et1 = 0.0f;
+    bool push = false;
+    uint32_t pref = 0u;
+    float pt0 = 0.0f, pt1 = 0.0f;
+    if (in_leaf) {
+        if (STATS) st.prims++;
+        if (ANY) {
+            if (any_candidate(q0, q1, q2, q3, tr.r, tmax_any)) {
+                occluded = true;
+                return true;
+            }
+        } else {
+            leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);
+        }
+        ++lf.slot;
+        --lf.left;
+        if (lf.left == 0u) {
+            if (!ANY && lf.sl >= 0 && lf.tl < h.t) {
+                h.t = lf.tl;
+                h.slot = lf.sl;
+                h.u = lf.lu;
+                h.v = lf.lv;
+            }
+            need_pop = true;
+        }
+    } else if (fetch) {
+        if (STATS) st.nodes++;
+        const float tlimit = ANY ? tmax_any : h.t;
+        float l0, l1, r0, r1;
+        bool lh = slab2(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, tr, l0, l1);
+        bool rh = slab2(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, tr, r0, r1);
+        lh = lh && !(l1 < 0.0f || l0 > tlimit);
+        rh = rh && !(r1 < 0.0f || r0 > tlimit);
+        const uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
+        const bool nearl = lh && (!rh || l0 < r0);  // KIRK: left first iff l0 < r0 (ties: right)
+        have = lh || rh;
+        need_pop = !have;
+        push = lh && rh;
+        eref = nearl ? lref : rref;
+        et0 = nearl ? l0 : r0;
+        et1 = nearl ? l1 : r1;
+        pref = nearl ? rref : lref;
+        pt0 = nearl ? r0 : l0;
+        pt1 = nearl ? r1 : l1;
+    }
+    if (push) stk.push(pref, pt0, pt1);
+    if (need_pop) {
+        if (stk.empty()) {
+            mode = M_IDLE;
+            occluded = false;
+            return true;
+        }
+        stk.pop(eref, et0, et1);
+        const float tlimit = ANY ? tmax_any : h.t;
+        if (et1 < 0.0f || et0 > tlimit) {
+            if (STATS) st.pruned++;
+            mode = M_POP;
+        } else {
+            have = true;
+        }
+    }
+    if (have) take_entry<STATS>(S, eref, et0, et1, mode, c, lf, st);
+    return false;
+}
+
 // Whole-ray forms (batch query kernels).
 template <bool STATS, class Stack>
 __device__ __forceinline__ void trace_closest(const DevScene& S, const Ray& r, Hit& h, Stack& stk, TravStats& st) {
