@@ -97,14 +97,19 @@ struct LdsStack {
         lds[k + 2 * R * 256] = bits_from_f(b);
         ++sp;
     }
+    // The ring slot is read unconditionally (a stale but harmless slot when
+    // the entry was spilled), pinned, and the rare spill read overrides it.
+    // Otherwise the compiler merges both reads into FLAT loads through a
+    // selected pointer: 3 extra vector-memory instructions and a vmcnt(0)
+    // wait on every pop.
     __device__ __forceinline__ void pop(uint32_t& r, float& a, float& b) {
         --sp;
-        if (sp >= lo) {
-            uint32_t k = slot(sp);
-            r = lds[k];
-            a = f_from_bits(lds[k + R * 256]);
-            b = f_from_bits(lds[k + 2 * R * 256]);
-        } else {
+        const uint32_t k = slot(sp);
+        r = lds[k];
+        a = f_from_bits(lds[k + R * 256]);
+        b = f_from_bits(lds[k + 2 * R * 256]);
+        asm volatile("" : "+v"(r), "+v"(a), "+v"(b));  // the LDS reads happen here
+        if (sp < lo) {
             int4 e = *gcell(sp);
             r = (uint32_t)e.x;
             a = f_from_bits((uint32_t)e.y);
