@@ -159,8 +159,8 @@ __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
 constexpr int RING = KHP_RING;        // k_extend LDS ring entries per lane (3 x 4 B each)
 constexpr int RING_SH = KHP_RING_SH;  // k_shadow
 constexpr int REFILL = KHP_REFILL;  // refill when >= REFILL lanes are idle
-constexpr size_t LDS_BYTES = 3 * RING * 256 * sizeof(uint32_t);
-constexpr size_t LDS_BYTES_SH = 3 * RING_SH * 256 * sizeof(uint32_t);
+constexpr size_t LDS_BYTES = 3 * RING * TRAV_BLOCK * sizeof(uint32_t);
+constexpr size_t LDS_BYTES_SH = 3 * RING_SH * TRAV_BLOCK * sizeof(uint32_t);
 
 #ifndef KHP_TOPREG
 #define KHP_TOPREG 0   // 1: stack top in registers with a prefetched next top (exact; measured 16 % slower)
@@ -279,7 +279,7 @@ __device__ __forceinline__ void trav_round(const DevScene& S, const TravRay& tr,
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
+__global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = Wv.cnt->nq[cur];
     TravStack<RING, STATS> stk;
@@ -333,6 +333,7 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
         }
         for (;;) {
 #if KHP_LOOP2
+            const bool tail_pf = KHP_TAIL_PF && exhausted && __popcll(act) <= KHP_TAIL_PF_LANES;
             if (STATS) {
                 unsigned long long wm = __ballot(has && (mode == M_NODE || mode == M_LEAF));
                 ++wit;
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
             }
             if (has) {
                 bool occ_unused;
-                if (iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused)) {
+                if (iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused, tail_pf, pf)) {
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = h.slot;
                     Wv.hu[idx] = h.u;
@@ -396,6 +397,9 @@ __global__ __launch_bounds__(256, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave
             }
 #endif
             act = __ballot(has);
+#if KHP_EXP_ABANDON   // timing experiment only (wrong results): sparse waves drop their rays once the queue is drained
+            if (exhausted && (uint32_t)__popcll(act) <= (uint32_t)KHP_EXP_ABANDON) { has = false; act = 0; }
+#endif
             if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
     }
@@ -695,7 +699,7 @@ __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
+__global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = Wv.shq->nsh;
     TravStack<RING_SH, STATS> stk;
@@ -748,6 +752,7 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
         }
         for (;;) {
 #if KHP_LOOP2
+            const bool tail_pf = KHP_TAIL_PF && exhausted && __popcll(act) <= KHP_TAIL_PF_LANES;
             if (STATS) {
                 unsigned long long wm = __ballot(has && (mode == M_NODE || mode == M_LEAF));
                 ++wit;
@@ -756,7 +761,7 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
             if (has) {
                 bool occ = false;
                 Hit hu_{0.0f, -1, 0.0f, 0.0f};
-                if (iter2<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ)) {
+                if (iter2<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ, tail_pf, pf)) {
                     Wv.vis[idx] = occ ? 1 : 0;
                     has = false;
                 }
@@ -785,6 +790,9 @@ __global__ __launch_bounds__(256, KHP_SH_WAVES) void k_shadow(DevScene S, Wave W
             }
 #endif
             act = __ballot(has);
+#if KHP_EXP_ABANDON   // timing experiment only (wrong results): sparse waves drop their rays once the queue is drained
+            if (exhausted && (uint32_t)__popcll(act) <= (uint32_t)KHP_EXP_ABANDON) { has = false; act = 0; }
+#endif
             if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
     }
@@ -1034,20 +1042,77 @@ struct TimedLaunch {
     hipEvent_t a, b;
 };
 
+// One independent set of in-flight paths: its own SoA wavefront state, queue
+// counters, shadow queues, traversal spill columns and stream pair.  A frame
+// is cut into up to KHP_MAX_SUBFRAMES pixel ranges, one per set, whose bounce
+// pipelines run on their own streams: a persistent traversal kernel's tail
+// (its last long rays on a mostly idle chip) fills with another set's blocks.
+#ifndef KHP_MAX_SUBFRAMES
+#define KHP_MAX_SUBFRAMES 4
+#endif
+#ifndef KHP_SUBFRAMES_DEFAULT
+#define KHP_SUBFRAMES_DEFAULT 1   // env KHP_SUBFRAMES overrides (1..KHP_MAX_SUBFRAMES)
+#endif
+#ifndef KHP_STAGGER_DEFAULT
+#define KHP_STAGGER_DEFAULT 0     // env KHP_STAGGER
+#endif
+#ifndef KHP_SET_STREAMS_DEFAULT
+#define KHP_SET_STREAMS_DEFAULT 2  // env KHP_SET_STREAMS: 1 = a set's shadow stage on its own main stream
+#endif
+struct PathSet {
+    size_t cap = 0;
+    DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
+    hipStream_t sA = nullptr, sB = nullptr;
+};
+
+#ifndef KHP_MAX_INFLIGHT
+#define KHP_MAX_INFLIGHT 3
+#endif
+#ifndef KHP_FRAMES_IN_FLIGHT_DEFAULT
+#define KHP_FRAMES_IN_FLIGHT_DEFAULT 2   // env KHP_FRAMES_IN_FLIGHT (asynchronous renders)
+#endif
+struct Snap {
+    int set;
+    uint32_t bounce;
+};
+// One frame slot: the events of the frame last enqueued on its path sets.
+struct FrameSlot {
+    std::vector<hipEvent_t> ev_pool, sync_pool;  // timing / ordering events, reused per frame
+    size_t ev_next = 0, sync_next = 0;
+    std::vector<TimedLaunch> launches;
+    std::vector<Snap> snaps;
+    hipEvent_t ev_start = nullptr, done_t = nullptr, done = nullptr;
+    bool inflight = false;
+    int K = 1;
+};
+static hipEvent_t slot_event(std::vector<hipEvent_t>& pool, size_t& next, bool no_timing) {
+    if (next == pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, no_timing ? hipEventDisableTiming : hipEventDefault) != hipSuccess) return nullptr;
+        pool.push_back(e);
+    }
+    return pool[next++];
+}
+
 struct khp_ctx {
     int device = 0;
     uint32_t flags = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;   // shadow stage of bounce b beside extend of bounce b+1
     std::vector<hipEvent_t> sync_pool;  // ordering events (no timing)
     int n_cu = 256;
     HostScene hs;
     bool scene_set = false, built = false;
     DevMem prims, aux, trinrm, trifrm, nodes, mats, lights;
     DevScene S{};
-    // wavefront
-    size_t cap = 0;
-    DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
+    // wavefront: path sets, KHP_MAX_SUBFRAMES per frame slot (ps[0] also serves the batch query API)
+    PathSet ps[KHP_MAX_INFLIGHT * KHP_MAX_SUBFRAMES];
+    FrameSlot fs[KHP_MAX_INFLIGHT];
+    uint64_t frame_no = 0;
+    hipEvent_t fb_evt = nullptr;   // the last framebuffer operation enqueued (accumulate or gather)
+    bool report_open = false;      // c->st accumulates harvested frames
+    hipEvent_t gather_evt = nullptr;  // end of the last framebuffer gather (becomes fb_evt)
+    hipEvent_t report_ref = nullptr;  // time origin of the open report
+    std::vector<std::pair<float, float>> ext_iv;  // the report's k_extend intervals (ms from report_ref)
     // framebuffer + pixel list
     DeviceObjects obj;        // device-flattened objects (device path)
     bool scene_on_host = false;
@@ -1072,6 +1137,8 @@ struct khp_ctx {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
 };
+
+static khp_status drain(khp_ctx* c);
 
 static hipEvent_t next_event(khp_ctx* c) {
     if (c->ev_next == c->ev_pool.size()) {
@@ -1107,9 +1174,7 @@ extern "C" khp_status khp_create(khp_ctx** out, int device, uint32_t flags) {
     c->flags = flags;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
-        if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(KHP_EDEVICE, "hipStreamCreate failed");
     }
@@ -1120,12 +1185,24 @@ extern "C" khp_status khp_create(khp_ctx** out, int device, uint32_t flags) {
 extern "C" void khp_destroy(khp_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    (void)drain(c);
+    if (c->gather_evt) (void)hipEventDestroy(c->gather_evt);
+    if (c->report_ref) (void)hipEventDestroy(c->report_ref);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    for (auto& w : c->ps) {
+        for (hipStream_t s : {w.sA, w.sB}) {
+            if (!s) continue;
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    }
+    for (auto& f : c->fs) {
+        for (auto e : f.ev_pool) (void)hipEventDestroy(e);
+        for (auto e : f.sync_pool) (void)hipEventDestroy(e);
+    }
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     for (auto e : c->sync_pool) (void)hipEventDestroy(e);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1133,6 +1210,10 @@ extern "C" void khp_destroy(khp_ctx* c) {
 static bool host_path(const khp_ctx* c) { return (c->flags & KHP_CTX_HOST_BUILD) || getenv("KHP_HOST_BUILD"); }
 
 static khp_status set_scene_impl(khp_ctx* c, const khp_scene* s, bool device_ptrs) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c) return fail(KHP_EINVAL, "ctx is null");
     auto t0 = std::chrono::steady_clock::now();
     const bool host = host_path(c);
@@ -1166,6 +1247,10 @@ extern "C" khp_status khp_set_scene_device(khp_ctx* c, const khp_scene* s) { ret
 extern "C" khp_status khp_gen_hairball_device(khp_ctx* c, uint32_t n, uint32_t verts, const float center[3],
                                               float ball_r, float root_r, uint32_t seed, float* d_base_r0,
                                               float* d_apex_r1) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || !center || (n && (!d_base_r0 || !d_apex_r1)) || verts < 2 || verts > 64)
         return fail(KHP_EINVAL, "bad hairball arguments");
     HIPCHK(hipSetDevice(c->device));
@@ -1177,6 +1262,10 @@ extern "C" khp_status khp_gen_hairball_device(khp_ctx* c, uint32_t n, uint32_t v
 extern "C" khp_status khp_gen_hairball_tris_device(khp_ctx* c, uint32_t n, uint32_t verts, const float center[3],
                                                    float ball_r, float root_r, uint32_t seed, uint32_t res,
                                                    float* d_v, float* d_n, float* d_frame) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || !center || (n && (!d_v || !d_n || !d_frame)) || verts < 2 || verts > 64 || res == 0)
         return fail(KHP_EINVAL, "bad hairball arguments");
     HIPCHK(hipSetDevice(c->device));
@@ -1201,6 +1290,10 @@ extern "C" khp_status khp_device_free(khp_ctx* c, void* p) {
 }
 
 extern "C" khp_status khp_device_copy(khp_ctx* c, void* dst, const void* src, size_t bytes, int to_device) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || (bytes && (!dst || !src))) return fail(KHP_EINVAL, "null argument");
     HIPCHK(hipSetDevice(c->device));
     if (bytes)
@@ -1218,6 +1311,10 @@ static hipError_t upload(DevMem& m, const T* data, size_t count, hipStream_t s) 
 }
 
 extern "C" khp_status khp_build_accel(khp_ctx* c) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c) return fail(KHP_EINVAL, "ctx is null");
     if (!c->scene_set) return fail(KHP_ENOTREADY, "khp_set_scene first");
     HIPCHK(hipSetDevice(c->device));
@@ -1314,12 +1411,12 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     // persistent grid sizes
     int nb = 0;
     if (c->flags & KHP_CTX_STATS)
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<true>, 256, LDS_BYTES));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<true>, TRAV_BLOCK, LDS_BYTES));
     else
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, 256, LDS_BYTES));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, TRAV_BLOCK, LDS_BYTES));
     c->grid_ext = std::max(1, nb) * c->n_cu;
     nb = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, 256, LDS_BYTES_SH));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, TRAV_BLOCK, LDS_BYTES_SH));
     c->grid_sh = std::max(1, nb) * c->n_cu;
     nb = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade, 256, 0));
@@ -1328,58 +1425,62 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     return KHP_OK;
 }
 
-static khp_status ensure_wave(khp_ctx* c, size_t cap) {
-    if (cap <= c->cap) return KHP_OK;
+static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap) {
+    if (cap <= w.cap) return KHP_OK;
     for (int q = 0; q < 2; ++q)
-        for (int k = 0; k < 7; ++k) HIPCHK(c->qbuf[q][k].ensure(cap * 4));
-    HIPCHK(c->ht.ensure(cap * 4));
-    HIPCHK(c->hslot.ensure(cap * 4));
-    HIPCHK(c->hu.ensure(cap * 4));
-    HIPCHK(c->hv.ensure(cap * 4));
+        for (int k = 0; k < 7; ++k) HIPCHK(w.qbuf[q][k].ensure(cap * 4));
+    HIPCHK(w.ht.ensure(cap * 4));
+    HIPCHK(w.hslot.ensure(cap * 4));
+    HIPCHK(w.hu.ensure(cap * 4));
+    HIPCHK(w.hv.ensure(cap * 4));
     for (int k = 0; k < 3; ++k) {
-        HIPCHK(c->Tb[k].ensure(cap * 4));
-        HIPCHK(c->Cb[k].ensure(cap * 4));
+        HIPCHK(w.Tb[k].ensure(cap * 4));
+        HIPCHK(w.Cb[k].ensure(cap * 4));
     }
-    HIPCHK(c->flagsb.ensure(cap * 4));
-    HIPCHK(c->keyb.ensure(cap * 4));
+    HIPCHK(w.flagsb.ensure(cap * 4));
+    HIPCHK(w.keyb.ensure(cap * 4));
     for (int q = 0; q < 2; ++q) {
-        HIPCHK(c->visb[q].ensure(cap));
-        HIPCHK(c->shb[q].ensure(cap * 6 * sizeof(float4)));
+        HIPCHK(w.visb[q].ensure(cap));
+        HIPCHK(w.shb[q].ensure(cap * 6 * sizeof(float4)));
     }
-    HIPCHK(c->shqb.ensure(2 * sizeof(ShadowQ)));
-    HIPCHK(c->cnt.ensure(sizeof(Counters)));
+    HIPCHK(w.shqb.ensure(2 * sizeof(ShadowQ)));
+    HIPCHK(w.cnt.ensure(sizeof(Counters)));
     // traversal-stack spill columns: one per resident lane, STACK_MAX entries deep
     // separate spill columns: k_extend and k_shadow may run at the same time
-    HIPCHK(c->spill.ensure((size_t)c->grid_ext * 256 * STACK_MAX * sizeof(int4)));
-    HIPCHK(c->spill_sh.ensure((size_t)c->grid_sh * 256 * STACK_MAX * sizeof(int4)));
-    c->cap = cap;
+    HIPCHK(w.spill.ensure((size_t)c->grid_ext * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
+    HIPCHK(w.spill_sh.ensure((size_t)c->grid_sh * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
+    if (!w.sA) {
+        HIPCHK(hipStreamCreateWithFlags(&w.sA, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&w.sB, hipStreamNonBlocking));
+    }
+    w.cap = cap;
     return KHP_OK;
 }
 
 // Device pointers of the wavefront state (sized by ensure_wave).
-static Wave wave_view(khp_ctx* c) {
+static Wave wave_view(PathSet& w) {
     Wave Wv{};
     for (int q = 0; q < 2; ++q) {
         for (int k = 0; k < 3; ++k) {
-            Wv.qo[q][k] = c->qbuf[q][k].as<float>();
-            Wv.qd[q][k] = c->qbuf[q][3 + k].as<float>();
+            Wv.qo[q][k] = w.qbuf[q][k].as<float>();
+            Wv.qd[q][k] = w.qbuf[q][3 + k].as<float>();
         }
-        Wv.qpid[q] = c->qbuf[q][6].as<uint32_t>();
+        Wv.qpid[q] = w.qbuf[q][6].as<uint32_t>();
     }
-    Wv.ht = c->ht.as<float>();
-    Wv.hslot = c->hslot.as<int32_t>();
-    Wv.hu = c->hu.as<float>();
-    Wv.hv = c->hv.as<float>();
+    Wv.ht = w.ht.as<float>();
+    Wv.hslot = w.hslot.as<int32_t>();
+    Wv.hu = w.hu.as<float>();
+    Wv.hv = w.hv.as<float>();
     for (int k = 0; k < 3; ++k) {
-        Wv.T[k] = c->Tb[k].as<float>();
-        Wv.C[k] = c->Cb[k].as<float>();
+        Wv.T[k] = w.Tb[k].as<float>();
+        Wv.C[k] = w.Cb[k].as<float>();
     }
-    Wv.flags = c->flagsb.as<int32_t>();
-    Wv.key = c->keyb.as<uint32_t>();
-    Wv.vis = c->visb[0].as<uint8_t>();
-    Wv.sh = c->shb[0].as<float4>();
-    Wv.shq = c->shqb.as<ShadowQ>();
-    Wv.cnt = c->cnt.as<Counters>();
+    Wv.flags = w.flagsb.as<int32_t>();
+    Wv.key = w.keyb.as<uint32_t>();
+    Wv.vis = w.visb[0].as<uint8_t>();
+    Wv.sh = w.shb[0].as<float4>();
+    Wv.shq = w.shqb.as<ShadowQ>();
+    Wv.cnt = w.cnt.as<Counters>();
     return Wv;
 }
 
@@ -1424,166 +1525,23 @@ static khp_status check_params(khp_ctx* c, const khp_render_params* p) {
     return KHP_OK;
 }
 
-static void timed(khp_ctx* c, int kind, bool begin, hipStream_t st = nullptr) {
-    hipEvent_t e = next_event(c);
+static void timed(khp_ctx* c, FrameSlot& f, int kind, bool begin, hipStream_t st) {
+    hipEvent_t e = slot_event(f.ev_pool, f.ev_next, false);
     if (!e) return;
-    (void)hipEventRecord(e, st ? st : c->stream);
-    if (begin) c->launches.push_back(TimedLaunch{kind, c->cur_bounce, e, nullptr});
-    else c->launches.back().b = e;
+    (void)hipEventRecord(e, st);
+    if (begin) f.launches.push_back(TimedLaunch{kind, c->cur_bounce, e, nullptr});
+    else f.launches.back().b = e;
 }
 
-extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* out_rgb) {
-    khp_status s = check_params(c, p);
-    if (s != KHP_OK) return s;
-    HIPCHK(hipSetDevice(c->device));
-    const size_t npix = (size_t)p->width * p->height;
-    if (c->fbW != p->width || c->fbH != p->height || !c->fb.p) {
-        HIPCHK(c->fb.ensure(npix * 3 * sizeof(float)));
-        HIPCHK(hipMemsetAsync(c->fb.p, 0, npix * 3 * sizeof(float), c->stream));
-        c->fbW = p->width;
-        c->fbH = p->height;
-    }
-    s = prepare_pixels(c, p);
-    if (s != KHP_OK) return s;
-    const uint32_t P_all = (uint32_t)c->pix_host.size();
-    size_t cap_paths = (size_t)1 << 24;
-    if (const char* e = getenv("KHP_MAX_PATHS")) cap_paths = std::max<size_t>(4096, strtoull(e, nullptr, 10));
-    uint32_t P_chunk = (uint32_t)std::min<size_t>(P_all, cap_paths);
-    uint32_t S_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(p->spp, cap_paths / std::max<uint32_t>(P_chunk, 1)));
-    s = ensure_wave(c, (size_t)P_chunk * S_chunk);
-    if (s != KHP_OK) return s;
-    HIPCHK(hipMemsetAsync(c->cnt.p, 0, sizeof(Counters), c->stream));
-    const bool stats = (c->flags & KHP_CTX_STATS) != 0 || (p->flags & KHP_RENDER_STATS) != 0;
-    c->launches.clear();
-    c->ev_next = 0;
-    Wave Wv = wave_view(c);
-    Wv.pix = c->pix.as<uint32_t>();
-    Wv.W = p->width;
-    Wv.H = p->height;
-    Wv.seed = p->seed;
-    Wv.depth = p->depth;
-    SpillArea sp_ext{c->spill.as<int4>(), (uint32_t)c->grid_ext * 256u};
-    SpillArea sp_sh{c->spill_sh.as<int4>(), (uint32_t)c->grid_sh * 256u};
-    HIPCHK(hipMemsetAsync(c->shqb.p, 0, 2 * sizeof(ShadowQ), c->stream));
-    size_t n_snap = 0;
-    std::vector<uint32_t> snap_bounce;
-    const char* dump_env = getenv("KHP_DUMP_BOUNCE");
-    const int dump_b = dump_env ? atoi(dump_env) : -1;
-    if (stats) {
-        size_t chunks = (size_t)((P_all + P_chunk - 1) / P_chunk) * ((p->spp + S_chunk - 1) / S_chunk);
-        HIPCHK(c->snap.ensure(chunks * p->depth * sizeof(Counters)));
-    }
-    // Two streams: A runs generate / extend / shade / accumulate, B runs the
-    // shadow stage (k_shadow + k_shadow_finish) of bounce b while A already
-    // traverses bounce b+1, so each persistent kernel's tail fills with the
-    // other's blocks.  Ordering: B(b) after shade(b) on A; shade(b+1) after
-    // B(b) (both update the path colour C in bounce order); the shadow queue
-    // of bounce b+2 reuses parity b's buffers only after shade(b+1), which
-    // already waited for B(b).  Instrumented renders stay on one stream so the
-    // per-bounce counter snapshots are exact.
-    const bool overlap = !stats && !getenv("KHP_NO_OVERLAP");
-    hipStream_t sA = c->stream, sB = overlap ? c->stream2 : c->stream;
-    size_t n_sync = 0;
-    c->cur_bounce = -1;
-    hipEvent_t ev_start = next_event(c);
-    (void)hipEventRecord(ev_start, sA);
-    if (overlap) {
-        hipEvent_t e0 = sync_event(c, n_sync++);
-        HIPCHK(hipEventRecord(e0, sA));
-        HIPCHK(hipStreamWaitEvent(sB, e0, 0));
-    }
-    for (uint32_t p0 = 0; p0 < P_all; p0 += P_chunk) {
-        uint32_t P = std::min(P_chunk, P_all - p0);
-        for (uint32_t s0 = 0; s0 < p->spp; s0 += S_chunk) {
-            uint32_t ns = std::min(S_chunk, p->spp - s0);
-            Wv.P = P;
-            Wv.p_off = p0;
-            Wv.sample0 = p->first_sample + s0;
-            Wv.n_samples = ns;
-            uint32_t npaths = P * ns;
-            timed(c, 3, true, sA);
-            hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wv);
-            timed(c, 3, false, sA);
-            hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
-            for (uint32_t b = 0; b < p->depth; ++b) {
-                int cur = b & 1;
-                const int par = b & 1;
-                c->cur_bounce = (int)b;
-                Wave Wb = Wv;
-                Wb.sh = c->shb[par].as<float4>();
-                Wb.vis = c->visb[par].as<uint8_t>();
-                Wb.shq = c->shqb.as<ShadowQ>() + par;
-                if (dump_b == (int)b) {
-                    uint32_t nq = 0;
-                    HIPCHK(hipMemcpyAsync(&nq, &Wv.cnt->nq[cur], 4, hipMemcpyDeviceToHost, sA));
-                    HIPCHK(hipStreamSynchronize(sA));
-                    c->dump.resize(6 * (size_t)nq);
-                    for (int k = 0; k < 3; ++k) {
-                        HIPCHK(hipMemcpy(c->dump.data() + (size_t)k * nq, Wv.qo[cur][k], 4 * (size_t)nq, hipMemcpyDeviceToHost));
-                        HIPCHK(hipMemcpy(c->dump.data() + (size_t)(3 + k) * nq, Wv.qd[cur][k], 4 * (size_t)nq, hipMemcpyDeviceToHost));
-                    }
-                }
-                hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
-                timed(c, 0, true, sA);
-                if (stats)
-                    hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(256), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
-                else
-                    hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(256), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
-                timed(c, 0, false, sA);
-                if (done_b) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
-                timed(c, 1, true, sA);
-                hipLaunchKernelGGL(k_shade, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
-                timed(c, 1, false, sA);
-                if (overlap) {
-                    hipEvent_t shaded = sync_event(c, n_sync++);
-                    HIPCHK(hipEventRecord(shaded, sA));
-                    HIPCHK(hipStreamWaitEvent(sB, shaded, 0));
-                }
-                timed(c, 2, true, sB);
-                if (stats)
-                    hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, sB, c->S, Wb, sp_sh);
-                else
-                    hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, sB, c->S, Wb, sp_sh);
-                timed(c, 2, false, sB);
-                timed(c, 2, true, sB);   // shadow stage = any-hit traversal + finish
-                hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
-                timed(c, 2, false, sB);
-                if (overlap) {
-                    done_b = sync_event(c, n_sync++);
-                    HIPCHK(hipEventRecord(done_b, sB));
-                }
-                if (stats) {
-                    HIPCHK(hipMemcpyAsync(c->snap.as<Counters>() + n_snap, c->cnt.p, sizeof(Counters),
-                                          hipMemcpyDeviceToDevice, sA));
-                    snap_bounce.push_back(b);
-                    ++n_snap;
-                }
-            }
-            c->cur_bounce = -1;
-            if (done_b) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
-            timed(c, 3, true, sA);
-            hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, c->fb.as<float>());
-            timed(c, 3, false, sA);
-            if (overlap) {  // the next chunk's shadow stages come after this chunk's accumulate
-                hipEvent_t acc = sync_event(c, n_sync++);
-                HIPCHK(hipEventRecord(acc, sA));
-                HIPCHK(hipStreamWaitEvent(sB, acc, 0));
-            }
-        }
-    }
-    hipEvent_t ev_end = next_event(c);
-    (void)hipEventRecord(ev_end, c->stream);
-    HIPCHK(hipGetLastError());
-    if (out_rgb && !(p->flags & KHP_RENDER_NO_READBACK)) {
-        hipMemcpyKind kind = (p->flags & KHP_RENDER_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-        HIPCHK(hipMemcpyAsync(out_rgb, c->fb.p, npix * 3 * sizeof(float), kind, c->stream));
-    }
-    HIPCHK(hipStreamSynchronize(c->stream));
-    float ms = 0.0f;
-    HIPCHK(hipEventElapsedTime(&ms, ev_start, ev_end));
-    c->st.render_ms = ms;
+// Zero the per-report fields of c->st (timings, counters, per-bounce tables).
+static void report_begin(khp_ctx* c) {
+    c->st.render_ms = 0.0;
     c->st.extend_ms = c->st.shade_ms = c->st.shadow_ms = c->st.other_ms = 0.0;
     c->st.extend_launches = 0;
+    c->st.extend_rays = c->st.shadow_rays = c->st.node_visits = c->st.prim_tests = 0;
+    c->st.shadow_node_visits = c->st.shadow_prim_tests = c->st.stack_spills = 0;
+    c->st.extend_pruned_pops = c->st.shadow_pruned_pops = 0;
+    for (int q = 0; q < 4; ++q) c->st.step_cycles[q] = 0;
     for (int k = 0; k < KHP_MAX_BOUNCE_STATS; ++k) {
         c->st.bounce_extend_ms[k] = c->st.bounce_shadow_ms[k] = 0.0;
         c->st.bounce_rays[k] = c->st.bounce_nodes[k] = c->st.bounce_prims[k] = 0;
@@ -1591,10 +1549,53 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
         c->st.bounce_wave_iters[k] = c->st.bounce_lanes_busy[k] = 0;
         c->st.bounce_shadow_wave_iters[k] = c->st.bounce_shadow_lanes_busy[k] = 0;
     }
-    for (auto& l : c->launches) {
+    c->st.frames = 0;
+    c->st.extend_busy_ms = 0.0;
+    c->ext_iv.clear();
+    if (!c->report_ref) (void)hipEventCreate(&c->report_ref);
+    (void)hipEventRecord(c->report_ref, c->stream);
+    c->report_open = true;
+}
+
+// Union of the report's k_extend intervals (ms).
+static double union_ms(std::vector<std::pair<float, float>>& iv) {
+    std::sort(iv.begin(), iv.end());
+    double tot = 0.0, lo = 0.0, hi = -1.0;
+    for (auto& x : iv) {
+        if (x.first > hi) {
+            if (hi > lo) tot += hi - lo;
+            lo = x.first;
+            hi = x.second;
+        } else if (x.second > hi) {
+            hi = x.second;
+        }
+    }
+    if (hi > lo) tot += hi - lo;
+    return tot;
+}
+
+// Wait for one in-flight frame and add its timings and counters to the open report.
+static khp_status harvest(khp_ctx* c, int slot) {
+    FrameSlot& f = c->fs[slot];
+    if (!f.inflight) return KHP_OK;
+    f.inflight = false;
+    HIPCHK(hipEventSynchronize(f.done));
+    if (!c->report_open) report_begin(c);
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, f.ev_start, f.done_t) == hipSuccess) c->st.render_ms += ms;
+    c->st.frames += 1;
+    c->st.subframes = (uint32_t)f.K;
+    for (auto& l : f.launches) {
         float t = 0.0f;
         if (l.b && hipEventElapsedTime(&t, l.a, l.b) == hipSuccess) {
-            if (l.kind == 0) { c->st.extend_ms += t; c->st.extend_launches++; }
+            if (l.kind == 0) {
+                c->st.extend_ms += t;
+                c->st.extend_launches++;
+                float t0 = 0.0f, t1 = 0.0f;
+                if (hipEventElapsedTime(&t0, c->report_ref, l.a) == hipSuccess &&
+                    hipEventElapsedTime(&t1, c->report_ref, l.b) == hipSuccess)
+                    c->ext_iv.push_back({t0, t1});
+            }
             else if (l.kind == 1) c->st.shade_ms += t;
             else if (l.kind == 2) c->st.shadow_ms += t;
             else c->st.other_ms += t;
@@ -1604,39 +1605,350 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
             }
         }
     }
-    Counters hc;
-    HIPCHK(hipMemcpy(&hc, c->cnt.p, sizeof(hc), hipMemcpyDeviceToHost));
-    c->st.extend_rays = hc.ext_rays;
-    c->st.shadow_rays = hc.sh_rays;
-    c->st.node_visits = hc.node_visits;
-    c->st.prim_tests = hc.prim_tests;
-    c->st.shadow_node_visits = hc.sh_node_visits;
-    c->st.shadow_prim_tests = hc.sh_prim_tests;
-    c->st.stack_spills = hc.spills;
-    c->st.extend_pruned_pops = hc.pruned;
-    c->st.shadow_pruned_pops = hc.sh_pruned;
-    for (int k = 0; k < 4; ++k) c->st.step_cycles[k] = hc.step_cycles[k];
-    if (n_snap) {
-        std::vector<Counters> sn(n_snap);
-        HIPCHK(hipMemcpy(sn.data(), c->snap.p, n_snap * sizeof(Counters), hipMemcpyDeviceToHost));
-        Counters prev{};
-        for (size_t k = 0; k < n_snap; ++k) {
-            const uint32_t b = snap_bounce[k];
+    for (int k = 0; k < f.K; ++k) {
+        Counters hc;
+        HIPCHK(hipMemcpy(&hc, c->ps[slot * KHP_MAX_SUBFRAMES + k].cnt.p, sizeof(hc), hipMemcpyDeviceToHost));
+        c->st.extend_rays += hc.ext_rays;
+        c->st.shadow_rays += hc.sh_rays;
+        c->st.node_visits += hc.node_visits;
+        c->st.prim_tests += hc.prim_tests;
+        c->st.shadow_node_visits += hc.sh_node_visits;
+        c->st.shadow_prim_tests += hc.sh_prim_tests;
+        c->st.stack_spills += hc.spills;
+        c->st.extend_pruned_pops += hc.pruned;
+        c->st.shadow_pruned_pops += hc.sh_pruned;
+        for (int q = 0; q < 4; ++q) c->st.step_cycles[q] += hc.step_cycles[q];
+    }
+    c->st.extend_busy_ms = union_ms(c->ext_iv);
+    if (!f.snaps.empty()) {
+        std::vector<Counters> sn(f.snaps.size());
+        HIPCHK(hipMemcpy(sn.data(), c->snap.p, sn.size() * sizeof(Counters), hipMemcpyDeviceToHost));
+        std::vector<Counters> prev(f.K, Counters{});   // per set: counters after its previous snapshot
+        for (size_t i = 0; i < sn.size(); ++i) {
+            const uint32_t b = f.snaps[i].bounce;
+            Counters& pv = prev[f.snaps[i].set];
             if (b < KHP_MAX_BOUNCE_STATS) {
-                c->st.bounce_rays[b] += sn[k].ext_rays - prev.ext_rays;
-                c->st.bounce_nodes[b] += sn[k].node_visits - prev.node_visits;
-                c->st.bounce_prims[b] += sn[k].prim_tests - prev.prim_tests;
-                c->st.bounce_shadow_rays[b] += sn[k].sh_rays - prev.sh_rays;
-                c->st.bounce_shadow_nodes[b] += sn[k].sh_node_visits - prev.sh_node_visits;
-                c->st.bounce_shadow_prims[b] += sn[k].sh_prim_tests - prev.sh_prim_tests;
-                c->st.bounce_wave_iters[b] += sn[k].iters - prev.iters;
-                c->st.bounce_lanes_busy[b] += sn[k].lanes_busy - prev.lanes_busy;
-                c->st.bounce_shadow_wave_iters[b] += sn[k].sh_iters - prev.sh_iters;
-                c->st.bounce_shadow_lanes_busy[b] += sn[k].sh_lanes_busy - prev.sh_lanes_busy;
+                c->st.bounce_rays[b] += sn[i].ext_rays - pv.ext_rays;
+                c->st.bounce_nodes[b] += sn[i].node_visits - pv.node_visits;
+                c->st.bounce_prims[b] += sn[i].prim_tests - pv.prim_tests;
+                c->st.bounce_shadow_rays[b] += sn[i].sh_rays - pv.sh_rays;
+                c->st.bounce_shadow_nodes[b] += sn[i].sh_node_visits - pv.sh_node_visits;
+                c->st.bounce_shadow_prims[b] += sn[i].sh_prim_tests - pv.sh_prim_tests;
+                c->st.bounce_wave_iters[b] += sn[i].iters - pv.iters;
+                c->st.bounce_lanes_busy[b] += sn[i].lanes_busy - pv.lanes_busy;
+                c->st.bounce_shadow_wave_iters[b] += sn[i].sh_iters - pv.sh_iters;
+                c->st.bounce_shadow_lanes_busy[b] += sn[i].sh_lanes_busy - pv.sh_lanes_busy;
             }
-            prev = sn[k];
+            pv = sn[i];
+        }
+        f.snaps.clear();
+    }
+    return KHP_OK;
+}
+
+// Wait for every in-flight frame (their stats go to the open report) and for
+// the context stream.  Every entry point that reads or replaces device state
+// other than through an asynchronous render calls this first.
+static khp_status drain(khp_ctx* c) {
+    for (int s = 0; s < KHP_MAX_INFLIGHT; ++s) {
+        khp_status r = harvest(c, s);
+        if (r != KHP_OK) return r;
+    }
+    if (c->stream) HIPCHK(hipStreamSynchronize(c->stream));
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_sync(khp_ctx* c) {
+    if (!c) return fail(KHP_EINVAL, "null context");
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->report_open) report_begin(c);
+    khp_status s = drain(c);
+    c->report_open = false;
+    return s;
+}
+
+extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* out_rgb) {
+    khp_status s = check_params(c, p);
+    if (s != KHP_OK) return s;
+    HIPCHK(hipSetDevice(c->device));
+    const bool stats = (c->flags & KHP_CTX_STATS) != 0 || (p->flags & KHP_RENDER_STATS) != 0;
+    const bool async = (p->flags & KHP_RENDER_ASYNC) != 0;
+    if (async && (stats || (out_rgb && !(p->flags & KHP_RENDER_NO_READBACK))))
+        return fail(KHP_EINVAL, "KHP_RENDER_ASYNC renders take no readback and no instrumentation");
+    const size_t npix = (size_t)p->width * p->height;
+    uint32_t T = p->tile_size ? p->tile_size : 64;
+    uint32_t nranks = p->tile_nranks > 1 ? p->tile_nranks : 1;
+    uint32_t pkey[5] = {p->width, p->height, T, nranks > 1 ? p->tile_rank : 0u, nranks};
+    const bool geometry_change = c->fbW != p->width || c->fbH != p->height || !c->fb.p ||
+                                 memcmp(pkey, c->pix_key, sizeof(pkey)) != 0 || !c->pix.p;
+    if (!async || geometry_change) {  // a synchronous render (or new buffers) first completes the in-flight frames
+        s = drain(c);
+        if (s != KHP_OK) return s;
+        c->report_open = false;
+    }
+    if (!async) report_begin(c);
+    else if (!c->report_open) report_begin(c);
+    if (c->fbW != p->width || c->fbH != p->height || !c->fb.p) {
+        HIPCHK(c->fb.ensure(npix * 3 * sizeof(float)));
+        HIPCHK(hipMemsetAsync(c->fb.p, 0, npix * 3 * sizeof(float), c->stream));
+        c->fbW = p->width;
+        c->fbH = p->height;
+    }
+    s = prepare_pixels(c, p);
+    if (s != KHP_OK) return s;
+    if (geometry_change) HIPCHK(hipStreamSynchronize(c->stream));
+    const uint32_t P_all = (uint32_t)c->pix_host.size();
+    // Frames in flight: an asynchronous render takes the next frame slot (its
+    // own path sets and streams) and returns once enqueued; up to
+    // KHP_FRAMES_IN_FLIGHT frames then run at the same time, and one frame's
+    // bounce-by-bounce latency chain (each persistent launch waits for its
+    // slowest ray) overlaps the others' work.  The framebuffer is written in
+    // render order: each frame's accumulate waits for the previous framebuffer
+    // operation (accumulate or gather).
+    int F = KHP_FRAMES_IN_FLIGHT_DEFAULT;
+    if (const char* e = getenv("KHP_FRAMES_IN_FLIGHT")) F = atoi(e);
+    F = std::max(1, std::min(F, KHP_MAX_INFLIGHT));
+    const int slot = async ? (int)(c->frame_no % (uint64_t)F) : 0;
+    c->frame_no += async ? 1 : 0;
+    s = harvest(c, slot);  // the slot's previous frame (async series)
+    if (s != KHP_OK) return s;
+    FrameSlot& f = c->fs[slot];
+    f.ev_next = 0;
+    f.sync_next = 0;
+    f.launches.clear();
+    f.snaps.clear();
+    // Path sets ("sub-frames"): a frame's paths are cut into K independent
+    // sets, each with its own wavefront state and bounce pipeline on its own
+    // stream(s).  KHP_SPLIT=s (default): set k renders the sample range
+    // [spp*k/K, spp*(k+1)/K) of every owned pixel, i.e. K progressive passes;
+    // their accumulate kernels run in sample order, so KIRK's running mean is
+    // unchanged.  KHP_SPLIT=p: set k renders a contiguous range of the owned
+    // pixel list (whole 8x8 blocks), all samples.  With KHP_STAGGER=1 set k+1
+    // starts when set k's first extend launch has finished.  The frame is
+    // identical for every K; instrumented renders keep the same launch
+    // structure, serialised on one stream.
+    int K = KHP_SUBFRAMES_DEFAULT;
+    if (const char* e = getenv("KHP_SUBFRAMES")) K = atoi(e);
+    const char* split_env = getenv("KHP_SPLIT");
+    const bool split_pix = split_env && split_env[0] == 'p';
+    int stagger = KHP_STAGGER_DEFAULT;
+    if (const char* e = getenv("KHP_STAGGER")) stagger = atoi(e);
+    int set_streams = KHP_SET_STREAMS_DEFAULT;
+    if (const char* e = getenv("KHP_SET_STREAMS")) set_streams = atoi(e) >= 2 ? 2 : 1;
+    // Concurrent frames share the chip: each persistent launch of an async
+    // render takes 1/G of the resident grid (KHP_GRID_DIV, default F).
+    int G = async ? F : 1;
+    if (const char* e = getenv("KHP_GRID_DIV")) G = std::max(1, atoi(e));
+    const int grid_ext = std::max(1, c->grid_ext / G), grid_sh = std::max(1, c->grid_sh / G);
+    K = std::max(1, std::min(K, KHP_MAX_SUBFRAMES));
+    K = (int)std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)K, split_pix ? (P_all + 63) / 64 : p->spp));
+    f.K = K;
+    size_t cap_paths = (size_t)1 << 24;
+    if (const char* e = getenv("KHP_MAX_PATHS")) cap_paths = std::max<size_t>(4096, strtoull(e, nullptr, 10));
+    uint32_t pix_lo[KHP_MAX_SUBFRAMES + 1], spp_lo[KHP_MAX_SUBFRAMES + 1];
+    for (int k = 0; k <= K; ++k) {
+        if (split_pix) {
+            uint64_t b = (uint64_t)((P_all + 63) / 64) * (uint64_t)k / (uint64_t)K * 64u;
+            pix_lo[k] = (uint32_t)std::min<uint64_t>(b, P_all);
+            spp_lo[k] = k == 0 ? 0u : p->spp;
+        } else {
+            pix_lo[k] = k == 0 ? 0u : P_all;
+            spp_lo[k] = (uint32_t)((uint64_t)p->spp * (uint64_t)k / (uint64_t)K);
         }
     }
+    auto set_pix = [&](int k, uint32_t& lo, uint32_t& hi) {
+        lo = split_pix ? pix_lo[k] : 0u;
+        hi = split_pix ? pix_lo[k + 1] : P_all;
+    };
+    auto set_spp = [&](int k, uint32_t& lo, uint32_t& hi) {
+        lo = split_pix ? 0u : spp_lo[k];
+        hi = split_pix ? p->spp : spp_lo[k + 1];
+    };
+    uint32_t P_chunk[KHP_MAX_SUBFRAMES], S_chunk[KHP_MAX_SUBFRAMES];
+    for (int k = 0; k < K; ++k) {
+        uint32_t a, b, sa, sb;
+        set_pix(k, a, b);
+        set_spp(k, sa, sb);
+        const uint32_t Pk = std::max<uint32_t>(1, b - a), Sk = std::max<uint32_t>(1, sb - sa);
+        P_chunk[k] = (uint32_t)std::min<size_t>(Pk, cap_paths);
+        S_chunk[k] = (uint32_t)std::max<size_t>(1, std::min<size_t>(Sk, cap_paths / std::max<uint32_t>(P_chunk[k], 1)));
+        s = ensure_wave(c, c->ps[slot * KHP_MAX_SUBFRAMES + k], (size_t)P_chunk[k] * S_chunk[k]);
+        if (s != KHP_OK) return s;
+    }
+    const char* dump_env = getenv("KHP_DUMP_BOUNCE");
+    const int dump_b = dump_env ? atoi(dump_env) : -1;
+    if (stats) {
+        size_t chunks = 0;
+        for (int k = 0; k < K; ++k) {
+            uint32_t a, b, sa, sb;
+            set_pix(k, a, b);
+            set_spp(k, sa, sb);
+            chunks += (size_t)((b - a + P_chunk[k] - 1) / P_chunk[k]) * ((sb - sa + S_chunk[k] - 1) / S_chunk[k]);
+        }
+        HIPCHK(c->snap.ensure(std::max<size_t>(1, chunks * p->depth) * sizeof(Counters)));
+    }
+    // Per set, two streams: A runs generate / extend / shade / accumulate, B
+    // runs the shadow stage (k_shadow + k_shadow_finish) of bounce b while A
+    // already traverses bounce b+1, so each persistent kernel's tail fills with
+    // the other's blocks.  Ordering within a set: B(b) after shade(b) on A;
+    // shade(b+1) after B(b) (both update the path colour C in bounce order);
+    // the shadow queue of bounce b+2 reuses parity b's buffers only after
+    // shade(b+1), which already waited for B(b).  Instrumented renders run
+    // everything on the context stream so the per-bounce snapshots are exact.
+    const bool overlap = !stats && !getenv("KHP_NO_OVERLAP");
+    c->cur_bounce = -1;
+    f.ev_start = slot_event(f.ev_pool, f.ev_next, false);
+    (void)hipEventRecord(f.ev_start, c->stream);
+    // Fork from the context stream (framebuffer clears, pixel-list uploads) --
+    // not for an asynchronous frame: the context stream also carries the joins
+    // of the frames still in flight, and waiting on it would serialise them.
+    hipEvent_t e_fork = nullptr;
+    if (!async || geometry_change) {
+        e_fork = slot_event(f.sync_pool, f.sync_next, true);
+        HIPCHK(hipEventRecord(e_fork, c->stream));
+    }
+    hipEvent_t prev_started = nullptr;  // KHP_STAGGER: the previous set's first extend launch finished
+    hipEvent_t prev_acc = c->fb_evt;    // the previous framebuffer operation (this set's accumulate waits for it)
+    std::vector<hipEvent_t> set_end;
+    for (int k = 0; k < K; ++k) {
+        PathSet& w = c->ps[slot * KHP_MAX_SUBFRAMES + k];
+        hipStream_t sA = overlap ? w.sA : c->stream;
+        hipStream_t sB = overlap ? (set_streams >= 2 ? w.sB : w.sA) : c->stream;
+        if (e_fork && sA != c->stream) HIPCHK(hipStreamWaitEvent(sA, e_fork, 0));
+        if (e_fork && sB != sA && sB != c->stream) HIPCHK(hipStreamWaitEvent(sB, e_fork, 0));
+        if (overlap && prev_started) {
+            HIPCHK(hipStreamWaitEvent(sA, prev_started, 0));
+            if (sB != sA) HIPCHK(hipStreamWaitEvent(sB, prev_started, 0));
+        }
+        prev_started = nullptr;
+        HIPCHK(hipMemsetAsync(w.cnt.p, 0, sizeof(Counters), sA));
+        HIPCHK(hipMemsetAsync(w.shqb.p, 0, 2 * sizeof(ShadowQ), sA));
+        if (sB != sA) {
+            hipEvent_t z = slot_event(f.sync_pool, f.sync_next, true);
+            HIPCHK(hipEventRecord(z, sA));
+            HIPCHK(hipStreamWaitEvent(sB, z, 0));
+        }
+        uint32_t set_p0, set_p1, set_s0, set_s1;
+        set_pix(k, set_p0, set_p1);
+        set_spp(k, set_s0, set_s1);
+        bool acc_waited = false;
+        Wave Wv = wave_view(w);
+        Wv.pix = c->pix.as<uint32_t>();
+        Wv.W = p->width;
+        Wv.H = p->height;
+        Wv.seed = p->seed;
+        Wv.depth = p->depth;
+        SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
+        SpillArea sp_sh{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
+        for (uint32_t p0 = set_p0; p0 < set_p1; p0 += P_chunk[k]) {
+            uint32_t P = std::min(P_chunk[k], set_p1 - p0);
+            for (uint32_t s0 = set_s0; s0 < set_s1; s0 += S_chunk[k]) {
+                uint32_t ns = std::min(S_chunk[k], set_s1 - s0);
+                Wv.P = P;
+                Wv.p_off = p0;
+                Wv.sample0 = p->first_sample + s0;
+                Wv.n_samples = ns;
+                uint32_t npaths = P * ns;
+                timed(c, f, 3, true, sA);
+                hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wv);
+                timed(c, f, 3, false, sA);
+                hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
+                for (uint32_t b = 0; b < p->depth; ++b) {
+                    int cur = b & 1;
+                    const int par = b & 1;
+                    c->cur_bounce = (int)b;
+                    Wave Wb = Wv;
+                    Wb.sh = w.shb[par].as<float4>();
+                    Wb.vis = w.visb[par].as<uint8_t>();
+                    Wb.shq = w.shqb.as<ShadowQ>() + par;
+                    if (dump_b == (int)b && k == 0) {
+                        uint32_t nq = 0;
+                        HIPCHK(hipMemcpyAsync(&nq, &Wv.cnt->nq[cur], 4, hipMemcpyDeviceToHost, sA));
+                        HIPCHK(hipStreamSynchronize(sA));
+                        c->dump.resize(6 * (size_t)nq);
+                        for (int q = 0; q < 3; ++q) {
+                            HIPCHK(hipMemcpy(c->dump.data() + (size_t)q * nq, Wv.qo[cur][q], 4 * (size_t)nq, hipMemcpyDeviceToHost));
+                            HIPCHK(hipMemcpy(c->dump.data() + (size_t)(3 + q) * nq, Wv.qd[cur][q], 4 * (size_t)nq, hipMemcpyDeviceToHost));
+                        }
+                    }
+                    hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
+                    timed(c, f, 0, true, sA);
+                    if (stats)
+                        hipLaunchKernelGGL(k_extend<true>, dim3(grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                    else
+                        hipLaunchKernelGGL(k_extend<false>, dim3(grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                    timed(c, f, 0, false, sA);
+                    if (overlap && stagger && k + 1 < K && !prev_started) {
+                        prev_started = slot_event(f.sync_pool, f.sync_next, true);
+                        HIPCHK(hipEventRecord(prev_started, sA));
+                    }
+                    if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
+                    timed(c, f, 1, true, sA);
+                    hipLaunchKernelGGL(k_shade, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                    timed(c, f, 1, false, sA);
+                    if (sB != sA) {
+                        hipEvent_t shaded = slot_event(f.sync_pool, f.sync_next, true);
+                        HIPCHK(hipEventRecord(shaded, sA));
+                        HIPCHK(hipStreamWaitEvent(sB, shaded, 0));
+                    }
+                    timed(c, f, 2, true, sB);
+                    if (stats)
+                        hipLaunchKernelGGL(k_shadow<true>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES_SH, sB, c->S, Wb, sp_sh);
+                    else
+                        hipLaunchKernelGGL(k_shadow<false>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES_SH, sB, c->S, Wb, sp_sh);
+                    timed(c, f, 2, false, sB);
+                    timed(c, f, 2, true, sB);   // shadow stage = any-hit traversal + finish
+                    hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
+                    timed(c, f, 2, false, sB);
+                    if (sB != sA) {
+                        done_b = slot_event(f.sync_pool, f.sync_next, true);
+                        HIPCHK(hipEventRecord(done_b, sB));
+                    }
+                    if (stats) {
+                        HIPCHK(hipMemcpyAsync(c->snap.as<Counters>() + f.snaps.size(), w.cnt.p, sizeof(Counters),
+                                              hipMemcpyDeviceToDevice, sA));
+                        f.snaps.push_back(Snap{k, b});
+                    }
+                }
+                c->cur_bounce = -1;
+                if (done_b) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
+                if (prev_acc && !acc_waited) {  // framebuffer order: previous frame / previous sample set
+                    HIPCHK(hipStreamWaitEvent(sA, prev_acc, 0));
+                    acc_waited = true;
+                }
+                timed(c, f, 3, true, sA);
+                hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, c->fb.as<float>());
+                timed(c, f, 3, false, sA);
+                if (sB != sA) {  // the next chunk's shadow stages come after this chunk's accumulate
+                    hipEvent_t acc = slot_event(f.sync_pool, f.sync_next, true);
+                    HIPCHK(hipEventRecord(acc, sA));
+                    HIPCHK(hipStreamWaitEvent(sB, acc, 0));
+                }
+            }
+        }
+        hipEvent_t e_end = slot_event(f.sync_pool, f.sync_next, true);
+        HIPCHK(hipEventRecord(e_end, sA));
+        set_end.push_back(e_end);
+        if (!split_pix) prev_acc = e_end;  // sample split: the next set accumulates after this one
+    }
+    // join: the frame is done when every set has accumulated
+    for (hipEvent_t e : set_end) HIPCHK(hipStreamWaitEvent(c->stream, e, 0));
+    f.done_t = slot_event(f.ev_pool, f.ev_next, false);
+    (void)hipEventRecord(f.done_t, c->stream);
+    f.done = slot_event(f.sync_pool, f.sync_next, true);
+    HIPCHK(hipEventRecord(f.done, c->stream));
+    c->fb_evt = f.done;
+    f.inflight = true;
+    HIPCHK(hipGetLastError());
+    if (async) return KHP_OK;
+    if (out_rgb && !(p->flags & KHP_RENDER_NO_READBACK)) {
+        hipMemcpyKind kind = (p->flags & KHP_RENDER_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        HIPCHK(hipMemcpyAsync(out_rgb, c->fb.p, npix * 3 * sizeof(float), kind, c->stream));
+    }
+    s = harvest(c, slot);
+    if (s != KHP_OK) return s;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->report_open = false;
     return KHP_OK;
 }
 
@@ -1652,6 +1964,10 @@ extern "C" void khp_tonemap_defaults(khp_tonemap* t) {
 }
 
 extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t* out_rgba) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || !out_rgba) return fail(KHP_EINVAL, "null argument");
     if (!c->fb.p) return fail(KHP_ENOTREADY, "nothing rendered yet");
     HIPCHK(hipSetDevice(c->device));
@@ -1755,6 +2071,10 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
 
 extern "C" khp_status khp_read_bvh(khp_ctx* c, uint32_t* n_nodes, uint32_t* depth, float* node_boxes,
                                    int32_t* node_first, int32_t* node_count, int32_t* object_ids) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || !n_nodes) return fail(KHP_EINVAL, "ctx or n_nodes is null");
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
     HostScene& hs = c->hs;
@@ -1782,6 +2102,10 @@ extern "C" khp_status khp_read_bvh(khp_ctx* c, uint32_t* n_nodes, uint32_t* dept
 
 extern "C" khp_status khp_read_layout(khp_ctx* c, uint32_t* n_records, uint32_t* n_slots, void* node_records,
                                       float* prim_records, uint32_t* prim_aux) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || !n_records || !n_slots) return fail(KHP_EINVAL, "null argument");
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
     HIPCHK(hipSetDevice(c->device));
@@ -1799,6 +2123,10 @@ extern "C" khp_status khp_read_layout(khp_ctx* c, uint32_t* n_records, uint32_t*
 }
 
 extern "C" khp_status khp_debug_queue(khp_ctx* c, uint32_t* n, float* orig, float* dir) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || !n) return fail(KHP_EINVAL, "null argument");
     const uint32_t m = (uint32_t)(c->dump.size() / 6);
     if (orig && dir) {
@@ -1813,6 +2141,10 @@ extern "C" khp_status khp_debug_queue(khp_ctx* c, uint32_t* n, float* orig, floa
 }
 
 extern "C" khp_status khp_read_framebuffer(khp_ctx* c, float* out_rgb) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || !out_rgb) return fail(KHP_EINVAL, "null argument");
     if (!c->fb.p) return fail(KHP_ENOTREADY, "nothing rendered yet");
     HIPCHK(hipSetDevice(c->device));
@@ -1865,31 +2197,32 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
                                        const float* tmax_h, float* t_out, int32_t* obj_out, float* uv_out,
                                        uint8_t* hit_out) {
     const bool shadow = hit_out != nullptr;
-    khp_status s = ensure_wave(c, n);
+    PathSet& w = c->ps[0];
+    khp_status s = ensure_wave(c, w, n);
     if (s != KHP_OK) return s;
     DevMem o, d, tm, t, ob, uv;
     HIPCHK(upload(o, orig, 3 * (size_t)n, c->stream));
     HIPCHK(upload(d, dir, 3 * (size_t)n, c->stream));
     if (shadow) HIPCHK(upload(tm, tmax_h, (size_t)n, c->stream));
-    HIPCHK(hipMemsetAsync(c->cnt.p, 0, sizeof(Counters), c->stream));
-    HIPCHK(hipMemsetAsync(c->shqb.p, 0, 2 * sizeof(ShadowQ), c->stream));
-    Wave Wv = wave_view(c);
+    HIPCHK(hipMemsetAsync(w.cnt.p, 0, sizeof(Counters), c->stream));
+    HIPCHK(hipMemsetAsync(w.shqb.p, 0, 2 * sizeof(ShadowQ), c->stream));
+    Wave Wv = wave_view(w);
     hipLaunchKernelGGL(k_load_rays, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, o.as<float>(), d.as<float>(),
                        Wv, shadow ? 1 : 0, tm.as<float>());
     const bool prod = trace_persistent() == 2;
     hipEvent_t e0 = next_event(c), e1 = next_event(c);
     (void)hipEventRecord(e0, c->stream);
     if (shadow) {
-        SpillArea sp{c->spill_sh.as<int4>(), (uint32_t)c->grid_sh * 256u};
-        if (prod) hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, c->stream, c->S, Wv, sp);
-        else hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(256), LDS_BYTES_SH, c->stream, c->S, Wv, sp);
+        SpillArea sp{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
+        if (prod) hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(TRAV_BLOCK), LDS_BYTES_SH, c->stream, c->S, Wv, sp);
+        else hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(TRAV_BLOCK), LDS_BYTES_SH, c->stream, c->S, Wv, sp);
         (void)hipEventRecord(e1, c->stream);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(hit_out, Wv.vis, n, hipMemcpyDeviceToHost, c->stream));
     } else {
-        SpillArea sp{c->spill.as<int4>(), (uint32_t)c->grid_ext * 256u};
-        if (prod) hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(256), LDS_BYTES, c->stream, c->S, Wv, 0, sp);
-        else hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(256), LDS_BYTES, c->stream, c->S, Wv, 0, sp);
+        SpillArea sp{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
+        if (prod) hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, c->stream, c->S, Wv, 0, sp);
+        else hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, c->stream, c->S, Wv, 0, sp);
         (void)hipEventRecord(e1, c->stream);
         HIPCHK(t.ensure(4 * (size_t)n));
         HIPCHK(ob.ensure(4 * (size_t)n));
@@ -1902,7 +2235,7 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
         if (uv_out) HIPCHK(hipMemcpyAsync(uv_out, uv.p, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
     }
     Counters hc;
-    HIPCHK(hipMemcpyAsync(&hc, c->cnt.p, sizeof(hc), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&hc, w.cnt.p, sizeof(hc), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->st.node_visits = shadow ? hc.sh_node_visits : hc.node_visits;
     c->st.prim_tests = shadow ? hc.sh_prim_tests : hc.prim_tests;
@@ -1916,6 +2249,10 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
 
 extern "C" khp_status khp_trace_closest(khp_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out,
                                         int32_t* obj_out, float* uv_out) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || (n && (!orig || !dir || !t_out || !obj_out))) return fail(KHP_EINVAL, "null argument");
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
     if (n == 0) return KHP_OK;
@@ -1946,6 +2283,10 @@ extern "C" khp_status khp_trace_closest(khp_ctx* c, uint32_t n, const float* ori
 
 extern "C" khp_status khp_trace_any(khp_ctx* c, uint32_t n, const float* orig, const float* dir, const float* tmax,
                                     uint8_t* hit_out) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || (n && (!orig || !dir || !tmax || !hit_out))) return fail(KHP_EINVAL, "null argument");
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
     if (n == 0) return KHP_OK;
@@ -1987,6 +2328,10 @@ extern "C" khp_status khp_comm_unique_id(uint8_t out_id[128]) {
 }
 
 extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint8_t id[128]) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(KHP_EINVAL, "bad comm arguments");
     HIPCHK(hipSetDevice(c->device));
     ncclUniqueId uid;
@@ -2027,12 +2372,19 @@ extern "C" khp_status khp_gather_framebuffer(khp_ctx* c, const khp_render_params
         HIPCHK(hipStreamSynchronize(c->stream));
         memcpy(c->gather_key, key, sizeof(key));
     }
+    // Enqueued on the context stream, which already carries the last frame's
+    // join, and not waited for: the next frame's accumulate waits for this
+    // gather through fb_evt, and any synchronous call completes it.
+    if (!c->gather_evt) HIPCHK(hipEventCreateWithFlags(&c->gather_evt, hipEventDisableTiming));
+    if (c->fb_evt) HIPCHK(hipStreamWaitEvent(c->stream, c->fb_evt, 0));
     if (c->rank != root) {
         uint32_t P = (uint32_t)c->gather_counts[c->rank];
         if (P) hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
                                   c->stage_pix.as<uint32_t>(), P, c->stage.as<float>());
         NCCLCHK(ncclSend(c->stage.p, (size_t)P * 3, ncclFloat32, root, c->comm, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->gather_evt, c->stream));
+        c->fb_evt = c->gather_evt;
         return KHP_OK;
     }
     // root: receive every other rank's pixels (one grouped recv), then scatter them into the framebuffer
@@ -2049,6 +2401,7 @@ extern "C" khp_status khp_gather_framebuffer(khp_ctx* c, const khp_render_params
         hipLaunchKernelGGL(k_unpack, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, c->stream,
                            c->fb.as<float>(), c->stage_pix.as<uint32_t>(), (uint32_t)total, c->stage.as<float>());
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventRecord(c->gather_evt, c->stream));
+    c->fb_evt = c->gather_evt;
     return KHP_OK;
 }

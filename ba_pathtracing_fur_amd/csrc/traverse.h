@@ -59,7 +59,17 @@ struct PrivStack {
     }
 };
 
-// The LDS image is three [R][256] arrays (ref, tmin bits, tmax bits) at the
+// Threads per block of the persistent traversal kernels.  One wave per block:
+// a block's LDS is released only when all of its waves have ended, so with
+// 4-wave blocks a launch's tail (a few long rays scattered over many blocks)
+// kept most of the chip's LDS allocated and no other kernel could start
+// there; with 1-wave blocks each finished wave frees its share at once.
+#ifndef KHP_TRAV_BLOCK
+#define KHP_TRAV_BLOCK 64
+#endif
+constexpr uint32_t TRAV_BLOCK = KHP_TRAV_BLOCK;
+
+// The LDS image is three [R][TRAV_BLOCK] arrays (ref, tmin bits, tmax bits) at the
 // start of the kernel's dynamic LDS; a lane's column starts at its threadIdx.x.
 // The spill area is [STACK_MAX][grid lanes] int4, addressed from blockIdx /
 // threadIdx only on the (rare) spill path, so it costs no registers.
@@ -80,21 +90,21 @@ struct LdsStack {
     }
     __device__ __forceinline__ void clear() { sp = lo = 0; }
     __device__ __forceinline__ bool empty() const { return sp == 0; }
-    __device__ __forceinline__ uint32_t slot(int e) const { return (uint32_t)((uint32_t)e % (uint32_t)R) * 256u + threadIdx.x; }
+    __device__ __forceinline__ uint32_t slot(int e) const { return (uint32_t)((uint32_t)e % (uint32_t)R) * TRAV_BLOCK + threadIdx.x; }
     __device__ __forceinline__ int4* gcell(int e) const {
         return spill + (size_t)e * stride + blockIdx.x * blockDim.x + threadIdx.x;
     }
     __device__ __forceinline__ void push(uint32_t r, float a, float b) {
         if (sp - lo == R) {  // ring full: move the oldest entry to the spill column
             uint32_t k = slot(lo);
-            *gcell(lo) = make_int4((int)lds[k], (int)lds[k + R * 256], (int)lds[k + 2 * R * 256], 0);
+            *gcell(lo) = make_int4((int)lds[k], (int)lds[k + R * TRAV_BLOCK], (int)lds[k + 2 * R * TRAV_BLOCK], 0);
             ++lo;
             if (COUNT) ++spills;
         }
         uint32_t k = slot(sp);
         lds[k] = r;
-        lds[k + R * 256] = bits_from_f(a);
-        lds[k + 2 * R * 256] = bits_from_f(b);
+        lds[k + R * TRAV_BLOCK] = bits_from_f(a);
+        lds[k + 2 * R * TRAV_BLOCK] = bits_from_f(b);
         ++sp;
     }
     // The ring slot is read unconditionally (a stale but harmless slot when
@@ -106,8 +116,8 @@ struct LdsStack {
         --sp;
         const uint32_t k = slot(sp);
         r = lds[k];
-        a = f_from_bits(lds[k + R * 256]);
-        b = f_from_bits(lds[k + 2 * R * 256]);
+        a = f_from_bits(lds[k + R * TRAV_BLOCK]);
+        b = f_from_bits(lds[k + 2 * R * TRAV_BLOCK]);
         asm volatile("" : "+v"(r), "+v"(a), "+v"(b));  // the LDS reads happen here
         if (sp < lo) {
             int4 e = *gcell(sp);
@@ -150,7 +160,7 @@ struct LdsStackT {
         clean = false;
     }
     __device__ __forceinline__ bool empty() const { return sp == 0; }
-    __device__ __forceinline__ uint32_t slot(int e) const { return (uint32_t)(e & (R - 1)) * 256u + threadIdx.x; }
+    __device__ __forceinline__ uint32_t slot(int e) const { return (uint32_t)(e & (R - 1)) * TRAV_BLOCK + threadIdx.x; }
     __device__ __forceinline__ int4* gcell(int e) const {
         return spill + (size_t)e * stride + blockIdx.x * blockDim.x + threadIdx.x;
     }
@@ -159,14 +169,14 @@ struct LdsStackT {
             const int e = sp - 1;
             if (e - lo == R) {  // ring full: the oldest ring entry goes to the spill column
                 uint32_t k = slot(lo);
-                *gcell(lo) = make_int4((int)lds[k], (int)lds[k + R * 256], (int)lds[k + 2 * R * 256], 0);
+                *gcell(lo) = make_int4((int)lds[k], (int)lds[k + R * TRAV_BLOCK], (int)lds[k + 2 * R * TRAV_BLOCK], 0);
                 ++lo;
                 if (COUNT) ++spills;
             }
             uint32_t k = slot(e);
             lds[k] = tr;
-            lds[k + R * 256] = bits_from_f(ta);
-            lds[k + 2 * R * 256] = bits_from_f(tb);
+            lds[k + R * TRAV_BLOCK] = bits_from_f(ta);
+            lds[k + 2 * R * TRAV_BLOCK] = bits_from_f(tb);
         }
         tr = r;
         ta = a;
@@ -184,8 +194,8 @@ struct LdsStackT {
             if (e >= lo) {
                 uint32_t k = slot(e);
                 tr = lds[k];
-                ta = f_from_bits(lds[k + R * 256]);
-                tb = f_from_bits(lds[k + 2 * R * 256]);
+                ta = f_from_bits(lds[k + R * TRAV_BLOCK]);
+                tb = f_from_bits(lds[k + 2 * R * TRAV_BLOCK]);
                 clean = true;
             } else {
                 int4 v = *gcell(e);
@@ -790,9 +800,30 @@ __device__ __forceinline__ bool trav2_begin(const DevScene& S, const TravRay& tr
 // One wave iteration of one lane (mode != M_IDLE).  ANY: any-hit with the
 // fixed limit tlimit = the ray's tMax; else closest hit, tlimit = h.t.
 // Returns true when the ray is finished; for ANY, `occluded` tells the result.
+// Tail prefetch (KHP_TAIL_PF): once a launch's queue is drained, the few
+// rays still running decide its duration, and each of their iterations waits
+// a full HBM round trip for the record it fetches.  In that phase the memory
+// system is idle, so as soon as an interior record's child boxes are tested,
+// the lines of the children that will be visited (the near one next
+// iteration, the pushed far one later) are requested with plain dword loads
+// whose results are discarded (`tail_pf` set by the caller, wave-uniform).
+// The loaded registers stay live until the next fetch has been waited for;
+// vmcnt retires loads in order, so they cannot be reused while in flight.
+// Exactness is unaffected: nothing reads the prefetched values.
+#ifndef KHP_TAIL_PF
+#define KHP_TAIL_PF 1
+#endif
+#ifndef KHP_TAIL_PF_LANES
+#define KHP_TAIL_PF_LANES 64   // prefetch when the queue is drained and at most this many lanes are busy
+#endif
+__device__ __forceinline__ void pf_line(const DevScene& S, uint32_t ref, float& d) {
+    asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(child_line(S, ref)) : "memory");
+}
+
 template <bool ANY, bool STATS, class Stack>
 __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
-                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
+                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded,
+                                      bool tail_pf, Prefetch& pf) {
     const bool in_leaf = mode == M_LEAF;
     const bool fetch = in_leaf || mode == M_NODE;
     const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
@@ -804,6 +835,9 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
         q3 = p[3];
         pin(q0); pin(q1); pin(q2); pin(q3);
     }
+#if KHP_TAIL_PF
+    asm volatile("" : "+v"(pf.d0), "+v"(pf.d1));  // prefetches issued last iteration are complete here
+#endif
     bool need_pop = mode == M_POP;
     bool have = false;  // a new entry (ref, t0, t1) for take_entry
     uint32_t eref = 0u;
@@ -851,6 +885,12 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
         pref = nearl ? rref : lref;
         pt0 = nearl ? r0 : l0;
         pt1 = nearl ? r1 : l1;
+#if KHP_TAIL_PF
+        if (tail_pf) {
+            if (have) pf_line(S, eref, pf.d0);
+            if (push) pf_line(S, pref, pf.d1);
+        }
+#endif
     }
     if (push) stk.push(pref, pt0, pt1);
     if (need_pop) {

@@ -29,6 +29,7 @@ LIGHT_POINT, LIGHT_QUAD, LIGHT_SPOT, LIGHT_SUN = 0, 1, 2, 3
 RENDER_OUT_DEVICE = 1 << 0
 RENDER_NO_READBACK = 1 << 1
 RENDER_STATS = 1 << 2
+RENDER_ASYNC = 1 << 3
 CTX_STATS = 1 << 0
 CTX_HOST_BUILD = 1 << 1
 
@@ -81,10 +82,11 @@ class Stats(ctypes.Structure):
                 ("bounce_extend_ms", c_double * 16), ("bounce_shadow_ms", c_double * 16),
                 ("bounce_wave_iters", c_uint64 * 16), ("bounce_lanes_busy", c_uint64 * 16),
                 ("bounce_shadow_wave_iters", c_uint64 * 16), ("bounce_shadow_lanes_busy", c_uint64 * 16),
-                ("step_cycles", c_uint64 * 4), ("bvh_on_device", c_uint32), ("pad0", c_uint32),
+                ("step_cycles", c_uint64 * 4), ("bvh_on_device", c_uint32), ("subframes", c_uint32),
                 ("flatten_ms", c_double), ("bvh_ms", c_double), ("bvh_kernel_ms", c_double), ("layout_ms", c_double),
                 ("flatten_kernel_ms", c_double), ("layout_kernel_ms", c_double),
-                ("extend_pruned_pops", c_uint64), ("shadow_pruned_pops", c_uint64)]
+                ("extend_pruned_pops", c_uint64), ("shadow_pruned_pops", c_uint64), ("frames", c_uint64),
+                ("extend_busy_ms", c_double)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if not isinstance(getattr(self, k), (int, float)) else getattr(self, k))
@@ -116,7 +118,8 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_gen_hairball", "khp_gen_icosphere", "khp_gen_torus", "khp_host_build", "khp_debug_queue",
             "khp_read_rgba8", "khp_tonemap_defaults", "khp_read_bvh",
             "khp_read_layout", "khp_set_scene_device", "khp_gen_hairball_device", "khp_device_alloc",
-            "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device"]
+            "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device",
+            "khp_sync"]
 
 _lib = None
 
@@ -147,6 +150,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_set_scene": (c_int, [c_void_p, P(SceneDesc)]),
         "khp_build_accel": (c_int, [c_void_p]),
         "khp_render": (c_int, [c_void_p, P(RenderParams), c_void_p]),
+        "khp_sync": (c_int, [c_void_p]),
         "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
         "khp_read_rgba8": (c_int, [c_void_p, P(Tonemap), P(c_uint8)]),
         "khp_tonemap_defaults": (None, [P(Tonemap)]),

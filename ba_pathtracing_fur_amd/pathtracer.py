@@ -159,14 +159,24 @@ class HipContext:
         N.check(self.lib, self.lib.khp_build_accel(self.ptr), "khp_build_accel")
 
     def render(self, width, height, spp, depth, seed=0x4B49524B, first_sample=0, tile_size=64, tile_rank=0,
-               tile_nranks=1, out: np.ndarray | None = None, readback=True, stats=False) -> np.ndarray | None:
-        flags = (0 if readback else N.RENDER_NO_READBACK) | (N.RENDER_STATS if stats else 0)
+               tile_nranks=1, out: np.ndarray | None = None, readback=True, stats=False,
+               async_: bool = False) -> np.ndarray | None:
+        """khp_render.  async_=True (no readback, no stats) enqueues the frame and
+        returns at once; frames in flight overlap; sync() completes them."""
+        if async_:
+            readback = False
+        flags = ((0 if readback else N.RENDER_NO_READBACK) | (N.RENDER_STATS if stats else 0) |
+                 (N.RENDER_ASYNC if async_ else 0))
         p = N.RenderParams(width, height, spp, depth, seed, first_sample, tile_size, tile_rank, tile_nranks, flags)
         if readback and out is None:
             out = np.zeros((height, width, 3), np.float32)
         ptr = out.ctypes.data_as(ctypes.c_void_p) if (readback and out is not None) else None
         N.check(self.lib, self.lib.khp_render(self.ptr, ctypes.byref(p), ptr), "khp_render")
         return out
+
+    def sync(self):
+        """khp_sync: complete every asynchronous frame; stats() then sums them."""
+        N.check(self.lib, self.lib.khp_sync(self.ptr), "khp_sync")
 
     def read_bvh(self) -> dict:
         """The tree khp_build_accel built (khp_read_bvh), in khp_host_build's layout."""

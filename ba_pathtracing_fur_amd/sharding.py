@@ -67,12 +67,20 @@ class ShardedFrame:
             dist.broadcast_object_list(obj, src=root)
             ctx.comm_init(world, rank, obj[0])
 
-    def render(self, width, height, spp, depth, seed=0x4B49524B, first_sample=0, stats=False, gather=True):
-        """One frame (or a progressive slice of samples) of this rank's tiles, framebuffer left in HBM."""
+    def render(self, width, height, spp, depth, seed=0x4B49524B, first_sample=0, stats=False, gather=True,
+               async_=False):
+        """One frame (or a progressive slice of samples) of this rank's tiles, framebuffer left in HBM.
+
+        async_=True enqueues the frame and its gather without waiting (frames in
+        flight overlap on the device); sync() completes them."""
         self.ctx.render(width, height, spp, depth, seed=seed, first_sample=first_sample, tile_size=self.tile,
-                        tile_rank=self.rank, tile_nranks=self.world, readback=False, stats=stats)
+                        tile_rank=self.rank, tile_nranks=self.world, readback=False, stats=stats,
+                        async_=async_ and not stats)
         if gather and self.world > 1:
             self.ctx.gather_framebuffer(width, height, spp, depth, self.tile, self.world, self.rank, self.root)
+
+    def sync(self):
+        self.ctx.sync()
 
     def barrier(self):
         if self.dist is not None and self.world > 1:

@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sync-steps", action="store_true",
+                    help="wait for each frame before the next (no frame pipelining)")
     ap.add_argument("--host-scene", action="store_true",
                     help="generate + flatten + build on the host (the pre-(f)1/(f)2 path) instead of in HBM")
     return ap.parse_args()
@@ -150,28 +152,44 @@ def main():
         log(f"scene: {n_objects} objects, gen+flatten {gen_s:.3f}s, BVH+layout {build_s:.3f}s "
             f"({setup}), depth {st0['bvh_depth']}, nodes {st0['n_nodes']}, HBM {st0['device_bytes'] / 1e9:.2f} GB")
     frame = ShardedFrame(ctx, rank, world, dist, tile=args.tile)
+    ext_ms_acc = []
+
+    pipelined = not args.sync_steps
 
     def step(stats=False):
-        frame.render(W, H, spp, depth, stats=stats)
+        # pipelined (default): the frame and its gather are enqueued and the next
+        # step starts at once, so consecutive frames overlap on the device (each
+        # frame alone is a chain of 2 x depth persistent launches that each wait
+        # for their slowest ray); frames still complete and accumulate in order.
+        frame.render(W, H, spp, depth, stats=stats, async_=pipelined and not stats)
 
     for _ in range(args.warmup):
         step()
+    frame.sync()
     # one instrumented frame (outside the timed region): exact visit counts
     step(stats=True)
     cnt = ctx.stats()
 
-    ext_ms = 0.0
-    ext_launches = 0
+    frame.sync()
     frame.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        s = ctx.stats()
-        ext_ms += s["extend_ms"]
-        ext_launches += s["extend_launches"]
+        if not pipelined:
+            s = ctx.stats()
+            ext_ms_acc.append((s["extend_ms"], s["extend_launches"], s["extend_busy_ms"]))
+    frame.sync()   # every frame and gather of the timed region is complete
     frame.barrier()
     elapsed = frame.max_over_ranks(time.perf_counter() - t0)
-    last = ctx.stats()
+    last = ctx.stats()   # pipelined: sums over the timed frames (khp_sync report)
+    if pipelined:
+        ext_ms, ext_launches, busy_ms = last["extend_ms"], last["extend_launches"], last["extend_busy_ms"]
+        nfr = max(1, last["frames"])
+    else:
+        ext_ms = sum(a for a, _, _ in ext_ms_acc)
+        ext_launches = sum(b for _, b, _ in ext_ms_acc)
+        busy_ms = sum(c for _, _, c in ext_ms_acc)
+        nfr = 1
     samples_per_step = W * H * spp
     value = args.steps * samples_per_step / elapsed / 1e6
     # roofline of the extend kernel (this rank's launches)
@@ -180,7 +198,15 @@ def main():
     launches_frame = max(1, cnt["extend_launches"])
     avg_launch_ms = ext_ms / max(1, ext_launches)
     bytes_per_launch = alg_bytes_frame / launches_frame
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    per_launch = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    # Pipelined frames run two frames' launches side by side, so a launch's own
+    # duration also counts time the chip spent on the other frame.  `achieved`
+    # divides the algorithmic bytes of every timed k_extend launch by the time
+    # during which at least one of them was running (union of their HIP-event
+    # intervals, khp_stats.extend_busy_ms); without overlap (--sync-steps) the
+    # union is the sum of the launch durations and this is bytes/launch over
+    # the average launch duration.
+    achieved = (bytes_per_launch * ext_launches) / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
     traffic = pmc_traffic()
     out = {
         "metric": "Msamples/s at 1080p 8spp, 1M-strand hairball; achieved HBM GB/s vs peak",
@@ -211,28 +237,34 @@ def main():
             "traffic": traffic,
             "bytes_per_launch": int(bytes_per_launch),
             "avg_launch_ms": round(avg_launch_ms, 4),
+            "achieved_per_launch": round(per_launch, 1),
+            "extend_busy_ms_per_frame": round(busy_ms / max(1, nfr if pipelined else args.steps), 3),
+            "achieved_def": "algorithmic bytes of all timed k_extend launches / union of their HIP-event "
+                            "intervals (= bytes per launch / avg launch duration when launches do not overlap)",
             "per_ray": {"nodes": round(cnt["node_visits"] / max(1, rays), 2),
                         "prims": round(cnt["prim_tests"] / max(1, rays), 2)},
         },
         "frame": {
             "extend_rays": rays, "shadow_rays": cnt["shadow_rays"],
-            "extend_ms": round(last["extend_ms"], 3), "shade_ms": round(last["shade_ms"], 3),
-            "shadow_ms": round(last["shadow_ms"], 3), "other_ms": round(last["other_ms"], 3),
-            "device_ms": round(last["render_ms"], 3),
+            "extend_ms": round(last["extend_ms"] / nfr, 3), "shade_ms": round(last["shade_ms"] / nfr, 3),
+            "shadow_ms": round(last["shadow_ms"] / nfr, 3), "other_ms": round(last["other_ms"] / nfr, 3),
+            "device_ms": round(last["render_ms"] / nfr, 3),
             "shadow_nodes_per_ray": round(cnt["shadow_node_visits"] / max(1, cnt["shadow_rays"]), 2),
             "stack_spills_per_ray": round(cnt["stack_spills"] / max(1, rays + cnt["shadow_rays"]), 4),
             "pruned_pops_per_ray": round(cnt["extend_pruned_pops"] / max(1, rays), 3),
             "shadow_pruned_pops_per_ray": round(cnt["shadow_pruned_pops"] / max(1, cnt["shadow_rays"]), 3),
+            "subframes": last.get("subframes"),
+            "pipelined": pipelined, "frames_in_flight": int(os.environ.get("KHP_FRAMES_IN_FLIGHT", "2")) if pipelined else 1,
             "build_s": round(build_s, 3),
             "setup": setup,
             "per_bounce": [
                 {"bounce": b, "rays": cnt["bounce_rays"][b],
                  "nodes_per_ray": round(cnt["bounce_nodes"][b] / max(1, cnt["bounce_rays"][b]), 2),
                  "prims_per_ray": round(cnt["bounce_prims"][b] / max(1, cnt["bounce_rays"][b]), 2),
-                 "extend_ms": round(last["bounce_extend_ms"][b], 3),
+                 "extend_ms": round(last["bounce_extend_ms"][b] / nfr, 3),
                  "shadow_rays": cnt["bounce_shadow_rays"][b],
                  "shadow_nodes_per_ray": round(cnt["bounce_shadow_nodes"][b] / max(1, cnt["bounce_shadow_rays"][b]), 2),
-                 "shadow_ms": round(last["bounce_shadow_ms"][b], 3),
+                 "shadow_ms": round(last["bounce_shadow_ms"][b] / nfr, 3),
                  "wave_iters": cnt["bounce_wave_iters"][b],
                  "lane_use": round(cnt["bounce_lanes_busy"][b] / max(1, 64 * cnt["bounce_wave_iters"][b]), 3),
                  "shadow_lane_use": round(cnt["bounce_shadow_lanes_busy"][b] / max(1, 64 * cnt["bounce_shadow_wave_iters"][b]), 3)}

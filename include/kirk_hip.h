@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 4
+#define KHP_ABI_VERSION 5
 
 typedef struct khp_ctx khp_ctx;
 
@@ -146,6 +146,8 @@ typedef struct {
 #define KHP_RENDER_OUT_DEVICE   (1u << 0)  /* out_rgb is a device pointer        */
 #define KHP_RENDER_NO_READBACK  (1u << 1)  /* keep framebuffer in HBM only       */
 #define KHP_RENDER_STATS        (1u << 2)  /* instrumented kernels for this call  */
+#define KHP_RENDER_ASYNC        (1u << 3)  /* enqueue and return (ABI 5): frames in flight overlap;
+                                              no readback, no STATS; khp_sync completes them */
 
 /* One khp_render call = samples [first_sample, first_sample+spp) of
  * PathTracer::render (CPU_PathTracer.cpp:17-52) for every pixel this rank
@@ -185,7 +187,8 @@ typedef struct {
      * resolve / record fetch / compute / loop+refill, summed over waves */
     uint64_t step_cycles[4];
     /* ABI 3: where khp_build_accel built the BVH and how long it took */
-    uint32_t bvh_on_device, pad0;    /* 1: device build (default), 0: host   */
+    uint32_t bvh_on_device;          /* 1: device build (default), 0: host   */
+    uint32_t subframes;              /* last khp_render: concurrent path sets (KHP_SUBFRAMES) */
     double flatten_ms;               /* khp_set_scene (flatten, incl. copies) */
     double bvh_ms;                   /* BVH build wall time incl. transfers   */
     double bvh_kernel_ms;            /* device build: GPU time of its kernels  */
@@ -194,6 +197,14 @@ typedef struct {
     double layout_kernel_ms;         /* device layout: GPU time of its kernels  */
     /* stack entries popped only to fail the prune test (instrumented renders) */
     uint64_t extend_pruned_pops, shadow_pruned_pops;
+    /* ABI 5: frames this report covers -- 1 after a synchronous khp_render; after
+     * khp_sync, every asynchronous frame completed since the previous report, with
+     * timings (extend_ms, extend_launches, ...) and counters summed over them */
+    uint64_t frames;
+    /* ABI 5: wall time during which at least one k_extend launch of the report
+     * was running (union of the launches' HIP-event intervals); equals extend_ms
+     * when launches do not overlap (synchronous renders) */
+    double extend_busy_ms;
 } khp_stats;
 #define KHP_MAX_BOUNCE_STATS 16
 
@@ -220,6 +231,12 @@ khp_status khp_build_accel(khp_ctx* ctx);
  * floats (host unless KHP_RENDER_OUT_DEVICE, ignored with NO_READBACK).
  * Pixels of tiles not owned by this rank are left untouched. */
 khp_status khp_render(khp_ctx* ctx, const khp_render_params* p, float* out_rgb);
+
+/* Completes every frame enqueued with KHP_RENDER_ASYNC (ABI 5).  A progressive
+ * caller (KIRK's PathTracer::render loop) enqueues its passes and syncs before
+ * reading the texture; passes accumulate in call order.  Any synchronous call
+ * (render, read, gather, scene change) also completes in-flight frames first. */
+khp_status khp_sync(khp_ctx* ctx);
 
 /* khp_set_scene with the geometry arrays (tri_v, tri_n, tri_mat, cone_*) in
  * device memory of ctx's GPU (materials, lights, camera stay host structs).

@@ -119,3 +119,12 @@ def test_product_does_not_link_the_oracle():
     import ba_pathtracing_fur_amd.native as nat
     src = "".join(open(m.__file__).read() for m in (pt, nat, S))
     assert "import oracle" not in src and "oracle_ffi" not in src
+
+
+def test_package_exports_and_queue_default():
+    import ba_pathtracing_fur_amd as P
+    for name in P.__all__:
+        assert getattr(P, name) is not None
+    # two frames in flight need more than HIP's default 4 hardware queues (see __init__)
+    if os.environ.get("KHP_KEEP_HW_QUEUES") != "1":
+        assert int(os.environ["GPU_MAX_HW_QUEUES"]) >= 8

@@ -107,6 +107,65 @@ def test_path_chunking(hip_ctx):
     assert_parity(got, oracle_ffi.Oracle(sd).render(128, 96, 3, 5, threads=16), exact=True)
 
 
+SET_MODES = [dict(KHP_SUBFRAMES="1"), dict(KHP_SUBFRAMES="3"), dict(KHP_SUBFRAMES="4", KHP_STAGGER="1"),
+             dict(KHP_SUBFRAMES="3", KHP_SPLIT="p"), dict(KHP_SUBFRAMES="4", KHP_STAGGER="1", KHP_SET_STREAMS="1")]
+
+
+@pytest.mark.parametrize("env", SET_MODES, ids=["-".join(f"{k[4:]}{v}" for k, v in m.items()) for m in SET_MODES])
+def test_path_sets_do_not_change_the_frame(hip_ctx, env):
+    """Path sets (KHP_SUBFRAMES: sample passes or pixel ranges on their own
+    streams, optionally staggered; also combined with path chunking) leave the
+    frame equal to the oracle's, bit for bit."""
+    sd = S.config2(120, 72, n_strands=1500)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    spp = 5
+    want = oracle_ffi.Oracle(sd).render(120, 72, spp, 5, threads=16)
+    os.environ.update(env)
+    try:
+        got = hip_ctx.render(120, 72, spp, 5)
+        assert hip_ctx.stats()["subframes"] == int(env["KHP_SUBFRAMES"])
+        assert_parity(got, want, exact=True)
+        os.environ["KHP_MAX_PATHS"] = "5000"
+        got = hip_ctx.render(120, 72, spp, 5)
+        assert_parity(got, want, exact=True)
+        got = hip_ctx.render(120, 72, spp, 5, stats=True)   # instrumented: one stream, per-set snapshots
+        st = hip_ctx.stats()
+        assert sum(st["bounce_rays"]) == st["extend_rays"] > 0
+        assert_parity(got, want, exact=True)
+    finally:
+        for k in list(env) + ["KHP_MAX_PATHS"]:
+            os.environ.pop(k, None)
+
+
+@pytest.mark.parametrize("fif", ["1", "2", "3"])
+def test_async_frames_in_flight(hip_ctx, fif):
+    """KHP_RENDER_ASYNC: progressive passes enqueued back to back (up to
+    KHP_FRAMES_IN_FLIGHT overlapping on the device) accumulate in call order;
+    after khp_sync the framebuffer is the oracle's 5-spp frame, and the report
+    covers every pass."""
+    sd = S.config2(96, 64, n_strands=1500)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    want = oracle_ffi.Oracle(sd).render(96, 64, 5, 5, threads=16)
+    os.environ["KHP_FRAMES_IN_FLIGHT"] = fif
+    try:
+        for first, n in ((0, 1), (1, 2), (3, 1), (4, 1)):
+            hip_ctx.render(96, 64, n, 5, first_sample=first, async_=True)
+        hip_ctx.sync()
+        st = hip_ctx.stats()
+        assert st["frames"] == 4 and st["extend_launches"] == 4 * 5
+        assert_parity(hip_ctx.read_framebuffer(96, 64), want, exact=True)
+        # a synchronous render after async ones completes them first
+        hip_ctx.render(96, 64, 2, 5, async_=True)
+        got = hip_ctx.render(96, 64, 3, 5, first_sample=2)
+        assert_parity(got, want, exact=True)
+        with pytest.raises(N.KhpError):
+            hip_ctx.render(96, 64, 1, 5, async_=True, stats=True)
+    finally:
+        os.environ.pop("KHP_FRAMES_IN_FLIGHT", None)
+
+
 def test_deterministic_across_runs(hip_ctx):
     sd = S.config3(64, 36, n_strands=5000)
     hip_ctx.set_scene(sd)

@@ -46,7 +46,7 @@ class OracleBackedCtx:
         self.uid, self.nranks, self.rank = uid, nranks, rank
 
     def render(self, width, height, spp, depth, seed, first_sample, tile_size, tile_rank, tile_nranks, readback,
-               stats):
+               stats, async_=False):
         self.o.render(width, height, spp, depth, seed=seed, first_sample=first_sample, threads=2, out=self.fb,
                       tile_size=tile_size, tile_rank=tile_rank, tile_nranks=tile_nranks)
 
@@ -63,6 +63,9 @@ class OracleBackedCtx:
             dist.recv(buf, src=r)
             self.fb[m] = buf.numpy()
 
+    def sync(self):
+        pass
+
 
 def _worker(rank, world, port, out_dir):
     sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")]
@@ -75,7 +78,9 @@ def _worker(rank, world, port, out_dir):
     frame = sharding.ShardedFrame(ctx, rank, world, dist, tile=TILE, unique_id=lambda: bytes(range(128)))
     assert ctx.uid == bytes(range(128))                  # root's id reached every rank
     frame.barrier()
-    frame.render(W, H, SPP, DEPTH)
+    for _ in range(2):   # bench.py's pipelined steps: asynchronous frames + gathers, one sync at the end
+        frame.render(W, H, SPP, DEPTH, async_=True)
+    frame.sync()
     assert frame.max_over_ranks(float(rank + 1)) == float(world)
     assert frame.sum_over_ranks(1.0) == float(world)
     if rank == 0:

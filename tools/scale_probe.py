@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--ranks-max", type=int, default=8, help="time at most this many ranks per N (spread over 0..N-1)")
+    ap.add_argument("--sync-steps", action="store_true", help="no frame pipelining (bench.py --sync-steps)")
     a = ap.parse_args()
     W, H, spp, depth = a.width, a.height, a.spp, a.depth
     ctx = HipContext(0)
@@ -40,15 +41,19 @@ def main():
     ctx.build_accel()
     out = []
     for n in a.nranks:
-        ranks = list(range(n)) if n <= a.ranks_max else [round(i * (n - 1) / (a.ranks_max - 1)) for i in range(a.ranks_max)]
+        ranks = (list(range(n)) if n <= a.ranks_max else [0] if a.ranks_max <= 1 else
+                 [round(i * (n - 1) / (a.ranks_max - 1)) for i in range(a.ranks_max)])
         per = {}
         for r in ranks:
-            kw = dict(seed=0x4B49524B, tile_size=a.tile, tile_rank=r, tile_nranks=n, readback=False)
+            kw = dict(seed=0x4B49524B, tile_size=a.tile, tile_rank=r, tile_nranks=n, readback=False,
+                      async_=not a.sync_steps)
             ctx.render(W, H, spp, depth, **kw)  # warmup
             ctx.render(W, H, spp, depth, **kw)
+            ctx.sync()
             t0 = time.perf_counter()
             for _ in range(a.steps):
                 ctx.render(W, H, spp, depth, **kw)
+            ctx.sync()
             per[r] = (time.perf_counter() - t0) / a.steps * 1e3
             print(f"N={n} rank {r}: {per[r]:.3f} ms/frame", file=sys.stderr, flush=True)
         worst = max(per.values())
