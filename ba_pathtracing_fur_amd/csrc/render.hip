@@ -34,8 +34,9 @@ using namespace khp;
 #define KHP_MAX_SEG 64
 #endif
 struct alignas(128) Counters {
-    uint32_t nq[2];        // ray queue sizes
-    uint32_t pad_a[30];
+    uint32_t nq[2];        // ray queue sizes: front part (predicted long rays)
+    uint32_t nqb[2];       // back part (predicted short rays), stored from the end of the buffers
+    uint32_t pad_a[28];
     uint32_t fetch_ext[KHP_MAX_SEG * 32];  // queue-segment claim cursors, one 128-B line each
     unsigned long long ext_rays, sh_rays;
     unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests, spills;
@@ -48,8 +49,9 @@ struct alignas(128) Counters {
 // (bounce parity) let k_shade of bounce b+1 fill one while k_shadow of bounce
 // b drains the other on the second stream.
 struct alignas(128) ShadowQ {
-    uint32_t nsh;
-    uint32_t pad[31];
+    uint32_t nsh;          // front part (predicted long shadow rays)
+    uint32_t nshb;         // back part
+    uint32_t pad[30];
     uint32_t fetch[KHP_MAX_SEG * 32];
 };
 
@@ -77,7 +79,22 @@ struct Wave {
     uint32_t sample0;     // global sample index of chunk sample 0
     uint32_t n_samples;   // samples in this chunk
     uint32_t depth;
+    uint8_t* heavy;       // per queue slot: the ray's traversal took more than heavy_T iterations
+    uint32_t cap;         // queue / path capacity of this set
+    uint32_t heavy_T;
 };
+
+// Longest-first queues.  A persistent traversal launch ends when its slowest
+// ray does; if long rays are claimed last, each launch ends one long-ray
+// latency (~1 ms inside the hairball) after its queue has drained.  k_shade
+// therefore writes the next bounce's rays (and the shadow rays) of paths
+// whose last traversal was long to the front of the queue buffers and the
+// others to the back (stored from the end), and the claim order takes the
+// front part of every claim segment first.  Paths are independent, so the
+// order changes no result.
+__device__ __forceinline__ uint32_t q_phys(uint32_t v, uint32_t nf, uint32_t cap) {
+    return v < nf ? v : cap - 1u - (v - nf);
+}
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
@@ -103,7 +120,10 @@ __device__ __forceinline__ T wave_sum(T v) {
 __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
     uint32_t n = Wv.P * Wv.n_samples;
     uint32_t pid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pid == 0) Wv.cnt->nq[0] = n;
+    if (pid == 0) {
+        Wv.cnt->nq[0] = n;   // primary rays: all in the front part
+        Wv.cnt->nqb[0] = 0;
+    }
     if (pid >= n) return;
     // pixel-major: the samples of one pixel are adjacent paths, so a wave traces
     // 64/n_samples neighbouring pixels x all their samples (cache reuse)
@@ -128,12 +148,14 @@ __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
 __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
     int nxt = cur ^ 1;
     c->nq[nxt] = 0;
+    c->nqb[nxt] = 0;
     q->nsh = 0;
+    q->nshb = 0;
     for (int g = 0; g < KHP_MAX_SEG; ++g) {
         c->fetch_ext[32 * g] = 0;
         q->fetch[32 * g] = 0;
     }
-    c->ext_rays += c->nq[cur];
+    c->ext_rays += c->nq[cur] + c->nqb[cur];
 }
 
 // ---- persistent lane-refill traversal -------------------------------------------------------
@@ -194,18 +216,33 @@ constexpr uint32_t NSEG = KHP_XCD_SPLIT ? 8u * KHP_SEG_PER_XCD : 1u;
 struct Claimer {
     uint32_t* fetch;  // NSEG cursors, one 128-B line each
     uint32_t n;       // queue length
+    uint32_t nf, nl, cap;  // front / back parts, buffer capacity (longest-first queues)
     uint32_t sg;      // segment this wave is draining (wave-uniform)
+    uint32_t rseg;    // segment of the current reservation
     uint32_t tried;   // segments found exhausted
     uint32_t res_lo, res_hi;  // reserved, not yet handed out (KHP_CLAIM_CHUNK)
-    __device__ __forceinline__ void init(uint32_t* f, uint32_t len) {
+    // Segment g holds the front-part slice [nf*g/NSEG, nf*(g+1)/NSEG) followed by
+    // the back-part slice [nl*g/NSEG, nl*(g+1)/NSEG): long rays first everywhere.
+    __device__ __forceinline__ void init(uint32_t* f, uint32_t front, uint32_t back, uint32_t capacity) {
         fetch = f;
-        n = len;
+        nf = front;
+        nl = back;
+        cap = capacity;
+        n = front + back;
+        rseg = 0;
         // group g = blockIdx % 8 (one XCD) owns the contiguous segments [g*K, g*K + K)
         sg = NSEG > 1 ? (blockIdx.x % 8u) * (NSEG / 8u) + (blockIdx.x / 8u) % (NSEG / 8u) : 0u;
         tried = 0;
         res_lo = res_hi = 0;
     }
-    __device__ __forceinline__ uint32_t lo(uint32_t g) const { return (uint32_t)((uint64_t)n * g / NSEG); }
+    __device__ __forceinline__ uint32_t hlo(uint32_t g) const { return (uint32_t)((uint64_t)nf * g / NSEG); }
+    __device__ __forceinline__ uint32_t llo(uint32_t g) const { return (uint32_t)((uint64_t)nl * g / NSEG); }
+    __device__ __forceinline__ uint32_t lo(uint32_t g) const { return hlo(g) + llo(g); }
+    // physical queue slot of virtual index v of the current reservation
+    __device__ __forceinline__ uint32_t phys(uint32_t v) const {
+        const uint32_t local = v - lo(rseg), hf = hlo(rseg + 1) - hlo(rseg);
+        return local < hf ? hlo(rseg) + local : cap - 1u - (llo(rseg) + (local - hf));
+    }
     // Reserve up to `want` indices from the current segment (moving on when it runs dry).
     __device__ __forceinline__ void reserve(uint32_t want) {
         while (res_lo >= res_hi && tried < NSEG) {
@@ -216,6 +253,7 @@ struct Claimer {
             if (base < len) {
                 res_lo = s0 + base;
                 res_hi = s0 + (base + want < len ? base + want : len);
+                rseg = sg;
             }
             if (base + want >= len) {
                 sg = (sg + 1) % NSEG;
@@ -278,10 +316,30 @@ __device__ __forceinline__ void trav_round(const DevScene& S, const TravRay& tr,
     }
 }
 
+#ifndef KHP_TAIL_PROBE
+#define KHP_TAIL_PROBE 0
+#endif
+// Tail priority: once a launch's queue is drained, the rays still in flight
+// set its end, and with frames in flight they compete for issue slots with
+// the other frame's bulk waves; raising the wave priority (s_setprio) lets
+// them issue first.
+#ifndef KHP_TAIL_PRIO
+#define KHP_TAIL_PRIO 0
+#endif
+#if KHP_TAIL_PROBE
+#define KHP_TAIL_PROBE_WAVES 65536
+__device__ unsigned long long g_tail_probe[6 * KHP_TAIL_PROBE_WAVES];
+extern "C" int khp_debug_tail_probe(unsigned long long* out, int reset) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_tail_probe)) != hipSuccess) return 1;
+    if (reset) return hipMemset(p, 0, sizeof(g_tail_probe)) == hipSuccess ? 0 : 1;
+    return hipMemcpy(out, p, sizeof(g_tail_probe), hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 template <bool STATS>
 __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
-    const uint32_t n = Wv.cnt->nq[cur];
+    const uint32_t nf = Wv.cnt->nq[cur], nb = Wv.cnt->nqb[cur];
     TravStack<RING, STATS> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0};
@@ -296,15 +354,26 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene 
 #if KHP_PROFILE_STEPS
     uint64_t prof[4] = {0, 0, 0, 0}, prof_last = __builtin_amdgcn_s_memtime(), prof_t0 = prof_last;
 #endif
+    uint32_t it = 0;  // this lane's iterations on its current ray (longest-first queues)
+#if KHP_TAIL_PROBE
+    // diagnostic build: per wave [start, queue drained, end] (s_memrealtime,
+    // 100 MHz), rays started, longest ray (iterations), iterations after the drain
+    uint64_t tp_start = __builtin_amdgcn_s_memrealtime(), tp_ex = 0;
+    uint32_t tp_rays = 0, tp_max = 0, tp_after = 0;
+#endif
     Claimer cl;
-    cl.init(Wv.cnt->fetch_ext, n);
+    cl.init(Wv.cnt->fetch_ext, nf, nb, Wv.cap);
     for (;;) {
         unsigned long long idle = __ballot(!has);
         if (!exhausted && __popcll(idle) >= REFILL) {
             uint32_t my;
             const bool got = cl.claim(idle, my, exhausted);
             if (!has && got) {
-                idx = my;
+                idx = cl.phys(my);
+                it = 0;
+#if KHP_TAIL_PROBE
+                ++tp_rays;
+#endif
                 Ray r;
                 r.o = mk(Wv.qo[cur][0][idx], Wv.qo[cur][1][idx], Wv.qo[cur][2][idx]);
                 r.d = mk(Wv.qd[cur][0][idx], Wv.qd[cur][1][idx], Wv.qd[cur][2][idx]);
@@ -323,6 +392,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene 
                     Wv.hslot[idx] = -1;
                     Wv.hu[idx] = 0.0f;
                     Wv.hv[idx] = 0.0f;
+                    Wv.heavy[idx] = 0;
                 }
             }
         }
@@ -333,7 +403,16 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene 
         }
         for (;;) {
 #if KHP_LOOP2
+#if KHP_TAIL_PROBE
+            if (exhausted) {
+                if (tp_ex == 0) tp_ex = __builtin_amdgcn_s_memrealtime();
+                ++tp_after;
+            }
+#endif
             const bool tail_pf = KHP_TAIL_PF && exhausted && __popcll(act) <= KHP_TAIL_PF_LANES;
+#if KHP_TAIL_PRIO
+            if (exhausted) __builtin_amdgcn_s_setprio(KHP_TAIL_PRIO);  // drained queue: this wave's rays end the launch
+#endif
             if (STATS) {
                 unsigned long long wm = __ballot(has && (mode == M_NODE || mode == M_LEAF));
                 ++wit;
@@ -341,11 +420,16 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene 
             }
             if (has) {
                 bool occ_unused;
+                ++it;
                 if (iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused, tail_pf, pf)) {
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = h.slot;
                     Wv.hu[idx] = h.u;
                     Wv.hv[idx] = h.v;
+                    Wv.heavy[idx] = it > Wv.heavy_T ? 1 : 0;
+#if KHP_TAIL_PROBE
+                    tp_max = it > tp_max ? it : tp_max;
+#endif
                     has = false;
                 }
             }
@@ -403,6 +487,25 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene 
             if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
     }
+#if KHP_TAIL_PROBE
+    {
+        uint32_t mx = tp_max;
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+        uint32_t nr = wave_sum(tp_rays);
+        if (lane_id() == 0) {
+            const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+            if (w < KHP_TAIL_PROBE_WAVES) {
+                unsigned long long* r = g_tail_probe + 6 * (size_t)w;
+                r[0] = tp_start;
+                r[1] = tp_ex;
+                r[2] = __builtin_amdgcn_s_memrealtime();
+                r[3] = nr;
+                r[4] = mx;
+                r[5] = tp_after;
+            }
+        }
+    }
+#endif
     if (STATS) {
         unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
         unsigned long long pr = wave_sum((unsigned long long)st.pruned);
@@ -466,20 +569,51 @@ __device__ __forceinline__ void block_alloc2(bool p0, bool p1, uint32_t* c0, uin
     __syncthreads();  // sh is reused by the next iteration
 }
 
+// Four outputs (next-bounce rays and shadow rays, each front or back): a lane
+// sets at most one of p0/p1 and one of p2/p3; i01 / i23 is its index in the
+// queue it was counted in.
+struct BlockAlloc4 {
+    uint32_t wcnt[4][4];
+    uint32_t base[4];
+};
+__device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3, uint32_t* c0, uint32_t* c1,
+                                             uint32_t* c2, uint32_t* c3, BlockAlloc4& sh, uint32_t& i01,
+                                             uint32_t& i23) {
+    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+    const unsigned long long m[4] = {__ballot(p0), __ballot(p1), __ballot(p2), __ballot(p3)};
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (lane == 0)
+        for (int q = 0; q < 4; ++q) sh.wcnt[q][wid] = (uint32_t)__popcll(m[q]);
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const uint32_t q = threadIdx.x;
+        const uint32_t tot = sh.wcnt[q][0] + sh.wcnt[q][1] + sh.wcnt[q][2] + sh.wcnt[q][3];
+        uint32_t* ctr = q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : c3;
+        sh.base[q] = tot ? atomicAdd(ctr, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t o[4] = {sh.base[0], sh.base[1], sh.base[2], sh.base[3]};
+    for (uint32_t w = 0; w < wid; ++w)
+        for (int q = 0; q < 4; ++q) o[q] += sh.wcnt[q][w];
+    i01 = p0 ? o[0] + (uint32_t)__popcll(m[0] & lt) : o[1] + (uint32_t)__popcll(m[1] & lt);
+    i23 = p2 ? o[2] + (uint32_t)__popcll(m[2] & lt) : o[3] + (uint32_t)__popcll(m[3] & lt);
+    __syncthreads();  // sh is reused by the next iteration
+}
+
 #ifndef KHP_SHADE_WAVES
 #define KHP_SHADE_WAVES 1
 #endif
 __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
-    const uint32_t n = Wv.cnt->nq[cur];
+    const uint32_t nf = Wv.cnt->nq[cur], n = nf + Wv.cnt->nqb[cur];
     const int nxt = cur ^ 1;
     const bool last = bounce + 1 >= Wv.depth;
     const uint32_t stride = gridDim.x * blockDim.x;
-#if KHP_BLOCK_ALLOC
-    __shared__ BlockAlloc2 balloc;
-#endif
+    __shared__ BlockAlloc4 balloc;
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {
-        uint32_t i = base + threadIdx.x;
-        bool active = i < n;
+        const uint32_t iv = base + threadIdx.x;
+        bool active = iv < n;
+        const uint32_t i = active ? q_phys(iv, nf, Wv.cap) : 0u;
+        const bool heavy = active && Wv.heavy[i] != 0;
         bool emit_ray = false, emit_sh = false;
         Ray nr;
         nr.o = nr.d = mk(0, 0, 0);
@@ -634,20 +768,16 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
             Wv.flags[pid] = flags;
             emit_ray = !last && !is_zero(T) && !is_zero(nr.d);
         }
-#if KHP_BLOCK_ALLOC
         uint32_t qi, si;
-        block_alloc2(emit_ray, emit_sh, &Wv.cnt->nq[nxt], &Wv.shq->nsh, balloc, qi, si);
-#else
-        uint32_t qi = wave_alloc(emit_ray, &Wv.cnt->nq[nxt]);
-#endif
+        block_alloc4(emit_ray && heavy, emit_ray && !heavy, emit_sh && heavy, emit_sh && !heavy,
+                     &Wv.cnt->nq[nxt], &Wv.cnt->nqb[nxt], &Wv.shq->nsh, &Wv.shq->nshb, balloc, qi, si);
+        qi = heavy ? qi : Wv.cap - 1u - qi;
+        si = heavy ? si : Wv.cap - 1u - si;
         if (emit_ray) {
             Wv.qo[nxt][0][qi] = nr.o.x; Wv.qo[nxt][1][qi] = nr.o.y; Wv.qo[nxt][2][qi] = nr.o.z;
             Wv.qd[nxt][0][qi] = nr.d.x; Wv.qd[nxt][1][qi] = nr.d.y; Wv.qd[nxt][2][qi] = nr.d.z;
             Wv.qpid[nxt][qi] = pid;
         }
-#if !KHP_BLOCK_ALLOC
-        uint32_t si = wave_alloc(emit_sh, &Wv.shq->nsh);
-#endif
         if (emit_sh) {
             float4* rec = Wv.sh + 6 * (size_t)si;
             rec[0] = make_float4(shr.o.x, shr.o.y, shr.o.z, sh_tmax);
@@ -665,9 +795,10 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
 // k_shadow_finish: one shadow record per lane, streaming; kept out of the
 // traversal kernel so k_shadow's registers go to traversal only.
 __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
-    const uint32_t n = Wv.shq->nsh;
+    const uint32_t nf = Wv.shq->nsh, n = nf + Wv.shq->nshb;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Wv.cnt->sh_rays, (unsigned long long)n);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (uint32_t iv = blockIdx.x * blockDim.x + threadIdx.x; iv < n; iv += gridDim.x * blockDim.x) {
+        const uint32_t i = q_phys(iv, nf, Wv.cap);
         const float4* rec = Wv.sh + 6 * (size_t)i;
         float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3], e = rec[4];
         uint32_t pid = bits_from_f(b.w);
@@ -701,7 +832,7 @@ __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
 template <bool STATS>
 __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
     extern __shared__ uint32_t lds[];
-    const uint32_t n = Wv.shq->nsh;
+    const uint32_t nf = Wv.shq->nsh, nb = Wv.shq->nshb;
     TravStack<RING_SH, STATS> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0};
@@ -717,7 +848,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
     bool found = false;
 #endif
     Claimer cl;
-    cl.init(Wv.shq->fetch, n);
+    cl.init(Wv.shq->fetch, nf, nb, Wv.cap);
     uint32_t idx = 0;
     for (;;) {
         unsigned long long idle = __ballot(!has);
@@ -725,7 +856,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
             uint32_t my;
             const bool got = cl.claim(idle, my, exhausted);
             if (!has && got) {
-                idx = my;
+                idx = cl.phys(my);
                 const float4* rec = Wv.sh + 6 * (size_t)idx;
                 float4 a = rec[0], b = rec[1];
                 Ray r;
@@ -753,6 +884,9 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
         for (;;) {
 #if KHP_LOOP2
             const bool tail_pf = KHP_TAIL_PF && exhausted && __popcll(act) <= KHP_TAIL_PF_LANES;
+#if KHP_TAIL_PRIO
+            if (exhausted) __builtin_amdgcn_s_setprio(KHP_TAIL_PRIO);  // drained queue: this wave's rays end the launch
+#endif
             if (STATS) {
                 unsigned long long wm = __ballot(has && (mode == M_NODE || mode == M_LEAF));
                 ++wit;
@@ -1062,9 +1196,13 @@ struct TimedLaunch {
 struct PathSet {
     size_t cap = 0;
     DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
+    DevMem heavyb;
     hipStream_t sA = nullptr, sB = nullptr;
 };
 
+#ifndef KHP_HEAVY_T
+#define KHP_HEAVY_T 160   // iterations above which a path's next rays go to the front (env KHP_HEAVY_T)
+#endif
 #ifndef KHP_MAX_INFLIGHT
 #define KHP_MAX_INFLIGHT 3
 #endif
@@ -1439,6 +1577,7 @@ static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap) {
     }
     HIPCHK(w.flagsb.ensure(cap * 4));
     HIPCHK(w.keyb.ensure(cap * 4));
+    HIPCHK(w.heavyb.ensure(cap));
     for (int q = 0; q < 2; ++q) {
         HIPCHK(w.visb[q].ensure(cap));
         HIPCHK(w.shb[q].ensure(cap * 6 * sizeof(float4)));
@@ -1481,6 +1620,10 @@ static Wave wave_view(PathSet& w) {
     Wv.sh = w.shb[0].as<float4>();
     Wv.shq = w.shqb.as<ShadowQ>();
     Wv.cnt = w.cnt.as<Counters>();
+    Wv.heavy = w.heavyb.as<uint8_t>();
+    Wv.cap = (uint32_t)w.cap;
+    Wv.heavy_T = KHP_HEAVY_T;
+    if (const char* e = getenv("KHP_HEAVY_T")) Wv.heavy_T = (uint32_t)strtoul(e, nullptr, 10);
     return Wv;
 }
 
