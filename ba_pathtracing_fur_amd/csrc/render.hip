@@ -1589,8 +1589,14 @@ static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap) {
     HIPCHK(w.spill.ensure((size_t)c->grid_ext * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
     HIPCHK(w.spill_sh.ensure((size_t)c->grid_sh * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
     if (!w.sA) {
-        HIPCHK(hipStreamCreateWithFlags(&w.sA, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&w.sB, hipStreamNonBlocking));
+        // KHP_STREAM_PRIO=A|B: the main (extend/shade) or the shadow stream of
+        // every path set gets the high hardware-queue priority (experiment knob)
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        const char* pe = getenv("KHP_STREAM_PRIO");
+        const int pa = (pe && pe[0] == 'A') ? hi : lo, pb = (pe && pe[0] == 'B') ? hi : lo;
+        HIPCHK(hipStreamCreateWithPriority(&w.sA, hipStreamNonBlocking, pa));
+        HIPCHK(hipStreamCreateWithPriority(&w.sB, hipStreamNonBlocking, pb));
     }
     w.cap = cap;
     return KHP_OK;

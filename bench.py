@@ -12,12 +12,24 @@ core, inputs (scene + BVH) resident in HBM, framebuffer left in HBM.  With
 (64x64 tiles, tile_id % N) and each step ends with the RCCL framebuffer
 gather to rank 0; total work is fixed, so scaling is "strong".
 
+Steps are pipelined (default): each frame is enqueued asynchronously
+(KHP_RENDER_ASYNC) and up to two frames run on the device at once, so one
+frame's chain of 2 x depth persistent launches -- each ending only when its
+slowest ray does -- overlaps the other frame's work; frames still complete and
+accumulate in order, and the timed region ends with khp_sync + a barrier.
+--sync-steps waits for every frame before starting the next.
+
 The JSON line also carries:
-  roofline     -- the extend (closest-hit) kernel: algorithmic bytes per launch
+  roofline     -- the extend (closest-hit) kernel: algorithmic bytes
                   (28 B ray + 32 B per visited node + 32 B per
                   primitive test + 16 B hit, visit counts from an instrumented
-                  frame) / its average launch time from HIP events in the
-                  timed region, against 8 TB/s HBM;
+                  frame) of all timed launches / the time during which at
+                  least one of them was running (union of their HIP-event
+                  intervals), against 8 TB/s HBM.  Without overlap
+                  (--sync-steps) that is bytes per launch / average launch
+                  time; avg_launch_ms and achieved_per_launch give the
+                  per-launch view (launch durations include the time the
+                  other frame's kernels shared the chip);
   cpu_baseline -- the C restatement (oracle/) timed on this host's cores on a
                   bounded sample of the same frame: progressive full-frame
                   samples 0, 1, ... until --cpu-seconds or the workload's spp.
@@ -38,7 +50,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--strands", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
