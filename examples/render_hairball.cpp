@@ -74,10 +74,19 @@ int main(int argc, char** argv) {
         double build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         khp_render_params p{W, H, spp, depth, SEED, 0, 64, 0, 1, KHP_RENDER_NO_READBACK};
         ctx.render(p);  // warm-up
+        // pipelined frames (ABI 5): enqueue every frame, complete them with one sync;
+        // the stats report then sums the frames (divided below)
+        khp_render_params pa = p;
+        pa.flags |= KHP_RENDER_ASYNC;
         t0 = std::chrono::steady_clock::now();
-        for (int f = 0; f < frames; ++f) ctx.render(p);
+        for (int f = 0; f < frames; ++f) ctx.render(pa);
+        ctx.sync();
         double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         khp_stats st = ctx.stats();
+        const double nf = st.frames ? (double)st.frames : 1.0;
+        st.extend_ms /= nf;
+        st.shade_ms /= nf;
+        st.shadow_ms /= nf;
         printf("{\"objects\": %zu, \"build_s\": %.2f, \"frames\": %d, \"ms_per_frame\": %.3f, \"Msamples_per_s\": %.2f, "
                "\"extend_ms\": %.2f, \"shade_ms\": %.2f, \"shadow_ms\": %.2f}\n",
                sb.n_objects(), build_s, frames, dt / frames * 1e3, (double)W * H * spp * frames / dt / 1e6,

@@ -101,6 +101,8 @@ class Context {
     void render(const khp_render_params& p, float* out_rgb = nullptr) {
         check(khp_render(c_, &p, out_rgb), "khp_render");
     }
+    // KHP_RENDER_ASYNC renders are complete (and accumulated in call order) after sync()
+    void sync() { check(khp_sync(c_), "khp_sync"); }
     void read_framebuffer(float* out_rgb) { check(khp_read_framebuffer(c_, out_rgb), "khp_read_framebuffer"); }
     // 8-bit texture (W*H*4); tm == nullptr: no tonemapping
     void read_rgba8(uint8_t* out_rgba, const khp_tonemap* tm = nullptr) {
