@@ -30,11 +30,13 @@ struct TravStats {
 struct TravRay {
     Ray r;
     v3 inv;
+    bool fin;  // all three inverse direction components are finite (fast slab test is exact)
 };
 
 __device__ __forceinline__ void trav_setup(TravRay& tr, const Ray& r) {
     tr.r = r;
     tr.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    tr.fin = __builtin_isfinite(tr.inv.x) && __builtin_isfinite(tr.inv.y) && __builtin_isfinite(tr.inv.z);
 }
 
 __device__ __forceinline__ bool ref_leaf(uint32_t r) { return (r & LEAF_BIT) != 0u; }
@@ -743,6 +745,27 @@ __device__ __forceinline__ bool slab_sel(float mnx, float mny, float mnz, float 
     return ok;
 }
 
+// Fast slab pair for rays whose inverse direction is finite on every axis
+// (every ray but those with an exactly zero direction component).  Then
+// (mn - o)*inv and (mx - o)*inv are finite and ordered by the sign of inv, so
+// min/max pick exactly the operands KIRK's sign selects pick, and KIRK's
+// chain of early-out comparisons is equivalent to max3(entries) <= min3(exits)
+// (each axis' own entry <= exit).  t0/t1 are bit-identical up to the sign of a
+// zero, which no comparison downstream distinguishes.  Rays with an infinite
+// component (0 * inf = NaN cases) take slab_sel.
+#ifndef KHP_FAST_SLAB
+#define KHP_FAST_SLAB 1
+#endif
+__device__ __forceinline__ bool slab_fast(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                          const TravRay& tr, float& t0, float& t1) {
+    const float ax = (mnx - tr.r.o.x) * tr.inv.x, bx = (mxx - tr.r.o.x) * tr.inv.x;
+    const float ay = (mny - tr.r.o.y) * tr.inv.y, by = (mxy - tr.r.o.y) * tr.inv.y;
+    const float az = (mnz - tr.r.o.z) * tr.inv.z, bz = (mxz - tr.r.o.z) * tr.inv.z;
+    t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    return t0 <= t1;
+}
+
 #ifndef KHP_SLAB_SEL
 #define KHP_SLAB_SEL 1
 #endif
@@ -870,8 +893,14 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
         if (STATS) st.nodes++;
         const float tlimit = ANY ? tmax_any : h.t;
         float l0, l1, r0, r1;
-        bool lh = slab2(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, tr, l0, l1);
-        bool rh = slab2(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, tr, r0, r1);
+        bool lh, rh;
+        if (KHP_FAST_SLAB && __ballot(!tr.fin) == 0ull) {  // wave-uniform
+            lh = slab_fast(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, tr, l0, l1);
+            rh = slab_fast(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, tr, r0, r1);
+        } else {
+            lh = slab2(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, tr, l0, l1);
+            rh = slab2(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, tr, r0, r1);
+        }
         lh = lh && !(l1 < 0.0f || l0 > tlimit);
         rh = rh && !(r1 < 0.0f || r0 > tlimit);
         const uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
