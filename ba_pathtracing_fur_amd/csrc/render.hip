@@ -1203,6 +1203,9 @@ struct PathSet {
 #ifndef KHP_HEAVY_T
 #define KHP_HEAVY_T 160   // iterations above which a path's next rays go to the front (env KHP_HEAVY_T)
 #endif
+#ifndef KHP_FRAME_STAGGER_DEFAULT
+#define KHP_FRAME_STAGGER_DEFAULT -1  // env KHP_FRAME_STAGGER (-1: frames start together; measured best)
+#endif
 #ifndef KHP_MAX_INFLIGHT
 #define KHP_MAX_INFLIGHT 3
 #endif
@@ -1247,6 +1250,7 @@ struct khp_ctx {
     FrameSlot fs[KHP_MAX_INFLIGHT];
     uint64_t frame_no = 0;
     hipEvent_t fb_evt = nullptr;   // the last framebuffer operation enqueued (accumulate or gather)
+    hipEvent_t prev_mid = nullptr; // asynchronous frames: the previous frame reached its stagger point
     bool report_open = false;      // c->st accumulates harvested frames
     hipEvent_t gather_evt = nullptr;  // end of the last framebuffer gather (becomes fb_evt)
     hipEvent_t report_ref = nullptr;  // time origin of the open report
@@ -1956,6 +1960,14 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
         e_fork = slot_event(f.sync_pool, f.sync_next, true);
         HIPCHK(hipEventRecord(e_fork, c->stream));
     }
+    // Frame stagger (asynchronous frames): a frame starts only when the previous
+    // one has finished its extend launch of bounce KHP_FRAME_STAGGER, so two
+    // frames in flight run out of phase -- one's long-ray tails beside the
+    // other's full launches -- instead of in lockstep (-1: no stagger).
+    int fstag = KHP_FRAME_STAGGER_DEFAULT;
+    if (const char* e = getenv("KHP_FRAME_STAGGER")) fstag = atoi(e);
+    hipEvent_t wait_mid = (async && fstag >= 0) ? c->prev_mid : nullptr;
+    hipEvent_t my_mid = nullptr;
     hipEvent_t prev_started = nullptr;  // KHP_STAGGER: the previous set's first extend launch finished
     hipEvent_t prev_acc = c->fb_evt;    // the previous framebuffer operation (this set's accumulate waits for it)
     std::vector<hipEvent_t> set_end;
@@ -1965,6 +1977,10 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
         hipStream_t sB = overlap ? (set_streams >= 2 ? w.sB : w.sA) : c->stream;
         if (e_fork && sA != c->stream) HIPCHK(hipStreamWaitEvent(sA, e_fork, 0));
         if (e_fork && sB != sA && sB != c->stream) HIPCHK(hipStreamWaitEvent(sB, e_fork, 0));
+        if (wait_mid) {
+            HIPCHK(hipStreamWaitEvent(sA, wait_mid, 0));
+            if (sB != sA) HIPCHK(hipStreamWaitEvent(sB, wait_mid, 0));
+        }
         if (overlap && prev_started) {
             HIPCHK(hipStreamWaitEvent(sA, prev_started, 0));
             if (sB != sA) HIPCHK(hipStreamWaitEvent(sB, prev_started, 0));
@@ -2027,6 +2043,10 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
                     else
                         hipLaunchKernelGGL(k_extend<false>, dim3(grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
                     timed(c, f, 0, false, sA);
+                    if (async && fstag >= 0 && (int)b == std::min(fstag, (int)p->depth - 1) && k == K - 1 && !my_mid) {
+                        my_mid = slot_event(f.sync_pool, f.sync_next, true);
+                        HIPCHK(hipEventRecord(my_mid, sA));
+                    }
                     if (overlap && stagger && k + 1 < K && !prev_started) {
                         prev_started = slot_event(f.sync_pool, f.sync_next, true);
                         HIPCHK(hipEventRecord(prev_started, sA));
@@ -2087,6 +2107,7 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     f.done = slot_event(f.sync_pool, f.sync_next, true);
     HIPCHK(hipEventRecord(f.done, c->stream));
     c->fb_evt = f.done;
+    c->prev_mid = async ? (my_mid ? my_mid : f.done) : nullptr;
     f.inflight = true;
     HIPCHK(hipGetLastError());
     if (async) return KHP_OK;
