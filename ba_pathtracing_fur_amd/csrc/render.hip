@@ -55,6 +55,9 @@ struct alignas(128) ShadowQ {
     uint32_t fetch[KHP_MAX_SEG * 32];
 };
 
+#ifndef KHP_MAX_FUSE
+#define KHP_MAX_FUSE 8
+#endif
 struct Wave {
     float* qo[2][3];
     float* qd[2][3];
@@ -77,7 +80,9 @@ struct Wave {
     uint32_t W, H;
     uint32_t seed;
     uint32_t sample0;     // global sample index of chunk sample 0
-    uint32_t n_samples;   // samples in this chunk
+    uint32_t n_samples;   // samples in this chunk (per frame)
+    uint32_t n_frames;    // fused frames in this chunk (paths: frame-major blocks of P x n_samples)
+    uint32_t fsample0[KHP_MAX_FUSE];  // per fused frame: global sample index of chunk sample 0
     uint32_t depth;
     uint8_t* heavy;       // per queue slot: the ray's traversal took more than heavy_T iterations
     uint32_t cap;         // queue / path capacity of this set
@@ -118,7 +123,8 @@ __device__ __forceinline__ T wave_sum(T v) {
 // ---- generate: camera rays (PathTracer::generatePrimaryRays, CPU_PathTracer.cpp:118-127;
 //      Camera::getRayFromPixel, Camera.cpp:59-66) -------------------------------------------
 __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
-    uint32_t n = Wv.P * Wv.n_samples;
+    const uint32_t per_frame = Wv.P * Wv.n_samples;
+    uint32_t n = per_frame * Wv.n_frames;
     uint32_t pid = blockIdx.x * blockDim.x + threadIdx.x;
     if (pid == 0) {
         Wv.cnt->nq[0] = n;   // primary rays: all in the front part
@@ -127,10 +133,11 @@ __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
     if (pid >= n) return;
     // pixel-major: the samples of one pixel are adjacent paths, so a wave traces
     // 64/n_samples neighbouring pixels x all their samples (cache reuse)
-    uint32_t p_local = pid / Wv.n_samples, s_local = pid - p_local * Wv.n_samples;
+    const uint32_t fr = pid / per_frame, pf = pid - fr * per_frame;
+    uint32_t p_local = pf / Wv.n_samples, s_local = pf - p_local * Wv.n_samples;
     uint32_t pixel = Wv.pix[Wv.p_off + p_local];
     uint32_t x = pixel % Wv.W, y = pixel / Wv.W;
-    uint32_t key = path_key(Wv.seed, pixel, Wv.sample0 + s_local);
+    uint32_t key = path_key(Wv.seed, pixel, Wv.fsample0[fr] + s_local);
     float u1 = draw_u01(key, dim_of(0, P_CAM_X)), u2 = draw_u01(key, dim_of(0, P_CAM_Y));
     const khp_camera& cam = S.cam;
     float s1 = ((float)x + u1) * cam.pixel_size, s2 = ((float)y + u2) * cam.pixel_size;
@@ -949,16 +956,18 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
 
 // ---- accumulate: PathTracer::drawTexture running mean (CPU_PathTracer.cpp:61-90) -------
 
-__global__ __launch_bounds__(256) void k_accumulate(Wave Wv, float* fb) {
+// Fused frames are accumulated one frame per launch (fr), in call order.
+__global__ __launch_bounds__(256) void k_accumulate(Wave Wv, float* fb, uint32_t fr) {
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= Wv.P) return;
     uint32_t pixel = Wv.pix[Wv.p_off + p];
     float* o = fb + 3 * (size_t)pixel;
     float r = o[0], g = o[1], b = o[2];
+    const size_t base = (size_t)fr * Wv.P * Wv.n_samples;
     for (uint32_t s = 0; s < Wv.n_samples; ++s) {
-        uint32_t pid = p * Wv.n_samples + s;
+        size_t pid = base + (size_t)p * Wv.n_samples + s;
         float cr = Wv.C[0][pid], cg = Wv.C[1][pid], cb = Wv.C[2][pid];
-        uint32_t k = Wv.sample0 + s;
+        uint32_t k = Wv.fsample0[fr] + s;
         if (k == 0) {
             r = cr; g = cg; b = cb;
         } else {
@@ -1206,11 +1215,14 @@ struct PathSet {
 #ifndef KHP_FRAME_STAGGER_DEFAULT
 #define KHP_FRAME_STAGGER_DEFAULT -1  // env KHP_FRAME_STAGGER (-1: frames start together; measured best)
 #endif
+#ifndef KHP_FUSE_FRAMES_DEFAULT
+#define KHP_FUSE_FRAMES_DEFAULT 8   // env KHP_FUSE_FRAMES: asynchronous frames per fused batch (measured best)
+#endif
 #ifndef KHP_MAX_INFLIGHT
 #define KHP_MAX_INFLIGHT 3
 #endif
 #ifndef KHP_FRAMES_IN_FLIGHT_DEFAULT
-#define KHP_FRAMES_IN_FLIGHT_DEFAULT 2   // env KHP_FRAMES_IN_FLIGHT (asynchronous renders)
+#define KHP_FRAMES_IN_FLIGHT_DEFAULT 1   // env KHP_FRAMES_IN_FLIGHT: batches in flight (asynchronous renders)
 #endif
 struct Snap {
     int set;
@@ -1225,6 +1237,13 @@ struct FrameSlot {
     hipEvent_t ev_start = nullptr, done_t = nullptr, done = nullptr;
     bool inflight = false;
     int K = 1;
+    uint32_t nf = 1;  // frames fused in this slot's batch
+};
+// An asynchronous operation waiting to be fused into the next batch.
+struct PendingOp {
+    enum Kind { RENDER, GATHER } kind;
+    khp_render_params p;
+    int root;
 };
 static hipEvent_t slot_event(std::vector<hipEvent_t>& pool, size_t& next, bool no_timing) {
     if (next == pool.size()) {
@@ -1253,6 +1272,7 @@ struct khp_ctx {
     hipEvent_t prev_mid = nullptr; // asynchronous frames: the previous frame reached its stagger point
     bool report_open = false;      // c->st accumulates harvested frames
     hipEvent_t gather_evt = nullptr;  // end of the last framebuffer gather (becomes fb_evt)
+    std::vector<PendingOp> pend;      // asynchronous renders (+ gathers) not yet enqueued (frame fusion)
     hipEvent_t report_ref = nullptr;  // time origin of the open report
     std::vector<std::pair<float, float>> ext_iv;  // the report's k_extend intervals (ms from report_ref)
     // framebuffer + pixel list
@@ -1736,7 +1756,7 @@ static khp_status harvest(khp_ctx* c, int slot) {
     if (!c->report_open) report_begin(c);
     float ms = 0.0f;
     if (hipEventElapsedTime(&ms, f.ev_start, f.done_t) == hipSuccess) c->st.render_ms += ms;
-    c->st.frames += 1;
+    c->st.frames += f.nf;
     c->st.subframes = (uint32_t)f.K;
     for (auto& l : f.launches) {
         float t = 0.0f;
@@ -1802,7 +1822,10 @@ static khp_status harvest(khp_ctx* c, int slot) {
 // Wait for every in-flight frame (their stats go to the open report) and for
 // the context stream.  Every entry point that reads or replaces device state
 // other than through an asynchronous render calls this first.
+static khp_status flush(khp_ctx* c);
 static khp_status drain(khp_ctx* c) {
+    khp_status fr = flush(c);
+    if (fr != KHP_OK) return fr;
     for (int s = 0; s < KHP_MAX_INFLIGHT; ++s) {
         khp_status r = harvest(c, s);
         if (r != KHP_OK) return r;
@@ -1820,14 +1843,24 @@ extern "C" khp_status khp_sync(khp_ctx* c) {
     return s;
 }
 
-extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* out_rgb) {
-    khp_status s = check_params(c, p);
-    if (s != KHP_OK) return s;
-    HIPCHK(hipSetDevice(c->device));
+// Enqueue one frame, or a fused batch of asynchronous frames (ops: their
+// render operations, which differ only in first_sample, and the framebuffer
+// gathers between them, in call order; p = the first render's parameters).
+static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root);
+static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* out_rgb,
+                                 const std::vector<PendingOp>* ops) {
+    khp_status s;
     const bool stats = (c->flags & KHP_CTX_STATS) != 0 || (p->flags & KHP_RENDER_STATS) != 0;
     const bool async = (p->flags & KHP_RENDER_ASYNC) != 0;
-    if (async && (stats || (out_rgb && !(p->flags & KHP_RENDER_NO_READBACK))))
-        return fail(KHP_EINVAL, "KHP_RENDER_ASYNC renders take no readback and no instrumentation");
+    // fused frames: their first samples, in call order
+    std::vector<uint32_t> fs0;
+    if (ops) {
+        for (const PendingOp& o : *ops)
+            if (o.kind == PendingOp::RENDER) fs0.push_back(o.p.first_sample);
+    } else {
+        fs0.push_back(p->first_sample);
+    }
+    const uint32_t nf = (uint32_t)fs0.size();
     const size_t npix = (size_t)p->width * p->height;
     uint32_t T = p->tile_size ? p->tile_size : 64;
     uint32_t nranks = p->tile_nranks > 1 ? p->tile_nranks : 1;
@@ -1895,8 +1928,10 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     const int grid_ext = std::max(1, c->grid_ext / G), grid_sh = std::max(1, c->grid_sh / G);
     K = std::max(1, std::min(K, KHP_MAX_SUBFRAMES));
     K = (int)std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)K, split_pix ? (P_all + 63) / 64 : p->spp));
+    if (nf > 1) K = 1;  // a fused batch is one path set
     f.K = K;
-    size_t cap_paths = (size_t)1 << 24;
+    f.nf = nf;
+    size_t cap_paths = (size_t)1 << 26;
     if (const char* e = getenv("KHP_MAX_PATHS")) cap_paths = std::max<size_t>(4096, strtoull(e, nullptr, 10));
     uint32_t pix_lo[KHP_MAX_SUBFRAMES + 1], spp_lo[KHP_MAX_SUBFRAMES + 1];
     for (int k = 0; k <= K; ++k) {
@@ -1923,9 +1958,22 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
         set_pix(k, a, b);
         set_spp(k, sa, sb);
         const uint32_t Pk = std::max<uint32_t>(1, b - a), Sk = std::max<uint32_t>(1, sb - sa);
-        P_chunk[k] = (uint32_t)std::min<size_t>(Pk, cap_paths);
-        S_chunk[k] = (uint32_t)std::max<size_t>(1, std::min<size_t>(Sk, cap_paths / std::max<uint32_t>(P_chunk[k], 1)));
-        s = ensure_wave(c, c->ps[slot * KHP_MAX_SUBFRAMES + k], (size_t)P_chunk[k] * S_chunk[k]);
+        if (nf > 1) {  // fused: every chunk carries all samples of all frames of its pixels
+            P_chunk[k] = (uint32_t)std::max<size_t>(1, std::min<size_t>(Pk, cap_paths / ((size_t)Sk * nf)));
+            S_chunk[k] = Sk;
+        } else {
+            P_chunk[k] = (uint32_t)std::min<size_t>(Pk, cap_paths);
+            S_chunk[k] = (uint32_t)std::max<size_t>(1, std::min<size_t>(Sk, cap_paths / std::max<uint32_t>(P_chunk[k], 1)));
+        }
+        // a partial batch (flushed by a sync) reserves room for a full one, so the
+        // first full batch does not allocate
+        size_t want = (size_t)P_chunk[k] * S_chunk[k] * nf;
+        if (nf > 1) {
+            int fuse = KHP_FUSE_FRAMES_DEFAULT;
+            if (const char* e = getenv("KHP_FUSE_FRAMES")) fuse = std::max(1, std::min(atoi(e), KHP_MAX_FUSE));
+            want = std::max(want, std::min<size_t>(cap_paths, (size_t)P_chunk[k] * S_chunk[k] * (size_t)fuse));
+        }
+        s = ensure_wave(c, c->ps[slot * KHP_MAX_SUBFRAMES + k], want);
         if (s != KHP_OK) return s;
     }
     const char* dump_env = getenv("KHP_DUMP_BOUNCE");
@@ -2011,9 +2059,11 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
                 uint32_t ns = std::min(S_chunk[k], set_s1 - s0);
                 Wv.P = P;
                 Wv.p_off = p0;
-                Wv.sample0 = p->first_sample + s0;
+                Wv.sample0 = fs0[0] + s0;
                 Wv.n_samples = ns;
-                uint32_t npaths = P * ns;
+                Wv.n_frames = nf;
+                for (uint32_t q = 0; q < nf; ++q) Wv.fsample0[q] = fs0[q] + s0;
+                uint32_t npaths = P * ns * nf;
                 timed(c, f, 3, true, sA);
                 hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wv);
                 timed(c, f, 3, false, sA);
@@ -2086,7 +2136,27 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
                     acc_waited = true;
                 }
                 timed(c, f, 3, true, sA);
-                hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, c->fb.as<float>());
+                if (!ops) {
+                    hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, c->fb.as<float>(), 0u);
+                } else {
+                    // fused frames in call order; a gather between two of them runs on the
+                    // context stream after the first's accumulate and before the second's
+                    // (a batch with gathers is one chunk: enqueue_frames' caller checks)
+                    uint32_t fr = 0;
+                    for (const PendingOp& o : *ops) {
+                        if (o.kind == PendingOp::RENDER) {
+                            hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv,
+                                               c->fb.as<float>(), fr++);
+                        } else {
+                            hipEvent_t acc = slot_event(f.sync_pool, f.sync_next, true);
+                            HIPCHK(hipEventRecord(acc, sA));
+                            c->fb_evt = acc;
+                            s = gather_now(c, &o.p, o.root);   // waits fb_evt, sets fb_evt to its own end
+                            if (s != KHP_OK) return s;
+                            HIPCHK(hipStreamWaitEvent(sA, c->fb_evt, 0));
+                        }
+                    }
+                }
                 timed(c, f, 3, false, sA);
                 if (sB != sA) {  // the next chunk's shadow stages come after this chunk's accumulate
                     hipEvent_t acc = slot_event(f.sync_pool, f.sync_next, true);
@@ -2122,6 +2192,105 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
     return KHP_OK;
 }
 
+
+// Frame fusion (asynchronous renders, KHP_FUSE_FRAMES = n > 1): up to n
+// consecutive asynchronous frames with the same geometry, spp, depth and seed
+// are enqueued as ONE batch -- one wavefront over all their paths, one
+// persistent launch per bounce -- and accumulated one frame after another in
+// call order (gathers in between run where they were called).  A launch's
+// tail (its slowest ray) is then paid once per batch instead of once per
+// frame.  Results are those of the frames rendered one by one.
+static bool fusable(const khp_render_params& a, const khp_render_params& b) {
+    return a.width == b.width && a.height == b.height && a.spp == b.spp && a.depth == b.depth && a.seed == b.seed &&
+           a.tile_size == b.tile_size && a.tile_rank == b.tile_rank && a.tile_nranks == b.tile_nranks &&
+           a.flags == b.flags;
+}
+
+static khp_status flush(khp_ctx* c) {
+    if (c->pend.empty()) return KHP_OK;
+    std::vector<PendingOp> ops;
+    ops.swap(c->pend);
+    const PendingOp* first = nullptr;
+    size_t nr = 0;
+    bool gathers = false;
+    for (const PendingOp& o : ops) {
+        if (o.kind == PendingOp::RENDER) {
+            if (!first) first = &o;
+            ++nr;
+        } else {
+            gathers = true;
+        }
+    }
+    if (!first) {  // only gathers
+        for (const PendingOp& o : ops) {
+            khp_status s = gather_now(c, &o.p, o.root);
+            if (s != KHP_OK) return s;
+        }
+        return KHP_OK;
+    }
+    // a batch with gathers must fit one chunk (every frame accumulated before the
+    // next frame's gather); otherwise enqueue the operations one by one
+    const uint32_t T = first->p.tile_size ? first->p.tile_size : 64;
+    std::vector<uint32_t> tmp;
+    size_t P = 0;
+    {
+        uint32_t nranks = first->p.tile_nranks > 1 ? first->p.tile_nranks : 1;
+        uint32_t pkey[5] = {first->p.width, first->p.height, T, nranks > 1 ? first->p.tile_rank : 0u, nranks};
+        if (memcmp(pkey, c->pix_key, sizeof(pkey)) == 0 && c->pix.p) {
+            P = c->pix_host.size();
+        } else {
+            owned_pixels(first->p.width, first->p.height, T, nranks > 1 ? first->p.tile_rank : 0u, nranks, tmp);
+            P = tmp.size();
+        }
+    }
+    size_t cap_paths = (size_t)1 << 26;
+    if (const char* e = getenv("KHP_MAX_PATHS")) cap_paths = std::max<size_t>(4096, strtoull(e, nullptr, 10));
+    const bool one_chunk = P * (size_t)first->p.spp * nr <= cap_paths;
+    if (nr == 1 || (gathers && !one_chunk)) {
+        for (const PendingOp& o : ops) {
+            khp_status s = o.kind == PendingOp::RENDER ? enqueue_frames(c, &o.p, nullptr, nullptr)
+                                                       : gather_now(c, &o.p, o.root);
+            if (s != KHP_OK) return s;
+        }
+        return KHP_OK;
+    }
+    return enqueue_frames(c, &first->p, nullptr, &ops);
+}
+
+extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* out_rgb) {
+    khp_status s = check_params(c, p);
+    if (s != KHP_OK) return s;
+    HIPCHK(hipSetDevice(c->device));
+    const bool stats = (c->flags & KHP_CTX_STATS) != 0 || (p->flags & KHP_RENDER_STATS) != 0;
+    const bool async = (p->flags & KHP_RENDER_ASYNC) != 0;
+    if (async && (stats || (out_rgb && !(p->flags & KHP_RENDER_NO_READBACK))))
+        return fail(KHP_EINVAL, "KHP_RENDER_ASYNC renders take no readback and no instrumentation");
+    if (!async) {
+        s = flush(c);
+        if (s != KHP_OK) return s;
+        return enqueue_frames(c, p, out_rgb, nullptr);
+    }
+    int fuse = KHP_FUSE_FRAMES_DEFAULT;
+    if (const char* e = getenv("KHP_FUSE_FRAMES")) fuse = atoi(e);
+    fuse = std::max(1, std::min(fuse, KHP_MAX_FUSE));
+    if (fuse <= 1) {
+        s = flush(c);
+        if (s != KHP_OK) return s;
+        return enqueue_frames(c, p, nullptr, nullptr);
+    }
+    for (const PendingOp& o : c->pend) {
+        if (o.kind == PendingOp::RENDER && !fusable(o.p, *p)) {
+            s = flush(c);
+            if (s != KHP_OK) return s;
+            break;
+        }
+    }
+    c->pend.push_back(PendingOp{PendingOp::RENDER, *p, 0});
+    size_t nr = 0;
+    for (const PendingOp& o : c->pend) nr += o.kind == PendingOp::RENDER;
+    if ((int)nr >= fuse) return flush(c);
+    return KHP_OK;
+}
 
 extern "C" void khp_tonemap_defaults(khp_tonemap* t) {
     if (!t) return;
@@ -2517,6 +2686,19 @@ extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint
 }
 
 extern "C" khp_status khp_gather_framebuffer(khp_ctx* c, const khp_render_params* p, int root) {
+    khp_status s = check_params(c, p);
+    if (s != KHP_OK) return s;
+    if (!c->comm) return fail(KHP_ENOTREADY, "khp_comm_init first");
+    if (root < 0 || root >= c->nranks) return fail(KHP_EINVAL, "bad root");
+    if (p->tile_nranks != (uint32_t)c->nranks) return fail(KHP_EINVAL, "tile_nranks must equal the comm size");
+    if (!c->pend.empty()) {  // behind asynchronous renders waiting for fusion: keep the call order
+        c->pend.push_back(PendingOp{PendingOp::GATHER, *p, root});
+        return KHP_OK;
+    }
+    return gather_now(c, p, root);
+}
+
+static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root) {
     khp_status s = check_params(c, p);
     if (s != KHP_OK) return s;
     if (!c->comm) return fail(KHP_ENOTREADY, "khp_comm_init first");

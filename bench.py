@@ -50,8 +50,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--strands", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -114,14 +114,17 @@ def cpu_baseline(sd, args, budget_s):
                       f"oracle BVH build {build_s:.1f} s excluded"}
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of the extend kernel from the committed PMC profile, if any."""
+def pmc_traffic(frames_per_launch: float):
+    """HBM bytes per k_extend launch from the committed PMC profile, scaled to
+    this run's frames per launch (the profile records how many fused frames
+    its launches carried), or None."""
     files = sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_extend_*.json")))
     if not files:
         return None
     try:
         with open(files[-1]) as f:
-            return json.load(f).get("bytes_per_launch")
+            d = json.load(f)
+        return int(d["bytes_per_launch"] / d.get("frames_per_launch", 1) * frames_per_launch)
     except Exception:
         return None
 
@@ -209,7 +212,11 @@ def main():
     alg_bytes_frame = 44 * rays + 32 * (cnt["node_visits"] + cnt["prim_tests"])
     launches_frame = max(1, cnt["extend_launches"])
     avg_launch_ms = ext_ms / max(1, ext_launches)
-    bytes_per_launch = alg_bytes_frame / launches_frame
+    # timed launches may carry several fused frames (KHP_FUSE_FRAMES): bytes per
+    # timed launch = the frames' algorithmic bytes / the launches they took
+    frames_timed = nfr if pipelined else args.steps
+    bytes_per_launch = alg_bytes_frame * frames_timed / max(1, ext_launches) if ext_launches else \
+        alg_bytes_frame / launches_frame
     per_launch = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     # Pipelined frames run two frames' launches side by side, so a launch's own
     # duration also counts time the chip spent on the other frame.  `achieved`
@@ -219,7 +226,7 @@ def main():
     # union is the sum of the launch durations and this is bytes/launch over
     # the average launch duration.
     achieved = (bytes_per_launch * ext_launches) / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
-    traffic = pmc_traffic()
+    traffic = pmc_traffic(frames_timed * launches_frame / max(1, ext_launches))
     out = {
         "metric": "Msamples/s at 1080p 8spp, 1M-strand hairball; achieved HBM GB/s vs peak",
         "value": round(value, 3),
@@ -266,7 +273,7 @@ def main():
             "pruned_pops_per_ray": round(cnt["extend_pruned_pops"] / max(1, rays), 3),
             "shadow_pruned_pops_per_ray": round(cnt["shadow_pruned_pops"] / max(1, cnt["shadow_rays"]), 3),
             "subframes": last.get("subframes"),
-            "pipelined": pipelined, "frames_in_flight": int(os.environ.get("KHP_FRAMES_IN_FLIGHT", "2")) if pipelined else 1,
+            "pipelined": pipelined, "fused_frames": int(os.environ.get("KHP_FUSE_FRAMES", "8")) if pipelined else 1,
             "build_s": round(build_s, 3),
             "setup": setup,
             "per_bounce": [

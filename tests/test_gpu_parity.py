@@ -149,6 +149,7 @@ def test_async_frames_in_flight(hip_ctx, fif):
     hip_ctx.build_accel()
     want = oracle_ffi.Oracle(sd).render(96, 64, 5, 5, threads=16)
     os.environ["KHP_FRAMES_IN_FLIGHT"] = fif
+    os.environ["KHP_FUSE_FRAMES"] = "1"   # frames in flight without fusion (test_fused_frames covers fusion)
     try:
         for first, n in ((0, 1), (1, 2), (3, 1), (4, 1)):
             hip_ctx.render(96, 64, n, 5, first_sample=first, async_=True)
@@ -164,6 +165,7 @@ def test_async_frames_in_flight(hip_ctx, fif):
             hip_ctx.render(96, 64, 1, 5, async_=True, stats=True)
     finally:
         os.environ.pop("KHP_FRAMES_IN_FLIGHT", None)
+        os.environ.pop("KHP_FUSE_FRAMES", None)
 
 
 def test_deterministic_across_runs(hip_ctx):
@@ -249,6 +251,42 @@ def test_single_rank_communicator():
     ctx.gather_framebuffer(16, 16, 1, 3, 64, 1, 0)
     assert np.array_equal(ctx.read_framebuffer(16, 16).view(np.uint32), a.view(np.uint32))
     ctx.close()
+
+
+@pytest.mark.parametrize("fuse", ["2", "4", "3"])
+def test_fused_frames(fuse):
+    """KHP_FUSE_FRAMES: asynchronous passes with equal parameters run as one
+    batch (one launch per bounce for all of them) and accumulate in call order
+    -- the framebuffer is the oracle's 8-spp frame; with a (1-rank) gather
+    after every pass, as bench.py does at N > 1, the gathers keep their place."""
+    from ba_pathtracing_fur_amd.pathtracer import comm_unique_id
+    sd = S.config2(72, 48, n_strands=1500)
+    want = oracle_ffi.Oracle(sd).render(72, 48, 8, 5, threads=16)
+    os.environ["KHP_FUSE_FRAMES"] = fuse
+    ctx = HipContext(0)
+    try:
+        ctx.set_scene(sd)
+        ctx.build_accel()
+        for first in range(0, 8, 2):
+            ctx.render(72, 48, 2, 5, first_sample=first, async_=True)
+        ctx.sync()
+        st = ctx.stats()
+        assert st["frames"] == 4
+        assert_parity(ctx.read_framebuffer(72, 48), want, exact=True)
+        ctx.comm_init(1, 0, comm_unique_id())
+        for first in range(0, 8, 2):
+            ctx.render(72, 48, 2, 5, first_sample=first, tile_size=64, tile_rank=0, tile_nranks=1, async_=True)
+            ctx.gather_framebuffer(72, 48, 2, 5, 64, 1, 0)
+        ctx.sync()
+        assert_parity(ctx.read_framebuffer(72, 48), want, exact=True)
+        # the same frame re-rendered every step (bench.py): the last one stays
+        for _ in range(5):
+            ctx.render(72, 48, 8, 5, async_=True)
+        ctx.sync()
+        assert_parity(ctx.read_framebuffer(72, 48), want, exact=True)
+    finally:
+        os.environ.pop("KHP_FUSE_FRAMES", None)
+        ctx.close()
 
 
 def test_native_library_is_loaded():
