@@ -66,10 +66,11 @@ struct Wave {
     int32_t* hslot;
     float* hu;
     float* hv;
-    float* T[3];
-    float* C[3];
-    int32_t* flags;
-    uint32_t* key;
+    // Per-path state, one 16-B record per array so that k_shade and
+    // k_shadow_finish, which reach paths in queue order (scattered pids after
+    // bounce 0), touch one line per array instead of one per component:
+    float4* TF;          // throughput T.xyz, BSDF flags (bits) in w
+    float4* CK;          // colour C.xyz, RNG key (bits) in w
     uint8_t* vis;        // shadow-ray occlusion flag per shadow record (this parity)
     ShadowQ* shq;        // shadow queue of this parity
     float4* sh;          // 6 float4 per shadow record
@@ -146,10 +147,8 @@ __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
     Wv.qo[0][0][pid] = r.o.x; Wv.qo[0][1][pid] = r.o.y; Wv.qo[0][2][pid] = r.o.z;
     Wv.qd[0][0][pid] = r.d.x; Wv.qd[0][1][pid] = r.d.y; Wv.qd[0][2][pid] = r.d.z;
     Wv.qpid[0][pid] = pid;
-    Wv.T[0][pid] = 1.0f; Wv.T[1][pid] = 1.0f; Wv.T[2][pid] = 1.0f;
-    Wv.C[0][pid] = 0.0f; Wv.C[1][pid] = 0.0f; Wv.C[2][pid] = 0.0f;
-    Wv.flags[pid] = 0;
-    Wv.key[pid] = key;
+    Wv.TF[pid] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));
+    Wv.CK[pid] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));
 }
 
 __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
@@ -638,10 +637,11 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
             r.d = mk(Wv.qd[cur][0][i], Wv.qd[cur][1][i], Wv.qd[cur][2][i]);
             float lambda = Wv.ht[i];
             int32_t slot = Wv.hslot[i];
-            v3 T = mk(Wv.T[0][pid], Wv.T[1][pid], Wv.T[2][pid]);
-            v3 C = mk(Wv.C[0][pid], Wv.C[1][pid], Wv.C[2][pid]);
-            int flags = Wv.flags[pid];
-            uint32_t key = Wv.key[pid];
+            const float4 tf = Wv.TF[pid], ck = Wv.CK[pid];
+            v3 T = mk(tf.x, tf.y, tf.z);
+            v3 C = mk(ck.x, ck.y, ck.z);
+            int flags = (int)bits_from_f(tf.w);
+            uint32_t key = bits_from_f(ck.w);
             // KIRK's linear ray-light test (CPU_PathTracer.cpp:185-208)
             float t_lights = FLT_MAX_;
             int t_index = -1;
@@ -770,9 +770,8 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
                     }
                 }
             }
-            Wv.T[0][pid] = T.x; Wv.T[1][pid] = T.y; Wv.T[2][pid] = T.z;
-            if (!emit_sh) { Wv.C[0][pid] = C.x; Wv.C[1][pid] = C.y; Wv.C[2][pid] = C.z; }
-            Wv.flags[pid] = flags;
+            Wv.TF[pid] = make_float4(T.x, T.y, T.z, f_from_bits((uint32_t)flags));
+            if (!emit_sh) Wv.CK[pid] = make_float4(C.x, C.y, C.z, ck.w);
             emit_ray = !last && !is_zero(T) && !is_zero(nr.d);
         }
         uint32_t qi, si;
@@ -830,9 +829,8 @@ __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
             float4 f = rec[5];
             acc = acc + mk(f.x, f.y, f.z);
         }
-        Wv.C[0][pid] = Wv.C[0][pid] + acc.x;
-        Wv.C[1][pid] = Wv.C[1][pid] + acc.y;
-        Wv.C[2][pid] = Wv.C[2][pid] + acc.z;
+        const float4 ck = Wv.CK[pid];
+        Wv.CK[pid] = make_float4(ck.x + acc.x, ck.y + acc.y, ck.z + acc.z, ck.w);
     }
 }
 
@@ -966,7 +964,8 @@ __global__ __launch_bounds__(256) void k_accumulate(Wave Wv, float* fb, uint32_t
     const size_t base = (size_t)fr * Wv.P * Wv.n_samples;
     for (uint32_t s = 0; s < Wv.n_samples; ++s) {
         size_t pid = base + (size_t)p * Wv.n_samples + s;
-        float cr = Wv.C[0][pid], cg = Wv.C[1][pid], cb = Wv.C[2][pid];
+        const float4 ck = Wv.CK[pid];
+        float cr = ck.x, cg = ck.y, cb = ck.z;
         uint32_t k = Wv.fsample0[fr] + s;
         if (k == 0) {
             r = cr; g = cg; b = cb;
@@ -1204,7 +1203,7 @@ struct TimedLaunch {
 #endif
 struct PathSet {
     size_t cap = 0;
-    DevMem qbuf[2][7], ht, hslot, hu, hv, Tb[3], Cb[3], flagsb, keyb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
+    DevMem qbuf[2][7], ht, hslot, hu, hv, TFb, CKb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
     DevMem heavyb;
     hipStream_t sA = nullptr, sB = nullptr;
 };
@@ -1595,12 +1594,8 @@ static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap) {
     HIPCHK(w.hslot.ensure(cap * 4));
     HIPCHK(w.hu.ensure(cap * 4));
     HIPCHK(w.hv.ensure(cap * 4));
-    for (int k = 0; k < 3; ++k) {
-        HIPCHK(w.Tb[k].ensure(cap * 4));
-        HIPCHK(w.Cb[k].ensure(cap * 4));
-    }
-    HIPCHK(w.flagsb.ensure(cap * 4));
-    HIPCHK(w.keyb.ensure(cap * 4));
+    HIPCHK(w.TFb.ensure(cap * sizeof(float4)));
+    HIPCHK(w.CKb.ensure(cap * sizeof(float4)));
     HIPCHK(w.heavyb.ensure(cap));
     for (int q = 0; q < 2; ++q) {
         HIPCHK(w.visb[q].ensure(cap));
@@ -1640,12 +1635,8 @@ static Wave wave_view(PathSet& w) {
     Wv.hslot = w.hslot.as<int32_t>();
     Wv.hu = w.hu.as<float>();
     Wv.hv = w.hv.as<float>();
-    for (int k = 0; k < 3; ++k) {
-        Wv.T[k] = w.Tb[k].as<float>();
-        Wv.C[k] = w.Cb[k].as<float>();
-    }
-    Wv.flags = w.flagsb.as<int32_t>();
-    Wv.key = w.keyb.as<uint32_t>();
+    Wv.TF = w.TFb.as<float4>();
+    Wv.CK = w.CKb.as<float4>();
     Wv.vis = w.visb[0].as<uint8_t>();
     Wv.sh = w.shb[0].as<float4>();
     Wv.shq = w.shqb.as<ShadowQ>();
