@@ -56,7 +56,7 @@ struct alignas(128) ShadowQ {
 };
 
 #ifndef KHP_MAX_FUSE
-#define KHP_MAX_FUSE 8
+#define KHP_MAX_FUSE 16
 #endif
 struct Wave {
     float* qo[2][3];
@@ -1215,7 +1215,7 @@ struct PathSet {
 #define KHP_FRAME_STAGGER_DEFAULT -1  // env KHP_FRAME_STAGGER (-1: frames start together; measured best)
 #endif
 #ifndef KHP_FUSE_FRAMES_DEFAULT
-#define KHP_FUSE_FRAMES_DEFAULT 8   // env KHP_FUSE_FRAMES: asynchronous frames per fused batch (measured best)
+#define KHP_FUSE_FRAMES_DEFAULT 16  // env KHP_FUSE_FRAMES: asynchronous frames per fused batch (8: 470, 16: 482-486 Msamples/s)
 #endif
 #ifndef KHP_MAX_INFLIGHT
 #define KHP_MAX_INFLIGHT 3
@@ -2237,15 +2237,53 @@ static khp_status flush(khp_ctx* c) {
     size_t cap_paths = (size_t)1 << 26;
     if (const char* e = getenv("KHP_MAX_PATHS")) cap_paths = std::max<size_t>(4096, strtoull(e, nullptr, 10));
     const bool one_chunk = P * (size_t)first->p.spp * nr <= cap_paths;
-    if (nr == 1 || (gathers && !one_chunk)) {
-        for (const PendingOp& o : ops) {
-            khp_status s = o.kind == PendingOp::RENDER ? enqueue_frames(c, &o.p, nullptr, nullptr)
-                                                       : gather_now(c, &o.p, o.root);
+    if (nr == 1 || !gathers || one_chunk) {
+        if (nr == 1) {
+            for (const PendingOp& o : ops) {
+                khp_status s = o.kind == PendingOp::RENDER ? enqueue_frames(c, &o.p, nullptr, nullptr)
+                                                           : gather_now(c, &o.p, o.root);
+                if (s != KHP_OK) return s;
+            }
+            return KHP_OK;
+        }
+        return enqueue_frames(c, &first->p, nullptr, &ops);
+    }
+    // gathers in a batch larger than one chunk: split it into consecutive
+    // groups of as many frames as one chunk holds (each with its gathers)
+    const size_t per_group = std::max<size_t>(1, cap_paths / std::max<size_t>(1, P * (size_t)first->p.spp));
+    std::vector<PendingOp> grp;
+    size_t g_r = 0;
+    auto run = [&]() -> khp_status {
+        khp_status s = KHP_OK;
+        if (g_r == 1) {
+            for (const PendingOp& o : grp) {
+                s = o.kind == PendingOp::RENDER ? enqueue_frames(c, &o.p, nullptr, nullptr) : gather_now(c, &o.p, o.root);
+                if (s != KHP_OK) break;
+            }
+        } else if (g_r > 1) {
+            const PendingOp* f0 = nullptr;
+            for (const PendingOp& o : grp)
+                if (o.kind == PendingOp::RENDER) { f0 = &o; break; }
+            s = enqueue_frames(c, &f0->p, nullptr, &grp);
+        } else {
+            for (const PendingOp& o : grp) {
+                s = gather_now(c, &o.p, o.root);
+                if (s != KHP_OK) break;
+            }
+        }
+        grp.clear();
+        g_r = 0;
+        return s;
+    };
+    for (const PendingOp& o : ops) {
+        if (o.kind == PendingOp::RENDER && g_r == per_group) {
+            khp_status s = run();
             if (s != KHP_OK) return s;
         }
-        return KHP_OK;
+        grp.push_back(o);
+        g_r += o.kind == PendingOp::RENDER;
     }
-    return enqueue_frames(c, &first->p, nullptr, &ops);
+    return run();
 }
 
 extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* out_rgb) {

@@ -50,8 +50,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=16)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--strands", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -273,7 +273,7 @@ def main():
             "pruned_pops_per_ray": round(cnt["extend_pruned_pops"] / max(1, rays), 3),
             "shadow_pruned_pops_per_ray": round(cnt["shadow_pruned_pops"] / max(1, cnt["shadow_rays"]), 3),
             "subframes": last.get("subframes"),
-            "pipelined": pipelined, "fused_frames": int(os.environ.get("KHP_FUSE_FRAMES", "8")) if pipelined else 1,
+            "pipelined": pipelined, "fused_frames": int(os.environ.get("KHP_FUSE_FRAMES", "16")) if pipelined else 1,
             "build_s": round(build_s, 3),
             "setup": setup,
             "per_bounce": [

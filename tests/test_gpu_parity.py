@@ -289,6 +289,31 @@ def test_fused_frames(fuse):
         ctx.close()
 
 
+@pytest.mark.parametrize("max_paths", ["14000", "4096"])
+def test_fused_frames_with_gathers_split(max_paths):
+    """A fused batch with gathers that does not fit one chunk is split into
+    chunk-sized groups (2 frames, or 1) that keep the call order."""
+    from ba_pathtracing_fur_amd.pathtracer import comm_unique_id
+    sd = S.config2(72, 48, n_strands=1500)
+    want = oracle_ffi.Oracle(sd).render(72, 48, 8, 5, threads=16)
+    os.environ.update(KHP_FUSE_FRAMES="4", KHP_MAX_PATHS=max_paths)
+    ctx = HipContext(0)
+    try:
+        ctx.set_scene(sd)
+        ctx.build_accel()
+        ctx.comm_init(1, 0, comm_unique_id())
+        for first in range(0, 8, 2):
+            ctx.render(72, 48, 2, 5, first_sample=first, tile_size=64, tile_rank=0, tile_nranks=1, async_=True)
+            ctx.gather_framebuffer(72, 48, 2, 5, 64, 1, 0)
+        ctx.sync()
+        assert ctx.stats()["frames"] == 4
+        assert_parity(ctx.read_framebuffer(72, 48), want, exact=True)
+    finally:
+        for k in ("KHP_FUSE_FRAMES", "KHP_MAX_PATHS"):
+            os.environ.pop(k, None)
+        ctx.close()
+
+
 def test_native_library_is_loaded():
     """The frames above came from libkirk_hip.so (no fallback exists); it must be mapped in-process."""
     maps = open("/proc/self/maps").read()
