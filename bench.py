@@ -257,6 +257,8 @@ def main():
             "bytes_per_launch": int(bytes_per_launch),
             "avg_launch_ms": round(avg_launch_ms, 4),
             "achieved_per_launch": round(per_launch, 1),
+            "frames_per_launch": round(frames_timed * launches_frame / max(1, ext_launches), 3),
+            "alg_bytes_per_frame": int(alg_bytes_frame),
             "extend_busy_ms_per_frame": round(busy_ms / max(1, nfr if pipelined else args.steps), 3),
             "achieved_def": "algorithmic bytes of all timed k_extend launches / union of their HIP-event "
                             "intervals (= bytes per launch / avg launch duration when launches do not overlap)",

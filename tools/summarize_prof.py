@@ -44,7 +44,13 @@ if pmc:
     f_ = avg("k_extend<false>", "fetch", "FETCH_SIZE")
     w_ = avg("k_extend<false>", "write", "WRITE_SIZE")
     if f_ is not None and w_ is not None:
-        fpl = int(os.environ.get("FRAMES_PER_LAUNCH", "16"))  # tools/profile.sh: 16 fused frames per launch
+        # frames carried by one k_extend launch of that run (fused frames / chunks):
+        # from the pass's own bench line, else FRAMES_PER_LAUNCH
+        fpl = float(os.environ.get("FRAMES_PER_LAUNCH", "1"))
+        try:
+            fpl = json.load(open(os.path.join(src, "fetch_bench.json")))["roofline"]["frames_per_launch"]
+        except Exception:
+            pass
         out = {"kernel": "k_extend<false>", "fetch_kb_raw": f_, "write_kb": w_,
                "bytes_per_launch": int((2 * f_ + w_) * 1024), "frames_per_launch": fpl,
                "note": "read = 2 x FETCH_SIZE (gfx950 half-count correction, MI355X_MICROARCH.md §HBM) + WRITE_SIZE; KB units"}
