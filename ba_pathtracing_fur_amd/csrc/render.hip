@@ -88,6 +88,7 @@ struct Wave {
     uint8_t* heavy;       // per queue slot: the ray's traversal took more than heavy_T iterations
     uint32_t cap;         // queue / path capacity of this set
     uint32_t heavy_T;
+    uint32_t sh_fold;     // k_shadow finishes its records (renders); 0: batch any-hit queries
 };
 
 // Longest-first queues.  A persistent traversal launch ends when its slowest
@@ -800,11 +801,9 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
 //      the deferred colour add (k_shadow_finish, SimpleShader.h:131-148) ---------------
 // k_shadow_finish: one shadow record per lane, streaming; kept out of the
 // traversal kernel so k_shadow's registers go to traversal only.
-__global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
-    const uint32_t nf = Wv.shq->nsh, n = nf + Wv.shq->nshb;
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Wv.cnt->sh_rays, (unsigned long long)n);
-    for (uint32_t iv = blockIdx.x * blockDim.x + threadIdx.x; iv < n; iv += gridDim.x * blockDim.x) {
-        const uint32_t i = q_phys(iv, nf, Wv.cap);
+// The light occlusion loop and colour add of one shadow record (SimpleShader.h:131-148).
+__device__ __forceinline__ void shadow_finish_one(const DevScene& S, const Wave& Wv, uint32_t i, bool occ) {
+    {
         const float4* rec = Wv.sh + 6 * (size_t)i;
         float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3], e = rec[4];
         uint32_t pid = bits_from_f(b.w);
@@ -812,7 +811,6 @@ __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
         r.o = mk(a.x, a.y, a.z);
         r.d = mk(b.x, b.y, b.z);
         const float tmax = a.w;
-        bool occ = Wv.vis[i] != 0;
         if (!occ) {
             for (int li = 0; li < S.n_lights; ++li) {
                 float t;
@@ -833,6 +831,24 @@ __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
         Wv.CK[pid] = make_float4(ck.x + acc.x, ck.y + acc.y, ck.z + acc.z, ck.w);
     }
 }
+
+__global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
+    const uint32_t nf = Wv.shq->nsh, n = nf + Wv.shq->nshb;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Wv.cnt->sh_rays, (unsigned long long)n);
+    for (uint32_t iv = blockIdx.x * blockDim.x + threadIdx.x; iv < n; iv += gridDim.x * blockDim.x) {
+        const uint32_t i = q_phys(iv, nf, Wv.cap);
+        shadow_finish_one(S, Wv, i, Wv.vis[i] != 0);
+    }
+}
+
+// KHP_SH_FOLD: k_shadow itself finishes its records.  A lane whose any-hit
+// test is done keeps (record, occluded) and runs shadow_finish_one at the
+// wave's next refill, together with the other idle lanes (>= REFILL of them),
+// or when the wave exits -- so the colour add costs one batched pass per
+// refill instead of a separate streaming kernel over all shadow records.
+#ifndef KHP_SH_FOLD
+#define KHP_SH_FOLD 0   // measured: no gain (k_shadow 57 -> 80 VGPRs with scratch), kept as an option
+#endif
 
 template <bool STATS>
 __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
@@ -855,9 +871,15 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
     Claimer cl;
     cl.init(Wv.shq->fetch, nf, nb, Wv.cap);
     uint32_t idx = 0;
+    bool fin = false, fin_occ = false;  // KHP_SH_FOLD: record idx awaits its finish
+    if (Wv.sh_fold && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Wv.cnt->sh_rays, (unsigned long long)(nf + nb));
     for (;;) {
         unsigned long long idle = __ballot(!has);
         if (!exhausted && __popcll(idle) >= REFILL) {
+            if (fin) {
+                shadow_finish_one(S, Wv, idx, fin_occ);
+                fin = false;
+            }
             uint32_t my;
             const bool got = cl.claim(idle, my, exhausted);
             if (!has && got) {
@@ -878,7 +900,11 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
 #else
                 has = trav_begin(S, tr, stk, c);
 #endif
-                if (!has) Wv.vis[idx] = 0;
+                if (!has) {
+                    Wv.vis[idx] = 0;
+                    fin = Wv.sh_fold != 0;
+                    fin_occ = false;
+                }
             }
         }
         unsigned long long act = __ballot(has);
@@ -902,6 +928,8 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
                 Hit hu_{0.0f, -1, 0.0f, 0.0f};
                 if (iter2<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ, tail_pf, pf)) {
                     Wv.vis[idx] = occ ? 1 : 0;
+                    fin = Wv.sh_fold != 0;
+                    fin_occ = occ;
                     has = false;
                 }
             }
@@ -935,6 +963,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
             if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
     }
+    if (fin) shadow_finish_one(S, Wv, idx, fin_occ);
     if (STATS) {
         unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
         unsigned long long pr = wave_sum((unsigned long long)st.pruned);
@@ -2042,6 +2071,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         Wv.H = p->height;
         Wv.seed = p->seed;
         Wv.depth = p->depth;
+        Wv.sh_fold = (KHP_SH_FOLD && KHP_LOOP2 && !getenv("KHP_NO_SH_FOLD")) ? 1u : 0u;
         SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
         SpillArea sp_sh{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
         for (uint32_t p0 = set_p0; p0 < set_p1; p0 += P_chunk[k]) {
@@ -2107,9 +2137,11 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     else
                         hipLaunchKernelGGL(k_shadow<false>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES_SH, sB, c->S, Wb, sp_sh);
                     timed(c, f, 2, false, sB);
-                    timed(c, f, 2, true, sB);   // shadow stage = any-hit traversal + finish
-                    hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
-                    timed(c, f, 2, false, sB);
+                    if (!Wb.sh_fold) {
+                        timed(c, f, 2, true, sB);   // shadow stage = any-hit traversal + finish
+                        hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
+                        timed(c, f, 2, false, sB);
+                    }
                     if (sB != sA) {
                         done_b = slot_event(f.sync_pool, f.sync_next, true);
                         HIPCHK(hipEventRecord(done_b, sB));
