@@ -871,15 +871,17 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
     Claimer cl;
     cl.init(Wv.shq->fetch, nf, nb, Wv.cap);
     uint32_t idx = 0;
-    bool fin = false, fin_occ = false;  // KHP_SH_FOLD: record idx awaits its finish
+    [[maybe_unused]] bool fin = false, fin_occ = false;  // KHP_SH_FOLD: record idx awaits its finish
     if (Wv.sh_fold && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Wv.cnt->sh_rays, (unsigned long long)(nf + nb));
     for (;;) {
         unsigned long long idle = __ballot(!has);
         if (!exhausted && __popcll(idle) >= REFILL) {
+#if KHP_SH_FOLD
             if (fin) {
                 shadow_finish_one(S, Wv, idx, fin_occ);
                 fin = false;
             }
+#endif
             uint32_t my;
             const bool got = cl.claim(idle, my, exhausted);
             if (!has && got) {
@@ -963,7 +965,9 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
             if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
     }
+#if KHP_SH_FOLD
     if (fin) shadow_finish_one(S, Wv, idx, fin_occ);
+#endif
     if (STATS) {
         unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
         unsigned long long pr = wave_sum((unsigned long long)st.pruned);
@@ -2071,7 +2075,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         Wv.H = p->height;
         Wv.seed = p->seed;
         Wv.depth = p->depth;
-        Wv.sh_fold = (KHP_SH_FOLD && KHP_LOOP2 && !getenv("KHP_NO_SH_FOLD")) ? 1u : 0u;
+        Wv.sh_fold = (KHP_SH_FOLD && KHP_LOOP2 && !getenv("KHP_NO_SH_FOLD")) ? 1u : 0u;  // compile-time option
         SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
         SpillArea sp_sh{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
         for (uint32_t p0 = set_p0; p0 < set_p1; p0 += P_chunk[k]) {
