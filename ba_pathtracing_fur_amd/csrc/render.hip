@@ -188,6 +188,10 @@ __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
 constexpr int RING = KHP_RING;        // k_extend LDS ring entries per lane (3 x 4 B each)
 constexpr int RING_SH = KHP_RING_SH;  // k_shadow
 constexpr int REFILL = KHP_REFILL;  // refill when >= REFILL lanes are idle
+#ifndef KHP_REFILL_SH
+#define KHP_REFILL_SH KHP_REFILL   // k_shadow: any-hit rays are short and end early
+#endif
+constexpr int REFILL_SH = KHP_REFILL_SH;
 constexpr size_t LDS_BYTES = 3 * RING * TRAV_BLOCK * sizeof(uint32_t);
 constexpr size_t LDS_BYTES_SH = 3 * RING_SH * TRAV_BLOCK * sizeof(uint32_t);
 
@@ -875,7 +879,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
     if (Wv.sh_fold && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Wv.cnt->sh_rays, (unsigned long long)(nf + nb));
     for (;;) {
         unsigned long long idle = __ballot(!has);
-        if (!exhausted && __popcll(idle) >= REFILL) {
+        if (!exhausted && __popcll(idle) >= REFILL_SH) {
 #if KHP_SH_FOLD
             if (fin) {
                 shadow_finish_one(S, Wv, idx, fin_occ);
@@ -962,7 +966,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
 #if KHP_EXP_ABANDON   // timing experiment only (wrong results): sparse waves drop their rays once the queue is drained
             if (exhausted && (uint32_t)__popcll(act) <= (uint32_t)KHP_EXP_ABANDON) { has = false; act = 0; }
 #endif
-            if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
+            if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL_SH)) break;
         }
     }
 #if KHP_SH_FOLD
