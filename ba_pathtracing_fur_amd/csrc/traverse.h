@@ -836,6 +836,9 @@ __device__ __forceinline__ bool trav2_begin(const DevScene& S, const TravRay& tr
 #ifndef KHP_TAIL_PF
 #define KHP_TAIL_PF 1
 #endif
+#ifndef KHP_ANY_PAIR
+#define KHP_ANY_PAIR 0
+#endif
 #ifndef KHP_TAIL_PF_LANES
 #define KHP_TAIL_PF_LANES 64   // prefetch when the queue is drained and at most this many lanes are busy
 #endif
@@ -851,12 +854,27 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
     const bool fetch = in_leaf || mode == M_NODE;
     const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
     float4 q0, q1, q2, q3;
+    // KHP_ANY_PAIR: an any-hit lane in a leaf with >= 2 candidates left loads
+    // and tests the next candidate too (same 128-B line for even-aligned leaf
+    // pairs).  Any-hit results do not depend on the order of tests, and the
+    // instrumented count stops at the first occluder as KIRK's loop does.
+    const bool pair = KHP_ANY_PAIR && ANY && in_leaf && lf.left >= 2u;
+    float4 q4, q5, q6, q7;
     if (fetch) {
         q0 = p[0];
         q1 = p[1];
         q2 = p[2];
         q3 = p[3];
+        if (pair) {
+            q4 = p[4];
+            q5 = p[5];
+            q6 = p[6];
+            q7 = p[7];
+        }
         pin(q0); pin(q1); pin(q2); pin(q3);
+        if (pair) {
+            pin(q4); pin(q5); pin(q6); pin(q7);
+        }
     }
 #if KHP_TAIL_PF
     asm volatile("" : "+v"(pf.d0), "+v"(pf.d1));  // prefetches issued last iteration are complete here
@@ -874,6 +892,15 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
             if (any_candidate(q0, q1, q2, q3, tr.r, tmax_any)) {
                 occluded = true;
                 return true;
+            }
+            if (pair) {
+                if (STATS) st.prims++;
+                if (any_candidate(q4, q5, q6, q7, tr.r, tmax_any)) {
+                    occluded = true;
+                    return true;
+                }
+                ++lf.slot;
+                --lf.left;
             }
         } else {
             leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);
