@@ -1898,7 +1898,10 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     if (!async || geometry_change) {  // a synchronous render (or new buffers) first completes the in-flight frames
         s = drain(c);
         if (s != KHP_OK) return s;
-        c->report_open = false;
+        // An asynchronous frame on new buffers keeps accumulating into the
+        // report opened since the last khp_sync; only a synchronous render
+        // starts a fresh one.
+        if (!async) c->report_open = false;
     }
     if (!async) report_begin(c);
     else if (!c->report_open) report_begin(c);

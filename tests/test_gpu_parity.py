@@ -314,6 +314,34 @@ def test_fused_frames_with_gathers_split(max_paths):
         ctx.close()
 
 
+def test_async_frames_across_changes():
+    """Pending/fused asynchronous frames are completed before anything that
+    changes what they read: a different frame size (new framebuffer), a new
+    scene, a synchronous read."""
+    sd = S.config2(48, 32, n_strands=800)
+    sd2 = S.config1(40, 24)
+    ctx = HipContext(0)
+    try:
+        ctx.set_scene(sd)
+        ctx.build_accel()
+        for _ in range(3):
+            ctx.render(48, 32, 2, 5, async_=True)
+        ctx.render(40, 24, 2, 5, async_=True)        # new geometry: the 48x32 frames are flushed first
+        ctx.sync()
+        assert ctx.stats()["frames"] == 4
+        assert_parity(ctx.read_framebuffer(40, 24), oracle_ffi.Oracle(sd).render(40, 24, 2, 5, threads=16),
+                      exact=True)
+        ctx.render(40, 24, 3, 5, async_=True)
+        ctx.set_scene(sd2)                           # scene change with a frame pending
+        ctx.build_accel()
+        got = ctx.render(40, 24, 2, 4)
+        assert_parity(got, oracle_ffi.Oracle(sd2).render(40, 24, 2, 4, threads=16), exact=True)
+        assert ctx.lib.khp_render(ctx.ptr, None, None) != 0   # null parameters: an error status, no crash
+        assert ctx.lib.khp_sync(None) != 0
+    finally:
+        ctx.close()
+
+
 def test_native_library_is_loaded():
     """The frames above came from libkirk_hip.so (no fallback exists); it must be mapped in-process."""
     maps = open("/proc/self/maps").read()
