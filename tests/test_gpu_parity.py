@@ -289,6 +289,37 @@ def test_fused_frames(fuse):
         ctx.close()
 
 
+def test_fused_full_size_matches_passes():
+    """The metric scene (1M strands, 1080p): 16 progressive 4-spp passes
+    fused into one batch (133M paths: 2 chunks at the default 2^26 paths per
+    chunk, 1 at 2^27) give the framebuffer of the same passes rendered one by
+    one, bit for bit; sampled rows are the oracle's 64-spp frame."""
+    ctx = HipContext(0)
+    try:
+        sd = S.config3_device(ctx, 1920, 1080, n_strands=1_000_000)
+        ctx.build_accel()
+        for k in range(16):
+            ctx.render(1920, 1080, 4, 5, first_sample=4 * k, readback=False)
+        want = ctx.read_framebuffer(1920, 1080)
+        for cap in (None, str(1 << 27)):
+            if cap:
+                os.environ["KHP_MAX_PATHS"] = cap
+            try:
+                for k in range(16):
+                    ctx.render(1920, 1080, 4, 5, first_sample=4 * k, async_=True)
+                ctx.sync()
+            finally:
+                os.environ.pop("KHP_MAX_PATHS", None)
+            assert ctx.stats()["frames"] == 16
+            assert np.array_equal(ctx.read_framebuffer(1920, 1080).view(np.uint32), want.view(np.uint32)), cap
+        host = S.config3(1920, 1080, n_strands=1_000_000)
+        rows = list(range(7, 1080, 270))
+        ref = oracle_ffi.Oracle(host).render(1920, 1080, 64, 5, threads=16, rows=(7, 1080, 270))
+        assert_parity(want[rows], ref[rows], exact=True)
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("max_paths", ["14000", "4096"])
 def test_fused_frames_with_gathers_split(max_paths):
     """A fused batch with gathers that does not fit one chunk is split into
