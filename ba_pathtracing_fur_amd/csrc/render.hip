@@ -1715,6 +1715,12 @@ static khp_status prepare_pixels(khp_ctx* c, const khp_render_params* p) {
     return KHP_OK;
 }
 
+// Paths per wavefront chunk (KHP_MAX_PATHS overrides).  A chunk's path state
+// is ~200 B per path, 27 GB at 2^27; at the metric row a 16-frame batch is two
+// such chunks (2^26: four chunks, 1.2% slower; 2^28: one chunk, 1% slower, as
+// its last shadow launch and accumulate then overlap no other chunk).
+static const size_t KHP_CHUNK_PATHS_DEFAULT = (size_t)1 << 27;
+
 static khp_status check_params(khp_ctx* c, const khp_render_params* p) {
     if (!c || !p) return fail(KHP_EINVAL, "null argument");
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
@@ -1962,7 +1968,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     if (nf > 1) K = 1;  // a fused batch is one path set
     f.K = K;
     f.nf = nf;
-    size_t cap_paths = (size_t)1 << 26;
+    size_t cap_paths = KHP_CHUNK_PATHS_DEFAULT;
     if (const char* e = getenv("KHP_MAX_PATHS")) cap_paths = std::max<size_t>(4096, strtoull(e, nullptr, 10));
     uint32_t pix_lo[KHP_MAX_SUBFRAMES + 1], spp_lo[KHP_MAX_SUBFRAMES + 1];
     for (int k = 0; k <= K; ++k) {
@@ -2277,7 +2283,7 @@ static khp_status flush(khp_ctx* c) {
             P = tmp.size();
         }
     }
-    size_t cap_paths = (size_t)1 << 26;
+    size_t cap_paths = KHP_CHUNK_PATHS_DEFAULT;
     if (const char* e = getenv("KHP_MAX_PATHS")) cap_paths = std::max<size_t>(4096, strtoull(e, nullptr, 10));
     const bool one_chunk = P * (size_t)first->p.spp * nr <= cap_paths;
     if (nr == 1 || !gathers || one_chunk) {

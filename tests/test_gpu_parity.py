@@ -291,8 +291,8 @@ def test_fused_frames(fuse):
 
 def test_fused_full_size_matches_passes():
     """The metric scene (1M strands, 1080p): 16 progressive 4-spp passes
-    fused into one batch (133M paths: 2 chunks at the default 2^26 paths per
-    chunk, 1 at 2^27) give the framebuffer of the same passes rendered one by
+    fused into one batch (133M paths: 1 chunk at the default 2^27 paths per
+    chunk, 2 at 2^26) give the framebuffer of the same passes rendered one by
     one, bit for bit; sampled rows are the oracle's 64-spp frame."""
     ctx = HipContext(0)
     try:
@@ -301,7 +301,7 @@ def test_fused_full_size_matches_passes():
         for k in range(16):
             ctx.render(1920, 1080, 4, 5, first_sample=4 * k, readback=False)
         want = ctx.read_framebuffer(1920, 1080)
-        for cap in (None, str(1 << 27)):
+        for cap in (None, str(1 << 26)):
             if cap:
                 os.environ["KHP_MAX_PATHS"] = cap
             try:
