@@ -56,7 +56,7 @@ struct alignas(128) ShadowQ {
 };
 
 #ifndef KHP_MAX_FUSE
-#define KHP_MAX_FUSE 16
+#define KHP_MAX_FUSE 32
 #endif
 struct Wave {
     float* qo[2][3];
@@ -1252,7 +1252,7 @@ struct PathSet {
 #define KHP_FRAME_STAGGER_DEFAULT -1  // env KHP_FRAME_STAGGER (-1: frames start together; measured best)
 #endif
 #ifndef KHP_FUSE_FRAMES_DEFAULT
-#define KHP_FUSE_FRAMES_DEFAULT 16  // env KHP_FUSE_FRAMES: asynchronous frames per fused batch (8: 470, 16: 482-486 Msamples/s)
+#define KHP_FUSE_FRAMES_DEFAULT 32  // env KHP_FUSE_FRAMES: asynchronous frames per fused batch (8: 470, 16: 485-487, 32: 497 Msamples/s)
 #endif
 #ifndef KHP_MAX_INFLIGHT
 #define KHP_MAX_INFLIGHT 3

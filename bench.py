@@ -275,7 +275,7 @@ def main():
             "pruned_pops_per_ray": round(cnt["extend_pruned_pops"] / max(1, rays), 3),
             "shadow_pruned_pops_per_ray": round(cnt["shadow_pruned_pops"] / max(1, cnt["shadow_rays"]), 3),
             "subframes": last.get("subframes"),
-            "pipelined": pipelined, "fused_frames": int(os.environ.get("KHP_FUSE_FRAMES", "16")) if pipelined else 1,
+            "pipelined": pipelined, "fused_frames": min(args.steps, int(os.environ.get("KHP_FUSE_FRAMES", "32"))) if pipelined else 1,
             "build_s": round(build_s, 3),
             "setup": setup,
             "per_bounce": [
