@@ -836,6 +836,9 @@ __device__ __forceinline__ bool trav2_begin(const DevScene& S, const TravRay& tr
 #ifndef KHP_TAIL_PF
 #define KHP_TAIL_PF 1
 #endif
+#ifndef KHP_ANY_ORDER
+#define KHP_ANY_ORDER 0  // any-hit child order: 0 KIRK's (near first), 1 far, 2 leaf, 3 longer overlap
+#endif
 #ifndef KHP_ANY_PAIR
 #define KHP_ANY_PAIR 0
 #endif
@@ -931,7 +934,21 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
         lh = lh && !(l1 < 0.0f || l0 > tlimit);
         rh = rh && !(r1 < 0.0f || r0 > tlimit);
         const uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
-        const bool nearl = lh && (!rh || l0 < r0);  // KIRK: left first iff l0 < r0 (ties: right)
+        bool nearl = lh && (!rh || l0 < r0);  // KIRK: left first iff l0 < r0 (ties: right)
+#if KHP_ANY_ORDER
+        // any-hit: the boolean does not depend on the visiting order (every
+        // entry KIRK would test is still tested until the first hit)
+        if (ANY && lh && rh) {
+#if KHP_ANY_ORDER == 1
+            nearl = !nearl;  // far child first
+#elif KHP_ANY_ORDER == 2
+            const bool ll = ref_leaf(lref), rl = ref_leaf(rref);
+            if (ll != rl) nearl = ll;  // a leaf child first
+#elif KHP_ANY_ORDER == 3
+            nearl = (l1 - l0) >= (r1 - r0);  // longer overlap first
+#endif
+        }
+#endif
         have = lh || rh;
         need_pop = !have;
         push = lh && rh;
