@@ -720,6 +720,9 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
                         sh_tmax = length(lightpos - h2l.o);
                         shr = h2l;
                         need_shadow = true;
+#ifdef KHP_DBG_LC0
+                        if (lc.x == 0.0f && lc.y == 0.0f && lc.z == 0.0f) atomicAdd(&Wv.cnt->sh_pruned, 1ull);
+#endif
                     }
                 }
                 v3 ev = bsdf_eval(s, nrm, nrm);
@@ -766,8 +769,17 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
                     }
                 }
                 if (add_now) {
-                    if (need_shadow) {
+                    if (need_shadow && !(lc.x == 0.0f && lc.y == 0.0f && lc.z == 0.0f)) {
                         emit_sh = true;  // colour is added by k_shadow
+                    } else if (need_shadow) {
+                        // Zero light colour (~30% of the metric row's shadow rays, mostly
+                        // hair lobes that vanish): shadow_finish_one's lc * (occ ? 0 : 1)
+                        // is lc itself for +-0, so the any-hit result cannot change the
+                        // colour and the ray is not traced.  Same operations as the finish.
+                        v3 dl = mk(0, 0, 0) + lc * 1.0f;
+                        v3 acc = (mk(0, 0, 0) + dl * Told) + AT;
+                        if (has_emit) acc = acc + ET;
+                        C = C + acc;
                     } else {
                         v3 acc = (mk(0, 0, 0) + mk(0, 0, 0) * Told) + AT;
                         if (has_emit) acc = acc + ET;
