@@ -42,7 +42,7 @@ struct alignas(128) Counters {
     unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests, spills;
     unsigned long long pruned, sh_pruned;  // entries popped only to fail the prune test
     unsigned long long iters, lanes_busy, sh_iters, sh_lanes_busy;  // wave iterations, lanes with work
-    unsigned long long step_cycles[4];  // KHP_PROFILE_STEPS: resolve, fetch, compute, loop/refill (extend)
+    unsigned long long step_cycles[4];  // unused (khp_stats.step_cycles stays 0)
 };
 
 // One bounce's shadow-ray queue (count + claim cursors).  Two of them
@@ -88,7 +88,6 @@ struct Wave {
     uint8_t* heavy;       // per queue slot: the ray's traversal took more than heavy_T iterations
     uint32_t cap;         // queue / path capacity of this set
     uint32_t heavy_T;
-    uint32_t sh_fold;     // k_shadow finishes its records (renders); 0: batch any-hit queries
 };
 
 // Longest-first queues.  A persistent traversal launch ends when its slowest
@@ -170,36 +169,15 @@ __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
 // idle, the wave claims that many new rays with a single atomic and the idle
 // lanes start them, so a wave never waits for its slowest ray to admit new
 // work (Aila & Laine's persistent "while-while" with speculative refill).
-#ifndef KHP_RING
-#define KHP_RING 8
-#endif
-#ifndef KHP_REFILL
-#define KHP_REFILL 24   // measured: 16 -> 24 +2.5 %, 32 and 40 slower
-#endif
-#ifndef KHP_TRAV_WAVES
-#define KHP_TRAV_WAVES 6   // 65 VGPRs without SLP packing; 6 x 24 KB LDS rings fill 144 of 160 KB (measured best)
-#endif
-#ifndef KHP_SH_WAVES
-#define KHP_SH_WAVES KHP_TRAV_WAVES
-#endif
-#ifndef KHP_RING_SH
-#define KHP_RING_SH KHP_RING
-#endif
-constexpr int RING = KHP_RING;        // k_extend LDS ring entries per lane (3 x 4 B each)
-constexpr int RING_SH = KHP_RING_SH;  // k_shadow
-constexpr int REFILL = KHP_REFILL;  // refill when >= REFILL lanes are idle
-#ifndef KHP_REFILL_SH
-#define KHP_REFILL_SH KHP_REFILL   // k_shadow: any-hit rays are short and end early
-#endif
-constexpr int REFILL_SH = KHP_REFILL_SH;
+// Measured on the metric row: 8-entry LDS rings, refill at 24
+// idle lanes and 6 waves per SIMD (72 VGPRs, 6 x 24 KB of LDS rings per CU)
+// are the best of the variants tried.
+constexpr int RING = 8;        // LDS ring entries per lane (3 x 4 B each)
+constexpr int REFILL = 24;     // refill when >= REFILL lanes are idle
+constexpr int TRAV_WAVES = 6;  // __launch_bounds__ waves per SIMD
 constexpr size_t LDS_BYTES = 3 * RING * TRAV_BLOCK * sizeof(uint32_t);
-constexpr size_t LDS_BYTES_SH = 3 * RING_SH * TRAV_BLOCK * sizeof(uint32_t);
-
-#ifndef KHP_TOPREG
-#define KHP_TOPREG 0   // 1: stack top in registers with a prefetched next top (exact; measured 16 % slower)
-#endif
-template <int R, bool COUNT>
-using TravStack = typename std::conditional<KHP_TOPREG != 0, LdsStackT<R, COUNT>, LdsStack<R, COUNT>>::type;
+template <bool STATS>
+using TravStack = LdsStack<RING, STATS>;
 
 struct SpillArea {
     int4* base;
@@ -209,21 +187,14 @@ struct SpillArea {
 // Work claiming with L2 affinity.  Blocks b and b+8 run on the same XCD
 // (round-robin placement -- used for speed only, never for correctness), and
 // each XCD has its own 4 MiB L2.  The queue is cut into NSEG contiguous
-// segments; the waves of block group g = blockIdx.x % 8 drain segment g first,
-// so each L2 serves one band of the frame (primary rays: a band of tiles;
-// secondary and shadow rays: the matching region of the scene), then move on
-// to the next segments so no XCD idles at the end of the launch.
-#ifndef KHP_XCD_SPLIT
-#define KHP_XCD_SPLIT 1
-#endif
-#ifndef KHP_SEG_PER_XCD
-#define KHP_SEG_PER_XCD 4   // sub-segments per XCD group: spreads claim atomics over more lines
-#endif
-constexpr uint32_t NSEG = KHP_XCD_SPLIT ? 8u * KHP_SEG_PER_XCD : 1u;
-
-#ifndef KHP_CLAIM_CHUNK
-#define KHP_CLAIM_CHUNK 0   // >0: indices a wave reserves per atomic (measured: no gain once cursors are line-padded)
-#endif
+// segments; the waves of block group g = blockIdx.x % 8 drain segments
+// [g*K, g*K + K) first, so each L2 serves one band of the frame (primary rays:
+// a band of tiles; secondary and shadow rays: the matching region of the
+// scene), then move on to the next segments so no XCD idles at the end of the
+// launch.  K = 4 sub-segments per XCD spread the claim atomics over more lines.
+constexpr uint32_t SEG_PER_XCD = 4;
+constexpr uint32_t NSEG = 8u * SEG_PER_XCD;
+static_assert(NSEG <= KHP_MAX_SEG, "claim cursors");
 struct Claimer {
     uint32_t* fetch;  // NSEG cursors, one 128-B line each
     uint32_t n;       // queue length
@@ -231,7 +202,7 @@ struct Claimer {
     uint32_t sg;      // segment this wave is draining (wave-uniform)
     uint32_t rseg;    // segment of the current reservation
     uint32_t tried;   // segments found exhausted
-    uint32_t res_lo, res_hi;  // reserved, not yet handed out (KHP_CLAIM_CHUNK)
+    uint32_t res_lo, res_hi;  // reserved, not yet handed out
     // Segment g holds the front-part slice [nf*g/NSEG, nf*(g+1)/NSEG) followed by
     // the back-part slice [nl*g/NSEG, nl*(g+1)/NSEG): long rays first everywhere.
     __device__ __forceinline__ void init(uint32_t* f, uint32_t front, uint32_t back, uint32_t capacity) {
@@ -241,8 +212,7 @@ struct Claimer {
         cap = capacity;
         n = front + back;
         rseg = 0;
-        // group g = blockIdx % 8 (one XCD) owns the contiguous segments [g*K, g*K + K)
-        sg = NSEG > 1 ? (blockIdx.x % 8u) * (NSEG / 8u) + (blockIdx.x / 8u) % (NSEG / 8u) : 0u;
+        sg = (blockIdx.x % 8u) * SEG_PER_XCD + (blockIdx.x / 8u) % SEG_PER_XCD;
         tried = 0;
         res_lo = res_hi = 0;
     }
@@ -277,7 +247,7 @@ struct Claimer {
     __device__ __forceinline__ bool claim(unsigned long long idle, uint32_t& my, bool& done) {
         const uint32_t lane = lane_id();
         const uint32_t k = (uint32_t)__popcll(idle);
-        reserve(KHP_CLAIM_CHUNK > 0 && KHP_CLAIM_CHUNK > k ? (uint32_t)KHP_CLAIM_CHUNK : k);
+        reserve(k);
         const uint32_t avail = res_hi - res_lo, take = k < avail ? k : avail;
         const uint32_t off = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
         my = res_lo + off;
@@ -288,90 +258,43 @@ struct Claimer {
     }
 };
 
-// ---- extend: closest hit for every queued ray ------------------------------------------
-#ifndef KHP_WW
-#define KHP_WW 0   // 1: while-while phases (measured 35 % slower: waves wait for the longest interior run); 0: if-if
-#endif
-#ifndef KHP_PROFILE_STEPS
-#define KHP_PROFILE_STEPS 0   // diagnostic build: s_memtime per traversal phase (instrumented kernels)
-#endif
-#ifndef KHP_ONEFETCH
-#define KHP_ONEFETCH 1   // one record fetch per lane per iteration (nodes and candidates alike)
-#endif
-#ifndef KHP_WW_EXT
-#define KHP_WW_EXT KHP_WW
-#endif
-#ifndef KHP_WW_SH
-#define KHP_WW_SH KHP_WW
-#endif
-
-// One traversal round of a wave.  KHP_WW: every lane with an interior entry
-// keeps descending until its entry is a leaf (or it runs out), then all lanes
-// holding a leaf test it together.  A lane never moves past its own leaf
-// before testing it, so each ray's visit order -- and therefore its result --
-// is exactly KIRK's; only the interleaving of lanes changes.
-template <bool STATS, bool WW, class LeafFn, class Stack>
-__device__ __forceinline__ void trav_round(const DevScene& S, const TravRay& tr, float tlimit_in, bool has, Stack& stk,
-                                           Cur& c, TravStats& st, LeafFn leaf, const float* tlimit_live) {
-    if (!has) return;
-    if (WW) {
-        // per-lane loop: the wave keeps issuing interior steps until every lane
-        // holds a leaf (or is done).  NB: a ballot-controlled form of this loop
-        // (exit when __ballot(interior) == 0) was measured to corrupt other
-        // lanes' traversal state on gfx950 / ROCm 7.2; keep the plain while.
-        while (cur_interior(c)) interior_step<STATS>(S, tr, *tlimit_live, stk, c, st);
-        if (cur_leaf(c)) leaf();
-    } else if (c.valid) {
-        if (ref_leaf(c.ref)) leaf();
-        else interior_step<STATS>(S, tr, *tlimit_live, stk, c, st);
+// Adds one traversal kernel's instrumented counters to the wavefront counters.
+template <class Stack>
+__device__ __forceinline__ void flush_stats(const TravStats& st, const Stack& stk, unsigned long long wit,
+                                            unsigned long long wbusy, unsigned long long* nodes,
+                                            unsigned long long* prims, unsigned long long* pruned,
+                                            unsigned long long* iters, unsigned long long* busy,
+                                            unsigned long long* spills) {
+    const unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
+    const unsigned long long pr = wave_sum((unsigned long long)st.pruned);
+    const unsigned long long sp = wave_sum((unsigned long long)stk.spills);
+    if (lane_id() == 0) {
+        atomicAdd(nodes, a);
+        atomicAdd(prims, b);
+        atomicAdd(pruned, pr);
+        atomicAdd(iters, wit);
+        atomicAdd(busy, wbusy);
+        atomicAdd(spills, sp);
     }
 }
 
-#ifndef KHP_TAIL_PROBE
-#define KHP_TAIL_PROBE 0
-#endif
-// Tail priority: once a launch's queue is drained, the rays still in flight
-// set its end, and with frames in flight they compete for issue slots with
-// the other frame's bulk waves; raising the wave priority (s_setprio) lets
-// them issue first.
-#ifndef KHP_TAIL_PRIO
-#define KHP_TAIL_PRIO 0
-#endif
-#if KHP_TAIL_PROBE
-#define KHP_TAIL_PROBE_WAVES 65536
-__device__ unsigned long long g_tail_probe[6 * KHP_TAIL_PROBE_WAVES];
-extern "C" int khp_debug_tail_probe(unsigned long long* out, int reset) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_tail_probe)) != hipSuccess) return 1;
-    if (reset) return hipMemset(p, 0, sizeof(g_tail_probe)) == hipSuccess ? 0 : 1;
-    return hipMemcpy(out, p, sizeof(g_tail_probe), hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
-}
-#endif
+// ---- extend: closest hit for every queued ray ------------------------------------------
 template <bool STATS>
-__global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
+__global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t nf = Wv.cnt->nq[cur], nb = Wv.cnt->nqb[cur];
-    TravStack<RING, STATS> stk;
+    TravStack<STATS> stk;
     stk.init(lds, spill.base, spill.stride);
-    TravStats st{0, 0};
+    TravStats st{0, 0, 0};
     TravRay tr;
     Hit h;
     Cur c{0u, 0.0f, 0.0f, false};
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
-    [[maybe_unused]] Prefetch pf{0.0f, 0.0f};
+    Prefetch pf{0.0f, 0.0f};
     bool has = false, exhausted = false;
     uint32_t idx = 0, mode = 0u;
     unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
-#if KHP_PROFILE_STEPS
-    uint64_t prof[4] = {0, 0, 0, 0}, prof_last = __builtin_amdgcn_s_memtime(), prof_t0 = prof_last;
-#endif
     uint32_t it = 0;  // this lane's iterations on its current ray (longest-first queues)
-#if KHP_TAIL_PROBE
-    // diagnostic build: per wave [start, queue drained, end] (s_memrealtime,
-    // 100 MHz), rays started, longest ray (iterations), iterations after the drain
-    uint64_t tp_start = __builtin_amdgcn_s_memrealtime(), tp_ex = 0;
-    uint32_t tp_rays = 0, tp_max = 0, tp_after = 0;
-#endif
     Claimer cl;
     cl.init(Wv.cnt->fetch_ext, nf, nb, Wv.cap);
     for (;;) {
@@ -382,9 +305,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene 
             if (!has && got) {
                 idx = cl.phys(my);
                 it = 0;
-#if KHP_TAIL_PROBE
-                ++tp_rays;
-#endif
                 Ray r;
                 r.o = mk(Wv.qo[cur][0][idx], Wv.qo[cur][1][idx], Wv.qo[cur][2][idx]);
                 r.d = mk(Wv.qd[cur][0][idx], Wv.qd[cur][1][idx], Wv.qd[cur][2][idx]);
@@ -393,11 +313,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene 
                 h.slot = -1;
                 h.u = h.v = 0.0f;
                 lf.left = 0;
-#if KHP_LOOP2
                 has = trav2_begin<STATS>(S, tr, h.t, stk, mode, c, lf, st);
-#else
-                has = trav_begin(S, tr, stk, c);
-#endif
                 if (!has) {  // missed the root box
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = -1;
@@ -413,17 +329,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene 
             continue;
         }
         for (;;) {
-#if KHP_LOOP2
-#if KHP_TAIL_PROBE
-            if (exhausted) {
-                if (tp_ex == 0) tp_ex = __builtin_amdgcn_s_memrealtime();
-                ++tp_after;
-            }
-#endif
-            const bool tail_pf = KHP_TAIL_PF && exhausted && __popcll(act) <= KHP_TAIL_PF_LANES;
-#if KHP_TAIL_PRIO
-            if (exhausted) __builtin_amdgcn_s_setprio(KHP_TAIL_PRIO);  // drained queue: this wave's rays end the launch
-#endif
             if (STATS) {
                 unsigned long long wm = __ballot(has && (mode == M_NODE || mode == M_LEAF));
                 ++wit;
@@ -432,113 +337,22 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene 
             if (has) {
                 bool occ_unused;
                 ++it;
-                if (iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused, tail_pf, pf)) {
+                if (iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused, exhausted, pf)) {
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = h.slot;
                     Wv.hu[idx] = h.u;
                     Wv.hv[idx] = h.v;
                     Wv.heavy[idx] = it > Wv.heavy_T ? 1 : 0;
-#if KHP_TAIL_PROBE
-                    tp_max = it > tp_max ? it : tp_max;
-#endif
                     has = false;
                 }
             }
-#elif KHP_ONEFETCH
-#if KHP_PROFILE_STEPS
-            uint64_t tp0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
-#endif
-            const bool work = has && resolve<STATS>(S, h.t, stk, c, lf, st);
-            if (has && !work) {
-                Wv.ht[idx] = h.t;
-                Wv.hslot[idx] = h.slot;
-                Wv.hu[idx] = h.u;
-                Wv.hv[idx] = h.v;
-                has = false;
-            }
-            if (STATS) {
-                unsigned long long wm = __ballot(work);
-                ++wit;
-                wbusy += (uint32_t)__popcll(wm);
-            }
-#if KHP_PROFILE_STEPS
-            if (STATS) {
-                uint64_t tp1 = __builtin_amdgcn_s_memtime();
-                float4 q0, q1, q2, q3;
-                if (work) {
-                    const float4* pp = work_record(S, c, lf);
-                    q0 = pp[0]; q1 = pp[1]; q2 = pp[2]; q3 = pp[3];
-                    pin(q0); pin(q1); pin(q2); pin(q3);
-                }
-                uint64_t tp2 = __builtin_amdgcn_s_memtime();
-                if (work) step1_closest_rec<STATS>(tr, h, stk, c, lf, st, q0, q1, q2, q3);
-                uint64_t tp3 = __builtin_amdgcn_s_memtime();
-                prof[0] += tp1 - tp0;
-                prof[1] += tp2 - tp1;
-                prof[2] += tp3 - tp2;
-                prof_last = tp3;
-            } else
-#endif
-            if (work) step1_closest<STATS>(S, tr, h, stk, c, lf, st, pf);
-#else
-            trav_round<STATS, KHP_WW_EXT>(S, tr, h.t, has, stk, c, st,
-                              [&] { leaf_step_closest<STATS>(S, tr, h, stk, c, st); }, &h.t);
-            if (has && !c.valid) {
-                Wv.ht[idx] = h.t;
-                Wv.hslot[idx] = h.slot;
-                Wv.hu[idx] = h.u;
-                Wv.hv[idx] = h.v;
-                has = false;
-            }
-#endif
             act = __ballot(has);
-#if KHP_EXP_ABANDON   // timing experiment only (wrong results): sparse waves drop their rays once the queue is drained
-            if (exhausted && (uint32_t)__popcll(act) <= (uint32_t)KHP_EXP_ABANDON) { has = false; act = 0; }
-#endif
             if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
     }
-#if KHP_TAIL_PROBE
-    {
-        uint32_t mx = tp_max;
-        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
-        uint32_t nr = wave_sum(tp_rays);
-        if (lane_id() == 0) {
-            const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-            if (w < KHP_TAIL_PROBE_WAVES) {
-                unsigned long long* r = g_tail_probe + 6 * (size_t)w;
-                r[0] = tp_start;
-                r[1] = tp_ex;
-                r[2] = __builtin_amdgcn_s_memrealtime();
-                r[3] = nr;
-                r[4] = mx;
-                r[5] = tp_after;
-            }
-        }
-    }
-#endif
-    if (STATS) {
-        unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
-        unsigned long long pr = wave_sum((unsigned long long)st.pruned);
-        if (lane_id() == 0) {
-            atomicAdd(&Wv.cnt->node_visits, a);
-            atomicAdd(&Wv.cnt->prim_tests, b);
-            atomicAdd(&Wv.cnt->pruned, pr);
-        }
-        unsigned long long sp_ = wave_sum((unsigned long long)stk.spills);
-        if (lane_id() == 0) {
-            atomicAdd(&Wv.cnt->spills, sp_);
-            atomicAdd(&Wv.cnt->iters, wit);
-            atomicAdd(&Wv.cnt->lanes_busy, wbusy);
-#if KHP_PROFILE_STEPS
-            uint64_t total = __builtin_amdgcn_s_memtime() - prof_t0;
-            atomicAdd(&Wv.cnt->step_cycles[0], (unsigned long long)prof[0]);
-            atomicAdd(&Wv.cnt->step_cycles[1], (unsigned long long)prof[1]);
-            atomicAdd(&Wv.cnt->step_cycles[2], (unsigned long long)prof[2]);
-            atomicAdd(&Wv.cnt->step_cycles[3], (unsigned long long)(total - prof[0] - prof[1] - prof[2]));
-#endif
-        }
-    }
+    if (STATS)
+        flush_stats(st, stk, wit, wbusy, &Wv.cnt->node_visits, &Wv.cnt->prim_tests, &Wv.cnt->pruned, &Wv.cnt->iters,
+                    &Wv.cnt->lanes_busy, &Wv.cnt->spills);
 }
 
 // ---- shade: traceRay light test + shaders (CPU_PathTracer.cpp:141-208; SimpleShader.h;
@@ -547,9 +361,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_TRAV_WAVES) void k_extend(DevScene 
 // atomic per 256-thread block and queue instead of one per wave.  Device-scope
 // atomics on a single counter serialize across the XCDs; with wave-level
 // allocation k_shade spent most of its time waiting on them.
-#ifndef KHP_BLOCK_ALLOC
-#define KHP_BLOCK_ALLOC 1
-#endif
 struct BlockAlloc2 {
     uint32_t wcnt[2][4];
     uint32_t base[2];
@@ -611,10 +422,7 @@ __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3,
     __syncthreads();  // sh is reused by the next iteration
 }
 
-#ifndef KHP_SHADE_WAVES
-#define KHP_SHADE_WAVES 1
-#endif
-__global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
+__global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
     const uint32_t nf = Wv.cnt->nq[cur], n = nf + Wv.cnt->nqb[cur];
     const int nxt = cur ^ 1;
     const bool last = bounce + 1 >= Wv.depth;
@@ -720,9 +528,6 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
                         sh_tmax = length(lightpos - h2l.o);
                         shr = h2l;
                         need_shadow = true;
-#ifdef KHP_DBG_LC0
-                        if (lc.x == 0.0f && lc.y == 0.0f && lc.z == 0.0f) atomicAdd(&Wv.cnt->sh_pruned, 1ull);
-#endif
                     }
                 }
                 v3 ev = bsdf_eval(s, nrm, nrm);
@@ -857,47 +662,27 @@ __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
     }
 }
 
-// KHP_SH_FOLD: k_shadow itself finishes its records.  A lane whose any-hit
-// test is done keeps (record, occluded) and runs shadow_finish_one at the
-// wave's next refill, together with the other idle lanes (>= REFILL of them),
-// or when the wave exits -- so the colour add costs one batched pass per
-// refill instead of a separate streaming kernel over all shadow records.
-#ifndef KHP_SH_FOLD
-#define KHP_SH_FOLD 0   // measured: no gain (k_shadow 57 -> 80 VGPRs with scratch), kept as an option
-#endif
-
 template <bool STATS>
-__global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
+__global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t nf = Wv.shq->nsh, nb = Wv.shq->nshb;
-    TravStack<RING_SH, STATS> stk;
+    TravStack<STATS> stk;
     stk.init(lds, spill.base, spill.stride);
-    TravStats st{0, 0};
+    TravStats st{0, 0, 0};
     TravRay tr;
     Cur c{0u, 0.0f, 0.0f, false};
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
-    [[maybe_unused]] Prefetch pf{0.0f, 0.0f};
+    Prefetch pf{0.0f, 0.0f};
     unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
     float tmax = 0.0f;
     uint32_t mode = 0u;
     bool has = false, exhausted = false;
-#if !KHP_ONEFETCH
-    bool found = false;
-#endif
     Claimer cl;
     cl.init(Wv.shq->fetch, nf, nb, Wv.cap);
     uint32_t idx = 0;
-    [[maybe_unused]] bool fin = false, fin_occ = false;  // KHP_SH_FOLD: record idx awaits its finish
-    if (Wv.sh_fold && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Wv.cnt->sh_rays, (unsigned long long)(nf + nb));
     for (;;) {
         unsigned long long idle = __ballot(!has);
-        if (!exhausted && __popcll(idle) >= REFILL_SH) {
-#if KHP_SH_FOLD
-            if (fin) {
-                shadow_finish_one(S, Wv, idx, fin_occ);
-                fin = false;
-            }
-#endif
+        if (!exhausted && __popcll(idle) >= REFILL) {
             uint32_t my;
             const bool got = cl.claim(idle, my, exhausted);
             if (!has && got) {
@@ -909,20 +694,9 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
                 r.d = mk(b.x, b.y, b.z);
                 tmax = a.w;
                 trav_setup(tr, r);
-#if !KHP_ONEFETCH
-                found = false;
-#endif
                 lf.left = 0;
-#if KHP_LOOP2
                 has = trav2_begin<STATS>(S, tr, tmax, stk, mode, c, lf, st);
-#else
-                has = trav_begin(S, tr, stk, c);
-#endif
-                if (!has) {
-                    Wv.vis[idx] = 0;
-                    fin = Wv.sh_fold != 0;
-                    fin_occ = false;
-                }
+                if (!has) Wv.vis[idx] = 0;
             }
         }
         unsigned long long act = __ballot(has);
@@ -931,11 +705,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
             continue;
         }
         for (;;) {
-#if KHP_LOOP2
-            const bool tail_pf = KHP_TAIL_PF && exhausted && __popcll(act) <= KHP_TAIL_PF_LANES;
-#if KHP_TAIL_PRIO
-            if (exhausted) __builtin_amdgcn_s_setprio(KHP_TAIL_PRIO);  // drained queue: this wave's rays end the launch
-#endif
             if (STATS) {
                 unsigned long long wm = __ballot(has && (mode == M_NODE || mode == M_LEAF));
                 ++wit;
@@ -944,61 +713,18 @@ __global__ __launch_bounds__(TRAV_BLOCK, KHP_SH_WAVES) void k_shadow(DevScene S,
             if (has) {
                 bool occ = false;
                 Hit hu_{0.0f, -1, 0.0f, 0.0f};
-                if (iter2<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ, tail_pf, pf)) {
+                if (iter2<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ, exhausted, pf)) {
                     Wv.vis[idx] = occ ? 1 : 0;
-                    fin = Wv.sh_fold != 0;
-                    fin_occ = occ;
                     has = false;
                 }
             }
-#elif KHP_ONEFETCH
-            const bool work = has && resolve<STATS>(S, tmax, stk, c, lf, st);
-            if (has && !work) {
-                Wv.vis[idx] = 0;
-                has = false;
-            }
-            if (STATS) {
-                unsigned long long wm = __ballot(work);
-                ++wit;
-                wbusy += (uint32_t)__popcll(wm);
-            }
-            if (work && step1_any<STATS>(S, tr, tmax, stk, c, lf, st, pf)) {
-                Wv.vis[idx] = 1;
-                has = false;
-            }
-#else
-            trav_round<STATS, KHP_WW_SH>(S, tr, tmax, has, stk, c, st,
-                              [&] { found = leaf_step_any<STATS>(S, tr, tmax, stk, c, st); }, &tmax);
-            if (has && (found || !c.valid)) {
-                Wv.vis[idx] = found ? 1 : 0;
-                has = false;
-            }
-#endif
             act = __ballot(has);
-#if KHP_EXP_ABANDON   // timing experiment only (wrong results): sparse waves drop their rays once the queue is drained
-            if (exhausted && (uint32_t)__popcll(act) <= (uint32_t)KHP_EXP_ABANDON) { has = false; act = 0; }
-#endif
-            if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL_SH)) break;
+            if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
         }
     }
-#if KHP_SH_FOLD
-    if (fin) shadow_finish_one(S, Wv, idx, fin_occ);
-#endif
-    if (STATS) {
-        unsigned long long a = wave_sum((unsigned long long)st.nodes), b = wave_sum((unsigned long long)st.prims);
-        unsigned long long pr = wave_sum((unsigned long long)st.pruned);
-        if (lane_id() == 0) {
-            atomicAdd(&Wv.cnt->sh_node_visits, a);
-            atomicAdd(&Wv.cnt->sh_prim_tests, b);
-            atomicAdd(&Wv.cnt->sh_pruned, pr);
-        }
-        unsigned long long sp_ = wave_sum((unsigned long long)stk.spills);
-        if (lane_id() == 0) {
-            atomicAdd(&Wv.cnt->sh_iters, wit);
-            atomicAdd(&Wv.cnt->sh_lanes_busy, wbusy);
-            atomicAdd(&Wv.cnt->spills, sp_);
-        }
-    }
+    if (STATS)
+        flush_stats(st, stk, wit, wbusy, &Wv.cnt->sh_node_visits, &Wv.cnt->sh_prim_tests, &Wv.cnt->sh_pruned,
+                    &Wv.cnt->sh_iters, &Wv.cnt->sh_lanes_busy, &Wv.cnt->spills);
 }
 
 // ---- accumulate: PathTracer::drawTexture running mean (CPU_PathTracer.cpp:61-90) -------
@@ -1228,52 +954,28 @@ __global__ void k_unpack(float* fb, const uint32_t* pix, uint32_t P, const float
     } while (0)
 
 struct TimedLaunch {
-    int kind;  // 0 extend, 1 shade, 2 shadow, 3 other
+    int kind;  // 0 extend, 1 shade, 2 shadow (any hit), 3 other, 4 shadow finish
     int bounce;
     hipEvent_t a, b;
 };
 
-// One independent set of in-flight paths: its own SoA wavefront state, queue
-// counters, shadow queues, traversal spill columns and stream pair.  A frame
-// is cut into up to KHP_MAX_SUBFRAMES pixel ranges, one per set, whose bounce
-// pipelines run on their own streams: a persistent traversal kernel's tail
-// (its last long rays on a mostly idle chip) fills with another set's blocks.
-#ifndef KHP_MAX_SUBFRAMES
-#define KHP_MAX_SUBFRAMES 4
-#endif
-#ifndef KHP_SUBFRAMES_DEFAULT
-#define KHP_SUBFRAMES_DEFAULT 1   // env KHP_SUBFRAMES overrides (1..KHP_MAX_SUBFRAMES)
-#endif
-#ifndef KHP_STAGGER_DEFAULT
-#define KHP_STAGGER_DEFAULT 0     // env KHP_STAGGER
-#endif
-#ifndef KHP_SET_STREAMS_DEFAULT
-#define KHP_SET_STREAMS_DEFAULT 2  // env KHP_SET_STREAMS: 1 = a set's shadow stage on its own main stream
-#endif
+// One set of in-flight paths: its own SoA wavefront state, queue counters,
+// shadow queues, traversal spill columns and stream pair (A: generate /
+// extend / shade / accumulate; B: the shadow stage).
 struct PathSet {
     size_t cap = 0;
     DevMem qbuf[2][7], ht, hslot, hu, hv, TFb, CKb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
     DevMem heavyb;
     hipStream_t sA = nullptr, sB = nullptr;
 };
+// Device bytes per path of a PathSet (ensure_wave): 2 x 7 queue columns, hit
+// t/slot/u/v, TF + CK records, heavy flag, 2 x (occlusion flag + 96-B shadow record).
+constexpr size_t PATH_BYTES = 2 * 7 * 4 + 4 * 4 + 2 * 16 + 1 + 2 * (1 + 6 * 16);
 
-#ifndef KHP_HEAVY_T
-#define KHP_HEAVY_T 160   // iterations above which a path's next rays go to the front (env KHP_HEAVY_T)
-#endif
-#ifndef KHP_FRAME_STAGGER_DEFAULT
-#define KHP_FRAME_STAGGER_DEFAULT -1  // env KHP_FRAME_STAGGER (-1: frames start together; measured best)
-#endif
-#ifndef KHP_FUSE_FRAMES_DEFAULT
-#define KHP_FUSE_FRAMES_DEFAULT 32  // env KHP_FUSE_FRAMES: asynchronous frames per fused batch (8: 470, 16: 485-487, 32: 497 Msamples/s)
-#endif
 #ifndef KHP_MAX_INFLIGHT
 #define KHP_MAX_INFLIGHT 3
 #endif
-#ifndef KHP_FRAMES_IN_FLIGHT_DEFAULT
-#define KHP_FRAMES_IN_FLIGHT_DEFAULT 1   // env KHP_FRAMES_IN_FLIGHT: batches in flight (asynchronous renders)
-#endif
 struct Snap {
-    int set;
     uint32_t bounce;
 };
 // One frame slot: the events of the frame last enqueued on its path sets.
@@ -1284,7 +986,6 @@ struct FrameSlot {
     std::vector<Snap> snaps;
     hipEvent_t ev_start = nullptr, done_t = nullptr, done = nullptr;
     bool inflight = false;
-    int K = 1;
     uint32_t nf = 1;  // frames fused in this slot's batch
 };
 // An asynchronous operation waiting to be fused into the next batch.
@@ -1312,12 +1013,13 @@ struct khp_ctx {
     bool scene_set = false, built = false;
     DevMem prims, aux, trinrm, trifrm, nodes, mats, lights;
     DevScene S{};
-    // wavefront: path sets, KHP_MAX_SUBFRAMES per frame slot (ps[0] also serves the batch query API)
-    PathSet ps[KHP_MAX_INFLIGHT * KHP_MAX_SUBFRAMES];
+    khp_ctx_params prm{};
+    size_t auto_chunk = 0;         // chunk_paths() when prm.chunk_paths == 0
+    // wavefront: one path set per frame slot (ps[0] also serves the batch query API)
+    PathSet ps[KHP_MAX_INFLIGHT];
     FrameSlot fs[KHP_MAX_INFLIGHT];
     uint64_t frame_no = 0;
     hipEvent_t fb_evt = nullptr;   // the last framebuffer operation enqueued (accumulate or gather)
-    hipEvent_t prev_mid = nullptr; // asynchronous frames: the previous frame reached its stagger point
     bool report_open = false;      // c->st accumulates harvested frames
     hipEvent_t gather_evt = nullptr;  // end of the last framebuffer gather (becomes fb_evt)
     std::vector<PendingOp> pend;      // asynchronous renders (+ gathers) not yet enqueued (frame fusion)
@@ -1331,7 +1033,7 @@ struct khp_ctx {
     uint32_t n_dnodes = 0, n_slots = 0;
     DevMem fb, pix, stage, stage_pix, snap;   // snap: per-bounce Counters snapshots (stats renders)
     int cur_bounce = -1;
-    std::vector<float> dump;   // KHP_DUMP_BOUNCE: SoA o.xyz, d.xyz of one bounce's extension queue
+    std::vector<float> dump;   // prm.dump_bounce: SoA o.xyz, d.xyz of one bounce's extension queue
     uint32_t fbW = 0, fbH = 0;
     std::vector<uint32_t> pix_host;
     uint32_t pix_key[5] = {0, 0, 0, 0, 0};
@@ -1372,6 +1074,39 @@ static hipEvent_t sync_event(khp_ctx* c, size_t k) {
 extern "C" int khp_abi_version(void) { return KHP_ABI_VERSION; }
 extern "C" const char* khp_last_error(void) { return last_error(); }
 
+extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
+    if (!out) return;
+    *out = khp_ctx_params{};
+    out->fuse_frames = 32;      // 8 -> 470, 16 -> 485, 32 -> 497 Msamples/s
+    out->frames_in_flight = 1;  // with fusion one batch at a time is fastest
+    out->chunk_paths = 0;       // min(2^27, fits in half the free HBM)
+    out->heavy_iters = 160;
+    out->dump_bounce = -1;
+    out->trace_kernels = 0;
+}
+
+extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {
+    if (!c || !out) return fail(KHP_EINVAL, "null argument");
+    *out = c->prm;
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
+    if (!c || !prm) return fail(KHP_EINVAL, "null argument");
+    if (prm->fuse_frames < 1 || prm->fuse_frames > KHP_MAX_FUSE) return fail(KHP_EINVAL, "fuse_frames must be 1..32");
+    if (prm->frames_in_flight < 1 || prm->frames_in_flight > KHP_MAX_INFLIGHT)
+        return fail(KHP_EINVAL, "frames_in_flight must be 1..3");
+    if (prm->chunk_paths != 0 && prm->chunk_paths < 4096) return fail(KHP_EINVAL, "chunk_paths must be 0 or >= 4096");
+    if (prm->chunk_paths > ((uint64_t)1 << 31)) return fail(KHP_EINVAL, "chunk_paths must be <= 2^31");
+    if (prm->trace_kernels > 2) return fail(KHP_EINVAL, "trace_kernels must be 0, 1 or 2");
+    HIPCHK(hipSetDevice(c->device));
+    khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
+    if (dr != KHP_OK) return dr;
+    c->prm = *prm;
+    c->auto_chunk = 0;
+    return KHP_OK;
+}
+
 extern "C" khp_status khp_create(khp_ctx** out, int device, uint32_t flags) {
     if (!out) return fail(KHP_EINVAL, "out is null");
     *out = nullptr;
@@ -1382,6 +1117,7 @@ extern "C" khp_status khp_create(khp_ctx** out, int device, uint32_t flags) {
     khp_ctx* c = new khp_ctx();
     c->device = device;
     c->flags = flags;
+    khp_ctx_params_defaults(&c->prm);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1417,7 +1153,7 @@ extern "C" void khp_destroy(khp_ctx* c) {
     delete c;
 }
 
-static bool host_path(const khp_ctx* c) { return (c->flags & KHP_CTX_HOST_BUILD) || getenv("KHP_HOST_BUILD"); }
+static bool host_path(const khp_ctx* c) { return (c->flags & KHP_CTX_HOST_BUILD) != 0; }
 
 static khp_status set_scene_impl(khp_ctx* c, const khp_scene* s, bool device_ptrs) {
     if (c) {  // complete asynchronous frames first
@@ -1626,7 +1362,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, TRAV_BLOCK, LDS_BYTES));
     c->grid_ext = std::max(1, nb) * c->n_cu;
     nb = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, TRAV_BLOCK, LDS_BYTES_SH));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, TRAV_BLOCK, LDS_BYTES));
     c->grid_sh = std::max(1, nb) * c->n_cu;
     nb = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade, 256, 0));
@@ -1657,21 +1393,15 @@ static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap) {
     HIPCHK(w.spill.ensure((size_t)c->grid_ext * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
     HIPCHK(w.spill_sh.ensure((size_t)c->grid_sh * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
     if (!w.sA) {
-        // KHP_STREAM_PRIO=A|B: the main (extend/shade) or the shadow stream of
-        // every path set gets the high hardware-queue priority (experiment knob)
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        const char* pe = getenv("KHP_STREAM_PRIO");
-        const int pa = (pe && pe[0] == 'A') ? hi : lo, pb = (pe && pe[0] == 'B') ? hi : lo;
-        HIPCHK(hipStreamCreateWithPriority(&w.sA, hipStreamNonBlocking, pa));
-        HIPCHK(hipStreamCreateWithPriority(&w.sB, hipStreamNonBlocking, pb));
+        HIPCHK(hipStreamCreateWithFlags(&w.sA, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&w.sB, hipStreamNonBlocking));
     }
     w.cap = cap;
     return KHP_OK;
 }
 
 // Device pointers of the wavefront state (sized by ensure_wave).
-static Wave wave_view(PathSet& w) {
+static Wave wave_view(const khp_ctx* c, PathSet& w) {
     Wave Wv{};
     for (int q = 0; q < 2; ++q) {
         for (int k = 0; k < 3; ++k) {
@@ -1692,8 +1422,7 @@ static Wave wave_view(PathSet& w) {
     Wv.cnt = w.cnt.as<Counters>();
     Wv.heavy = w.heavyb.as<uint8_t>();
     Wv.cap = (uint32_t)w.cap;
-    Wv.heavy_T = KHP_HEAVY_T;
-    if (const char* e = getenv("KHP_HEAVY_T")) Wv.heavy_T = (uint32_t)strtoul(e, nullptr, 10);
+    Wv.heavy_T = c->prm.heavy_iters;
     return Wv;
 }
 
@@ -1727,11 +1456,26 @@ static khp_status prepare_pixels(khp_ctx* c, const khp_render_params* p) {
     return KHP_OK;
 }
 
-// Paths per wavefront chunk (KHP_MAX_PATHS overrides).  A chunk's path state
-// is ~200 B per path, 27 GB at 2^27; at the metric row a 16-frame batch is two
-// such chunks (2^26: four chunks, 1.2% slower; 2^28: one chunk, 1% slower, as
-// its last shadow launch and accumulate then overlap no other chunk).
-static const size_t KHP_CHUNK_PATHS_DEFAULT = (size_t)1 << 27;
+// Paths per wavefront chunk.  A chunk's path state is PATH_BYTES (~300 B) per
+// path, 40 GB at 2^27; at the metric row a 32-frame batch is four such chunks
+// (16-frame batches: 2^26 four chunks 1.2% slower, 2^28 one chunk 1% slower,
+// as its last shadow launch and accumulate then overlap no other chunk).  By
+// default the smaller of 2^27 and the largest power of two whose path sets
+// (one per batch in flight) fit in half the free HBM.
+// Decided once per context (and again after khp_set_params), before the path
+// sets themselves take memory, so the chunking stays the same frame to frame.
+static size_t chunk_paths(khp_ctx* c) {
+    if (c->prm.chunk_paths) return (size_t)c->prm.chunk_paths;
+    if (c->auto_chunk) return c->auto_chunk;
+    size_t free_b = 0, total_b = 0;
+    size_t cap = (size_t)1 << 27;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
+        const size_t fit = free_b / 2 / (PATH_BYTES * (size_t)std::max<uint32_t>(1, c->prm.frames_in_flight));
+        while (cap > ((size_t)1 << 16) && cap > fit) cap >>= 1;
+    }
+    c->auto_chunk = cap;
+    return cap;
+}
 
 static khp_status check_params(khp_ctx* c, const khp_render_params* p) {
     if (!c || !p) return fail(KHP_EINVAL, "null argument");
@@ -1757,6 +1501,8 @@ static void report_begin(khp_ctx* c) {
     c->st.render_ms = 0.0;
     c->st.extend_ms = c->st.shade_ms = c->st.shadow_ms = c->st.other_ms = 0.0;
     c->st.extend_launches = 0;
+    c->st.shadow_launches = 0;
+    c->st.shadow_finish_ms = 0.0;
     c->st.extend_rays = c->st.shadow_rays = c->st.node_visits = c->st.prim_tests = 0;
     c->st.shadow_node_visits = c->st.shadow_prim_tests = c->st.stack_spills = 0;
     c->st.extend_pruned_pops = c->st.shadow_pruned_pops = 0;
@@ -1803,7 +1549,7 @@ static khp_status harvest(khp_ctx* c, int slot) {
     float ms = 0.0f;
     if (hipEventElapsedTime(&ms, f.ev_start, f.done_t) == hipSuccess) c->st.render_ms += ms;
     c->st.frames += f.nf;
-    c->st.subframes = (uint32_t)f.K;
+    c->st.subframes = 1;
     for (auto& l : f.launches) {
         float t = 0.0f;
         if (l.b && hipEventElapsedTime(&t, l.a, l.b) == hipSuccess) {
@@ -1816,17 +1562,24 @@ static khp_status harvest(khp_ctx* c, int slot) {
                     c->ext_iv.push_back({t0, t1});
             }
             else if (l.kind == 1) c->st.shade_ms += t;
-            else if (l.kind == 2) c->st.shadow_ms += t;
-            else c->st.other_ms += t;
+            else if (l.kind == 2) {
+                c->st.shadow_ms += t;
+                c->st.shadow_launches++;
+            } else if (l.kind == 4) {
+                c->st.shadow_ms += t;
+                c->st.shadow_finish_ms += t;
+            } else {
+                c->st.other_ms += t;
+            }
             if (l.bounce >= 0 && l.bounce < KHP_MAX_BOUNCE_STATS) {
                 if (l.kind == 0) c->st.bounce_extend_ms[l.bounce] += t;
-                if (l.kind == 2) c->st.bounce_shadow_ms[l.bounce] += t;
+                if (l.kind == 2 || l.kind == 4) c->st.bounce_shadow_ms[l.bounce] += t;
             }
         }
     }
-    for (int k = 0; k < f.K; ++k) {
+    {
         Counters hc;
-        HIPCHK(hipMemcpy(&hc, c->ps[slot * KHP_MAX_SUBFRAMES + k].cnt.p, sizeof(hc), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&hc, c->ps[slot].cnt.p, sizeof(hc), hipMemcpyDeviceToHost));
         c->st.extend_rays += hc.ext_rays;
         c->st.shadow_rays += hc.sh_rays;
         c->st.node_visits += hc.node_visits;
@@ -1842,10 +1595,9 @@ static khp_status harvest(khp_ctx* c, int slot) {
     if (!f.snaps.empty()) {
         std::vector<Counters> sn(f.snaps.size());
         HIPCHK(hipMemcpy(sn.data(), c->snap.p, sn.size() * sizeof(Counters), hipMemcpyDeviceToHost));
-        std::vector<Counters> prev(f.K, Counters{});   // per set: counters after its previous snapshot
+        Counters pv{};   // counters after the previous snapshot
         for (size_t i = 0; i < sn.size(); ++i) {
             const uint32_t b = f.snaps[i].bounce;
-            Counters& pv = prev[f.snaps[i].set];
             if (b < KHP_MAX_BOUNCE_STATS) {
                 c->st.bounce_rays[b] += sn[i].ext_rays - pv.ext_rays;
                 c->st.bounce_nodes[b] += sn[i].node_visits - pv.node_visits;
@@ -1933,303 +1685,205 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     if (s != KHP_OK) return s;
     if (geometry_change) HIPCHK(hipStreamSynchronize(c->stream));
     const uint32_t P_all = (uint32_t)c->pix_host.size();
-    // Frames in flight: an asynchronous render takes the next frame slot (its
-    // own path sets and streams) and returns once enqueued; up to
-    // KHP_FRAMES_IN_FLIGHT frames then run at the same time, and one frame's
-    // bounce-by-bounce latency chain (each persistent launch waits for its
-    // slowest ray) overlaps the others' work.  The framebuffer is written in
-    // render order: each frame's accumulate waits for the previous framebuffer
+    // Batches in flight: an asynchronous render takes the next frame slot (its
+    // own path set and streams) and returns once enqueued; up to
+    // prm.frames_in_flight batches then run at the same time, each persistent
+    // launch taking 1/F of the resident grid.  The framebuffer is written in
+    // render order: each accumulate waits for the previous framebuffer
     // operation (accumulate or gather).
-    int F = KHP_FRAMES_IN_FLIGHT_DEFAULT;
-    if (const char* e = getenv("KHP_FRAMES_IN_FLIGHT")) F = atoi(e);
-    F = std::max(1, std::min(F, KHP_MAX_INFLIGHT));
+    const int F = (int)std::max<uint32_t>(1, std::min<uint32_t>(c->prm.frames_in_flight, KHP_MAX_INFLIGHT));
     const int slot = async ? (int)(c->frame_no % (uint64_t)F) : 0;
     c->frame_no += async ? 1 : 0;
-    s = harvest(c, slot);  // the slot's previous frame (async series)
+    s = harvest(c, slot);  // the slot's previous batch (async series)
     if (s != KHP_OK) return s;
     FrameSlot& f = c->fs[slot];
     f.ev_next = 0;
     f.sync_next = 0;
     f.launches.clear();
     f.snaps.clear();
-    // Path sets ("sub-frames"): a frame's paths are cut into K independent
-    // sets, each with its own wavefront state and bounce pipeline on its own
-    // stream(s).  KHP_SPLIT=s (default): set k renders the sample range
-    // [spp*k/K, spp*(k+1)/K) of every owned pixel, i.e. K progressive passes;
-    // their accumulate kernels run in sample order, so KIRK's running mean is
-    // unchanged.  KHP_SPLIT=p: set k renders a contiguous range of the owned
-    // pixel list (whole 8x8 blocks), all samples.  With KHP_STAGGER=1 set k+1
-    // starts when set k's first extend launch has finished.  The frame is
-    // identical for every K; instrumented renders keep the same launch
-    // structure, serialised on one stream.
-    int K = KHP_SUBFRAMES_DEFAULT;
-    if (const char* e = getenv("KHP_SUBFRAMES")) K = atoi(e);
-    const char* split_env = getenv("KHP_SPLIT");
-    const bool split_pix = split_env && split_env[0] == 'p';
-    int stagger = KHP_STAGGER_DEFAULT;
-    if (const char* e = getenv("KHP_STAGGER")) stagger = atoi(e);
-    int set_streams = KHP_SET_STREAMS_DEFAULT;
-    if (const char* e = getenv("KHP_SET_STREAMS")) set_streams = atoi(e) >= 2 ? 2 : 1;
-    // Concurrent frames share the chip: each persistent launch of an async
-    // render takes 1/G of the resident grid (KHP_GRID_DIV, default F).
-    int G = async ? F : 1;
-    if (const char* e = getenv("KHP_GRID_DIV")) G = std::max(1, atoi(e));
-    const int grid_ext = std::max(1, c->grid_ext / G), grid_sh = std::max(1, c->grid_sh / G);
-    K = std::max(1, std::min(K, KHP_MAX_SUBFRAMES));
-    K = (int)std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)K, split_pix ? (P_all + 63) / 64 : p->spp));
-    if (nf > 1) K = 1;  // a fused batch is one path set
-    f.K = K;
     f.nf = nf;
-    size_t cap_paths = KHP_CHUNK_PATHS_DEFAULT;
-    if (const char* e = getenv("KHP_MAX_PATHS")) cap_paths = std::max<size_t>(4096, strtoull(e, nullptr, 10));
-    uint32_t pix_lo[KHP_MAX_SUBFRAMES + 1], spp_lo[KHP_MAX_SUBFRAMES + 1];
-    for (int k = 0; k <= K; ++k) {
-        if (split_pix) {
-            uint64_t b = (uint64_t)((P_all + 63) / 64) * (uint64_t)k / (uint64_t)K * 64u;
-            pix_lo[k] = (uint32_t)std::min<uint64_t>(b, P_all);
-            spp_lo[k] = k == 0 ? 0u : p->spp;
-        } else {
-            pix_lo[k] = k == 0 ? 0u : P_all;
-            spp_lo[k] = (uint32_t)((uint64_t)p->spp * (uint64_t)k / (uint64_t)K);
-        }
+    const int G = async ? F : 1;
+    const int grid_ext = std::max(1, c->grid_ext / G), grid_sh = std::max(1, c->grid_sh / G);
+    // Chunks: the owned pixels x samples (x fused frames) are cut into chunks
+    // of at most chunk_paths() paths, pixel-major; a fused chunk carries all
+    // samples of all frames of its pixels.
+    const size_t cap_paths = chunk_paths(c);
+    uint32_t P_chunk, S_chunk;
+    if (nf > 1) {
+        P_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(std::max<uint32_t>(1, P_all),
+                                                                 cap_paths / ((size_t)p->spp * nf)));
+        S_chunk = p->spp;
+    } else {
+        P_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(P_all, cap_paths));
+        S_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(p->spp, cap_paths / P_chunk));
     }
-    auto set_pix = [&](int k, uint32_t& lo, uint32_t& hi) {
-        lo = split_pix ? pix_lo[k] : 0u;
-        hi = split_pix ? pix_lo[k + 1] : P_all;
-    };
-    auto set_spp = [&](int k, uint32_t& lo, uint32_t& hi) {
-        lo = split_pix ? 0u : spp_lo[k];
-        hi = split_pix ? p->spp : spp_lo[k + 1];
-    };
-    uint32_t P_chunk[KHP_MAX_SUBFRAMES], S_chunk[KHP_MAX_SUBFRAMES];
-    for (int k = 0; k < K; ++k) {
-        uint32_t a, b, sa, sb;
-        set_pix(k, a, b);
-        set_spp(k, sa, sb);
-        const uint32_t Pk = std::max<uint32_t>(1, b - a), Sk = std::max<uint32_t>(1, sb - sa);
-        if (nf > 1) {  // fused: every chunk carries all samples of all frames of its pixels
-            P_chunk[k] = (uint32_t)std::max<size_t>(1, std::min<size_t>(Pk, cap_paths / ((size_t)Sk * nf)));
-            S_chunk[k] = Sk;
-        } else {
-            P_chunk[k] = (uint32_t)std::min<size_t>(Pk, cap_paths);
-            S_chunk[k] = (uint32_t)std::max<size_t>(1, std::min<size_t>(Sk, cap_paths / std::max<uint32_t>(P_chunk[k], 1)));
-        }
-        // a partial batch (flushed by a sync) reserves room for a full one, so the
-        // first full batch does not allocate
-        size_t want = (size_t)P_chunk[k] * S_chunk[k] * nf;
-        if (nf > 1) {
-            int fuse = KHP_FUSE_FRAMES_DEFAULT;
-            if (const char* e = getenv("KHP_FUSE_FRAMES")) fuse = std::max(1, std::min(atoi(e), KHP_MAX_FUSE));
-            want = std::max(want, std::min<size_t>(cap_paths, (size_t)P_chunk[k] * S_chunk[k] * (size_t)fuse));
-        }
-        s = ensure_wave(c, c->ps[slot * KHP_MAX_SUBFRAMES + k], want);
-        if (s != KHP_OK) return s;
+    // a partial batch (flushed by a sync) reserves room for a full one, so the
+    // first full batch does not allocate
+    size_t want = (size_t)P_chunk * S_chunk * nf;
+    if (nf > 1) {
+        const uint32_t fuse = std::max<uint32_t>(1, std::min<uint32_t>(c->prm.fuse_frames, KHP_MAX_FUSE));
+        want = std::max(want, std::min<size_t>(cap_paths, (size_t)P_chunk * S_chunk * fuse));
     }
-    const char* dump_env = getenv("KHP_DUMP_BOUNCE");
-    const int dump_b = dump_env ? atoi(dump_env) : -1;
+    PathSet& w = c->ps[slot];
+    s = ensure_wave(c, w, want);
+    if (s != KHP_OK) return s;
+    const int dump_b = (!async && !ops) ? c->prm.dump_bounce : -1;
     if (stats) {
-        size_t chunks = 0;
-        for (int k = 0; k < K; ++k) {
-            uint32_t a, b, sa, sb;
-            set_pix(k, a, b);
-            set_spp(k, sa, sb);
-            chunks += (size_t)((b - a + P_chunk[k] - 1) / P_chunk[k]) * ((sb - sa + S_chunk[k] - 1) / S_chunk[k]);
-        }
+        const size_t chunks = (size_t)((P_all + P_chunk - 1) / P_chunk) * ((p->spp + S_chunk - 1) / S_chunk);
         HIPCHK(c->snap.ensure(std::max<size_t>(1, chunks * p->depth) * sizeof(Counters)));
     }
-    // Per set, two streams: A runs generate / extend / shade / accumulate, B
-    // runs the shadow stage (k_shadow + k_shadow_finish) of bounce b while A
-    // already traverses bounce b+1, so each persistent kernel's tail fills with
-    // the other's blocks.  Ordering within a set: B(b) after shade(b) on A;
-    // shade(b+1) after B(b) (both update the path colour C in bounce order);
-    // the shadow queue of bounce b+2 reuses parity b's buffers only after
-    // shade(b+1), which already waited for B(b).  Instrumented renders run
-    // everything on the context stream so the per-bounce snapshots are exact.
-    const bool overlap = !stats && !getenv("KHP_NO_OVERLAP");
+    // Two streams: A runs generate / extend / shade / accumulate, B runs the
+    // shadow stage (k_shadow + k_shadow_finish) of bounce b while A already
+    // traverses bounce b+1, so each persistent kernel's tail fills with the
+    // other's blocks.  Ordering: B(b) after shade(b) on A; shade(b+1) after
+    // B(b) (both update the path colour C in bounce order); the shadow queue
+    // of bounce b+2 reuses parity b's buffers only after shade(b+1), which
+    // already waited for B(b).  Instrumented renders run everything on the
+    // context stream so the per-bounce snapshots are exact.
+    const bool overlap = !stats;
+    hipStream_t sA = overlap ? w.sA : c->stream;
+    hipStream_t sB = overlap ? w.sB : c->stream;
     c->cur_bounce = -1;
     f.ev_start = slot_event(f.ev_pool, f.ev_next, false);
     (void)hipEventRecord(f.ev_start, c->stream);
     // Fork from the context stream (framebuffer clears, pixel-list uploads) --
     // not for an asynchronous frame: the context stream also carries the joins
     // of the frames still in flight, and waiting on it would serialise them.
-    hipEvent_t e_fork = nullptr;
     if (!async || geometry_change) {
-        e_fork = slot_event(f.sync_pool, f.sync_next, true);
+        hipEvent_t e_fork = slot_event(f.sync_pool, f.sync_next, true);
         HIPCHK(hipEventRecord(e_fork, c->stream));
+        if (sA != c->stream) HIPCHK(hipStreamWaitEvent(sA, e_fork, 0));
+        if (sB != c->stream) HIPCHK(hipStreamWaitEvent(sB, e_fork, 0));
     }
-    // Frame stagger (asynchronous frames): a frame starts only when the previous
-    // one has finished its extend launch of bounce KHP_FRAME_STAGGER, so two
-    // frames in flight run out of phase -- one's long-ray tails beside the
-    // other's full launches -- instead of in lockstep (-1: no stagger).
-    int fstag = KHP_FRAME_STAGGER_DEFAULT;
-    if (const char* e = getenv("KHP_FRAME_STAGGER")) fstag = atoi(e);
-    hipEvent_t wait_mid = (async && fstag >= 0) ? c->prev_mid : nullptr;
-    hipEvent_t my_mid = nullptr;
-    hipEvent_t prev_started = nullptr;  // KHP_STAGGER: the previous set's first extend launch finished
-    hipEvent_t prev_acc = c->fb_evt;    // the previous framebuffer operation (this set's accumulate waits for it)
-    std::vector<hipEvent_t> set_end;
-    for (int k = 0; k < K; ++k) {
-        PathSet& w = c->ps[slot * KHP_MAX_SUBFRAMES + k];
-        hipStream_t sA = overlap ? w.sA : c->stream;
-        hipStream_t sB = overlap ? (set_streams >= 2 ? w.sB : w.sA) : c->stream;
-        if (e_fork && sA != c->stream) HIPCHK(hipStreamWaitEvent(sA, e_fork, 0));
-        if (e_fork && sB != sA && sB != c->stream) HIPCHK(hipStreamWaitEvent(sB, e_fork, 0));
-        if (wait_mid) {
-            HIPCHK(hipStreamWaitEvent(sA, wait_mid, 0));
-            if (sB != sA) HIPCHK(hipStreamWaitEvent(sB, wait_mid, 0));
-        }
-        if (overlap && prev_started) {
-            HIPCHK(hipStreamWaitEvent(sA, prev_started, 0));
-            if (sB != sA) HIPCHK(hipStreamWaitEvent(sB, prev_started, 0));
-        }
-        prev_started = nullptr;
-        HIPCHK(hipMemsetAsync(w.cnt.p, 0, sizeof(Counters), sA));
-        HIPCHK(hipMemsetAsync(w.shqb.p, 0, 2 * sizeof(ShadowQ), sA));
-        if (sB != sA) {
-            hipEvent_t z = slot_event(f.sync_pool, f.sync_next, true);
-            HIPCHK(hipEventRecord(z, sA));
-            HIPCHK(hipStreamWaitEvent(sB, z, 0));
-        }
-        uint32_t set_p0, set_p1, set_s0, set_s1;
-        set_pix(k, set_p0, set_p1);
-        set_spp(k, set_s0, set_s1);
-        bool acc_waited = false;
-        Wave Wv = wave_view(w);
-        Wv.pix = c->pix.as<uint32_t>();
-        Wv.W = p->width;
-        Wv.H = p->height;
-        Wv.seed = p->seed;
-        Wv.depth = p->depth;
-        Wv.sh_fold = (KHP_SH_FOLD && KHP_LOOP2 && !getenv("KHP_NO_SH_FOLD")) ? 1u : 0u;  // compile-time option
-        SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
-        SpillArea sp_sh{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
-        for (uint32_t p0 = set_p0; p0 < set_p1; p0 += P_chunk[k]) {
-            uint32_t P = std::min(P_chunk[k], set_p1 - p0);
-            for (uint32_t s0 = set_s0; s0 < set_s1; s0 += S_chunk[k]) {
-                uint32_t ns = std::min(S_chunk[k], set_s1 - s0);
-                Wv.P = P;
-                Wv.p_off = p0;
-                Wv.sample0 = fs0[0] + s0;
-                Wv.n_samples = ns;
-                Wv.n_frames = nf;
-                for (uint32_t q = 0; q < nf; ++q) Wv.fsample0[q] = fs0[q] + s0;
-                uint32_t npaths = P * ns * nf;
-                timed(c, f, 3, true, sA);
-                hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wv);
-                timed(c, f, 3, false, sA);
-                hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
-                for (uint32_t b = 0; b < p->depth; ++b) {
-                    int cur = b & 1;
-                    const int par = b & 1;
-                    c->cur_bounce = (int)b;
-                    Wave Wb = Wv;
-                    Wb.sh = w.shb[par].as<float4>();
-                    Wb.vis = w.visb[par].as<uint8_t>();
-                    Wb.shq = w.shqb.as<ShadowQ>() + par;
-                    if (dump_b == (int)b && k == 0) {
-                        uint32_t nq = 0;
-                        HIPCHK(hipMemcpyAsync(&nq, &Wv.cnt->nq[cur], 4, hipMemcpyDeviceToHost, sA));
-                        HIPCHK(hipStreamSynchronize(sA));
-                        c->dump.resize(6 * (size_t)nq);
-                        for (int q = 0; q < 3; ++q) {
-                            HIPCHK(hipMemcpy(c->dump.data() + (size_t)q * nq, Wv.qo[cur][q], 4 * (size_t)nq, hipMemcpyDeviceToHost));
-                            HIPCHK(hipMemcpy(c->dump.data() + (size_t)(3 + q) * nq, Wv.qd[cur][q], 4 * (size_t)nq, hipMemcpyDeviceToHost));
-                        }
-                    }
-                    hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
-                    timed(c, f, 0, true, sA);
-                    if (stats)
-                        hipLaunchKernelGGL(k_extend<true>, dim3(grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
-                    else
-                        hipLaunchKernelGGL(k_extend<false>, dim3(grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
-                    timed(c, f, 0, false, sA);
-                    if (async && fstag >= 0 && (int)b == std::min(fstag, (int)p->depth - 1) && k == K - 1 && !my_mid) {
-                        my_mid = slot_event(f.sync_pool, f.sync_next, true);
-                        HIPCHK(hipEventRecord(my_mid, sA));
-                    }
-                    if (overlap && stagger && k + 1 < K && !prev_started) {
-                        prev_started = slot_event(f.sync_pool, f.sync_next, true);
-                        HIPCHK(hipEventRecord(prev_started, sA));
-                    }
-                    if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
-                    timed(c, f, 1, true, sA);
-                    hipLaunchKernelGGL(k_shade, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
-                    timed(c, f, 1, false, sA);
-                    if (sB != sA) {
-                        hipEvent_t shaded = slot_event(f.sync_pool, f.sync_next, true);
-                        HIPCHK(hipEventRecord(shaded, sA));
-                        HIPCHK(hipStreamWaitEvent(sB, shaded, 0));
-                    }
-                    timed(c, f, 2, true, sB);
-                    if (stats)
-                        hipLaunchKernelGGL(k_shadow<true>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES_SH, sB, c->S, Wb, sp_sh);
-                    else
-                        hipLaunchKernelGGL(k_shadow<false>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES_SH, sB, c->S, Wb, sp_sh);
-                    timed(c, f, 2, false, sB);
-                    if (!Wb.sh_fold) {
-                        timed(c, f, 2, true, sB);   // shadow stage = any-hit traversal + finish
-                        hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
-                        timed(c, f, 2, false, sB);
-                    }
-                    if (sB != sA) {
-                        done_b = slot_event(f.sync_pool, f.sync_next, true);
-                        HIPCHK(hipEventRecord(done_b, sB));
-                    }
-                    if (stats) {
-                        HIPCHK(hipMemcpyAsync(c->snap.as<Counters>() + f.snaps.size(), w.cnt.p, sizeof(Counters),
-                                              hipMemcpyDeviceToDevice, sA));
-                        f.snaps.push_back(Snap{k, b});
+    hipEvent_t prev_acc = c->fb_evt;  // the previous framebuffer operation (this batch's accumulate waits for it)
+    HIPCHK(hipMemsetAsync(w.cnt.p, 0, sizeof(Counters), sA));
+    HIPCHK(hipMemsetAsync(w.shqb.p, 0, 2 * sizeof(ShadowQ), sA));
+    if (sB != sA) {
+        hipEvent_t z = slot_event(f.sync_pool, f.sync_next, true);
+        HIPCHK(hipEventRecord(z, sA));
+        HIPCHK(hipStreamWaitEvent(sB, z, 0));
+    }
+    bool acc_waited = false;
+    Wave Wv = wave_view(c, w);
+    Wv.pix = c->pix.as<uint32_t>();
+    Wv.W = p->width;
+    Wv.H = p->height;
+    Wv.seed = p->seed;
+    Wv.depth = p->depth;
+    SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
+    SpillArea sp_sh{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
+    for (uint32_t p0 = 0; p0 < P_all; p0 += P_chunk) {
+        const uint32_t P = std::min(P_chunk, P_all - p0);
+        for (uint32_t s0 = 0; s0 < p->spp; s0 += S_chunk) {
+            const uint32_t ns = std::min(S_chunk, p->spp - s0);
+            Wv.P = P;
+            Wv.p_off = p0;
+            Wv.sample0 = fs0[0] + s0;
+            Wv.n_samples = ns;
+            Wv.n_frames = nf;
+            for (uint32_t q = 0; q < nf; ++q) Wv.fsample0[q] = fs0[q] + s0;
+            const uint32_t npaths = P * ns * nf;
+            timed(c, f, 3, true, sA);
+            hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wv);
+            timed(c, f, 3, false, sA);
+            hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
+            for (uint32_t b = 0; b < p->depth; ++b) {
+                const int cur = b & 1;
+                c->cur_bounce = (int)b;
+                Wave Wb = Wv;
+                Wb.sh = w.shb[cur].as<float4>();
+                Wb.vis = w.visb[cur].as<uint8_t>();
+                Wb.shq = w.shqb.as<ShadowQ>() + cur;
+                if (dump_b == (int)b && p0 == 0 && s0 == 0) {
+                    uint32_t nq = 0;
+                    HIPCHK(hipMemcpyAsync(&nq, &Wv.cnt->nq[cur], 4, hipMemcpyDeviceToHost, sA));
+                    HIPCHK(hipStreamSynchronize(sA));
+                    c->dump.resize(6 * (size_t)nq);
+                    for (int q = 0; q < 3; ++q) {
+                        HIPCHK(hipMemcpy(c->dump.data() + (size_t)q * nq, Wv.qo[cur][q], 4 * (size_t)nq, hipMemcpyDeviceToHost));
+                        HIPCHK(hipMemcpy(c->dump.data() + (size_t)(3 + q) * nq, Wv.qd[cur][q], 4 * (size_t)nq, hipMemcpyDeviceToHost));
                     }
                 }
-                c->cur_bounce = -1;
-                if (done_b) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
-                if (prev_acc && !acc_waited) {  // framebuffer order: previous frame / previous sample set
-                    HIPCHK(hipStreamWaitEvent(sA, prev_acc, 0));
-                    acc_waited = true;
+                hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
+                timed(c, f, 0, true, sA);
+                if (stats)
+                    hipLaunchKernelGGL(k_extend<true>, dim3(grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                else
+                    hipLaunchKernelGGL(k_extend<false>, dim3(grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                timed(c, f, 0, false, sA);
+                if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
+                timed(c, f, 1, true, sA);
+                hipLaunchKernelGGL(k_shade, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                timed(c, f, 1, false, sA);
+                if (sB != sA) {
+                    hipEvent_t shaded = slot_event(f.sync_pool, f.sync_next, true);
+                    HIPCHK(hipEventRecord(shaded, sA));
+                    HIPCHK(hipStreamWaitEvent(sB, shaded, 0));
                 }
-                timed(c, f, 3, true, sA);
-                if (!ops) {
-                    hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, c->fb.as<float>(), 0u);
-                } else {
-                    // fused frames in call order; a gather between two of them runs on the
-                    // context stream after the first's accumulate and before the second's
-                    // (a batch with gathers is one chunk: enqueue_frames' caller checks)
-                    uint32_t fr = 0;
-                    for (const PendingOp& o : *ops) {
-                        if (o.kind == PendingOp::RENDER) {
-                            hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv,
-                                               c->fb.as<float>(), fr++);
-                        } else {
-                            hipEvent_t acc = slot_event(f.sync_pool, f.sync_next, true);
-                            HIPCHK(hipEventRecord(acc, sA));
-                            c->fb_evt = acc;
-                            s = gather_now(c, &o.p, o.root);   // waits fb_evt, sets fb_evt to its own end
-                            if (s != KHP_OK) return s;
-                            HIPCHK(hipStreamWaitEvent(sA, c->fb_evt, 0));
-                        }
-                    }
+                timed(c, f, 2, true, sB);
+                if (stats)
+                    hipLaunchKernelGGL(k_shadow<true>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sB, c->S, Wb, sp_sh);
+                else
+                    hipLaunchKernelGGL(k_shadow<false>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sB, c->S, Wb, sp_sh);
+                timed(c, f, 2, false, sB);
+                timed(c, f, 4, true, sB);   // shadow stage = any-hit traversal + finish
+                hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
+                timed(c, f, 4, false, sB);
+                if (sB != sA) {
+                    done_b = slot_event(f.sync_pool, f.sync_next, true);
+                    HIPCHK(hipEventRecord(done_b, sB));
                 }
-                timed(c, f, 3, false, sA);
-                if (sB != sA) {  // the next chunk's shadow stages come after this chunk's accumulate
-                    hipEvent_t acc = slot_event(f.sync_pool, f.sync_next, true);
-                    HIPCHK(hipEventRecord(acc, sA));
-                    HIPCHK(hipStreamWaitEvent(sB, acc, 0));
+                if (stats) {
+                    HIPCHK(hipMemcpyAsync(c->snap.as<Counters>() + f.snaps.size(), w.cnt.p, sizeof(Counters),
+                                          hipMemcpyDeviceToDevice, sA));
+                    f.snaps.push_back(Snap{b});
                 }
             }
+            c->cur_bounce = -1;
+            if (done_b) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
+            if (prev_acc && !acc_waited) {  // framebuffer order: previous frame
+                HIPCHK(hipStreamWaitEvent(sA, prev_acc, 0));
+                acc_waited = true;
+            }
+            timed(c, f, 3, true, sA);
+            if (!ops) {
+                hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, c->fb.as<float>(), 0u);
+            } else {
+                // fused frames in call order; a gather between two of them runs on the
+                // context stream after the first's accumulate and before the second's
+                // (a batch with gathers is one chunk: flush() checks)
+                uint32_t fr = 0;
+                for (const PendingOp& o : *ops) {
+                    if (o.kind == PendingOp::RENDER) {
+                        hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv,
+                                           c->fb.as<float>(), fr++);
+                    } else {
+                        hipEvent_t acc = slot_event(f.sync_pool, f.sync_next, true);
+                        HIPCHK(hipEventRecord(acc, sA));
+                        c->fb_evt = acc;
+                        s = gather_now(c, &o.p, o.root);   // waits fb_evt, sets fb_evt to its own end
+                        if (s != KHP_OK) return s;
+                        HIPCHK(hipStreamWaitEvent(sA, c->fb_evt, 0));
+                    }
+                }
+            }
+            timed(c, f, 3, false, sA);
+            if (sB != sA) {  // the next chunk's shadow stages come after this chunk's accumulate
+                hipEvent_t acc = slot_event(f.sync_pool, f.sync_next, true);
+                HIPCHK(hipEventRecord(acc, sA));
+                HIPCHK(hipStreamWaitEvent(sB, acc, 0));
+            }
         }
-        hipEvent_t e_end = slot_event(f.sync_pool, f.sync_next, true);
-        HIPCHK(hipEventRecord(e_end, sA));
-        set_end.push_back(e_end);
-        if (!split_pix) prev_acc = e_end;  // sample split: the next set accumulates after this one
     }
-    // join: the frame is done when every set has accumulated
-    for (hipEvent_t e : set_end) HIPCHK(hipStreamWaitEvent(c->stream, e, 0));
+    // join: the batch is done when its last chunk has accumulated
+    hipEvent_t e_end = slot_event(f.sync_pool, f.sync_next, true);
+    HIPCHK(hipEventRecord(e_end, sA));
+    HIPCHK(hipStreamWaitEvent(c->stream, e_end, 0));
     f.done_t = slot_event(f.ev_pool, f.ev_next, false);
     (void)hipEventRecord(f.done_t, c->stream);
     f.done = slot_event(f.sync_pool, f.sync_next, true);
     HIPCHK(hipEventRecord(f.done, c->stream));
     c->fb_evt = f.done;
-    c->prev_mid = async ? (my_mid ? my_mid : f.done) : nullptr;
     f.inflight = true;
     HIPCHK(hipGetLastError());
     if (async) return KHP_OK;
@@ -2245,7 +1899,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
 }
 
 
-// Frame fusion (asynchronous renders, KHP_FUSE_FRAMES = n > 1): up to n
+// Frame fusion (asynchronous renders, khp_ctx_params.fuse_frames = n > 1): up to n
 // consecutive asynchronous frames with the same geometry, spp, depth and seed
 // are enqueued as ONE batch -- one wavefront over all their paths, one
 // persistent launch per bounce -- and accumulated one frame after another in
@@ -2295,8 +1949,7 @@ static khp_status flush(khp_ctx* c) {
             P = tmp.size();
         }
     }
-    size_t cap_paths = KHP_CHUNK_PATHS_DEFAULT;
-    if (const char* e = getenv("KHP_MAX_PATHS")) cap_paths = std::max<size_t>(4096, strtoull(e, nullptr, 10));
+    const size_t cap_paths = chunk_paths(c);
     const bool one_chunk = P * (size_t)first->p.spp * nr <= cap_paths;
     if (nr == 1 || !gathers || one_chunk) {
         if (nr == 1) {
@@ -2360,9 +2013,7 @@ extern "C" khp_status khp_render(khp_ctx* c, const khp_render_params* p, float* 
         if (s != KHP_OK) return s;
         return enqueue_frames(c, p, out_rgb, nullptr);
     }
-    int fuse = KHP_FUSE_FRAMES_DEFAULT;
-    if (const char* e = getenv("KHP_FUSE_FRAMES")) fuse = atoi(e);
-    fuse = std::max(1, std::min(fuse, KHP_MAX_FUSE));
+    const int fuse = (int)std::max<uint32_t>(1, std::min<uint32_t>(c->prm.fuse_frames, KHP_MAX_FUSE));
     if (fuse <= 1) {
         s = flush(c);
         if (s != KHP_OK) return s;
@@ -2584,7 +2235,7 @@ extern "C" khp_status khp_read_framebuffer(khp_ctx* c, float* out_rgb) {
 }
 
 // ---- batch queries through the persistent wavefront kernels (test hook) -------------
-// KHP_TRACE_PERSISTENT=1 routes khp_trace_closest / khp_trace_any through k_extend /
+// khp_ctx_params.trace_kernels = 1|2 routes khp_trace_closest / khp_trace_any through k_extend /
 // k_shadow -- the kernels the renderer uses -- instead of the one-ray-per-thread
 // kernels, so tests can check the production traversal ray by ray.
 __global__ void k_load_rays(uint32_t n, const float* orig, const float* dir, Wave Wv, int as_shadow,
@@ -2615,12 +2266,9 @@ __global__ void k_store_hits(DevScene S, uint32_t n, Wave Wv, float* t, int32_t*
     uv[2 * i + 1] = Wv.hv[i];
 }
 
-// 0: one-ray-per-thread kernels; 1: instrumented persistent kernels (KIRK's
-// plain BVH2 steps, visit counts); 2: production persistent kernels (paired).
-static int trace_persistent() {
-    const char* e = getenv("KHP_TRACE_PERSISTENT");
-    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-}
+// prm.trace_kernels -- 0: one-ray-per-thread kernels; 1: instrumented
+// persistent kernels (KIRK's visit counts); 2: production persistent kernels.
+static int trace_persistent(const khp_ctx* c) { return (int)c->prm.trace_kernels; }
 
 static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig, const float* dir,
                                        const float* tmax_h, float* t_out, int32_t* obj_out, float* uv_out,
@@ -2635,16 +2283,16 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
     if (shadow) HIPCHK(upload(tm, tmax_h, (size_t)n, c->stream));
     HIPCHK(hipMemsetAsync(w.cnt.p, 0, sizeof(Counters), c->stream));
     HIPCHK(hipMemsetAsync(w.shqb.p, 0, 2 * sizeof(ShadowQ), c->stream));
-    Wave Wv = wave_view(w);
+    Wave Wv = wave_view(c, w);
     hipLaunchKernelGGL(k_load_rays, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, o.as<float>(), d.as<float>(),
                        Wv, shadow ? 1 : 0, tm.as<float>());
-    const bool prod = trace_persistent() == 2;
+    const bool prod = trace_persistent(c) == 2;
     hipEvent_t e0 = next_event(c), e1 = next_event(c);
     (void)hipEventRecord(e0, c->stream);
     if (shadow) {
         SpillArea sp{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
-        if (prod) hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(TRAV_BLOCK), LDS_BYTES_SH, c->stream, c->S, Wv, sp);
-        else hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(TRAV_BLOCK), LDS_BYTES_SH, c->stream, c->S, Wv, sp);
+        if (prod) hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, c->stream, c->S, Wv, sp);
+        else hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, c->stream, c->S, Wv, sp);
         (void)hipEventRecord(e1, c->stream);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(hit_out, Wv.vis, n, hipMemcpyDeviceToHost, c->stream));
@@ -2686,7 +2334,7 @@ extern "C" khp_status khp_trace_closest(khp_ctx* c, uint32_t n, const float* ori
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
     if (n == 0) return KHP_OK;
     HIPCHK(hipSetDevice(c->device));
-    if (trace_persistent()) return trace_persistent_run(c, n, orig, dir, nullptr, t_out, obj_out, uv_out, nullptr);
+    if (trace_persistent(c)) return trace_persistent_run(c, n, orig, dir, nullptr, t_out, obj_out, uv_out, nullptr);
     DevMem o, d, t, ob, uv, stb;
     HIPCHK(upload(o, orig, 3 * (size_t)n, c->stream));
     HIPCHK(upload(d, dir, 3 * (size_t)n, c->stream));
@@ -2720,7 +2368,7 @@ extern "C" khp_status khp_trace_any(khp_ctx* c, uint32_t n, const float* orig, c
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
     if (n == 0) return KHP_OK;
     HIPCHK(hipSetDevice(c->device));
-    if (trace_persistent()) return trace_persistent_run(c, n, orig, dir, tmax, nullptr, nullptr, nullptr, hit_out);
+    if (trace_persistent(c)) return trace_persistent_run(c, n, orig, dir, tmax, nullptr, nullptr, nullptr, hit_out);
     DevMem o, d, tm, h;
     HIPCHK(upload(o, orig, 3 * (size_t)n, c->stream));
     HIPCHK(upload(d, dir, 3 * (size_t)n, c->stream));

@@ -131,111 +131,13 @@ struct LdsStack {
     }
 };
 
-// LdsStack with the top entry held in registers.  pop() returns the register
-// top at once and issues the LDS (or spill) read of the entry below it, whose
-// latency then overlaps the rest of the iteration; push() writes the old top
-// back only if it is not already in its ring slot (`clean`).
-//   entries [0, lo) live in the global spill column, [lo, sp-1) in the LDS
-//   ring, entry sp-1 (the top) in registers -- and also in its ring slot when
-//   clean.  At most R entries occupy the ring.
-template <int R, bool COUNT>
-struct LdsStackT {
-    static_assert((R & (R - 1)) == 0, "ring size must be a power of two");
-    uint32_t* lds;
-    int4* spill;
-    uint32_t stride;
-    int sp, lo;
-    uint32_t tr;
-    float ta, tb;
-    bool clean;
-    uint32_t spills;
-    __device__ __forceinline__ void init(uint32_t* lds_base, int4* spill_base, uint32_t grid_lanes) {
-        lds = lds_base;
-        spill = spill_base;
-        stride = grid_lanes;
-        sp = lo = 0;
-        clean = false;
-        spills = 0;
-    }
-    __device__ __forceinline__ void clear() {
-        sp = lo = 0;
-        clean = false;
-    }
-    __device__ __forceinline__ bool empty() const { return sp == 0; }
-    __device__ __forceinline__ uint32_t slot(int e) const { return (uint32_t)(e & (R - 1)) * TRAV_BLOCK + threadIdx.x; }
-    __device__ __forceinline__ int4* gcell(int e) const {
-        return spill + (size_t)e * stride + blockIdx.x * blockDim.x + threadIdx.x;
-    }
-    __device__ __forceinline__ void push(uint32_t r, float a, float b) {
-        if (sp > 0 && !clean) {
-            const int e = sp - 1;
-            if (e - lo == R) {  // ring full: the oldest ring entry goes to the spill column
-                uint32_t k = slot(lo);
-                *gcell(lo) = make_int4((int)lds[k], (int)lds[k + R * TRAV_BLOCK], (int)lds[k + 2 * R * TRAV_BLOCK], 0);
-                ++lo;
-                if (COUNT) ++spills;
-            }
-            uint32_t k = slot(e);
-            lds[k] = tr;
-            lds[k + R * TRAV_BLOCK] = bits_from_f(ta);
-            lds[k + 2 * R * TRAV_BLOCK] = bits_from_f(tb);
-        }
-        tr = r;
-        ta = a;
-        tb = b;
-        clean = false;
-        ++sp;
-    }
-    __device__ __forceinline__ void pop(uint32_t& r, float& a, float& b) {
-        r = tr;
-        a = ta;
-        b = tb;
-        --sp;
-        if (sp > 0) {
-            const int e = sp - 1;
-            if (e >= lo) {
-                uint32_t k = slot(e);
-                tr = lds[k];
-                ta = f_from_bits(lds[k + R * TRAV_BLOCK]);
-                tb = f_from_bits(lds[k + 2 * R * TRAV_BLOCK]);
-                clean = true;
-            } else {
-                int4 v = *gcell(e);
-                tr = (uint32_t)v.x;
-                ta = f_from_bits((uint32_t)v.y);
-                tb = f_from_bits((uint32_t)v.z);
-                lo = e;
-                clean = false;
-            }
-        }
-    }
-};
-
-#ifndef KHP_PIN
-#define KHP_PIN 0   // 1: force whole-record loads (measured 10 % slower: the split lets lanes that fail an early-out skip the late fields)
-#endif
 // Materialise a fetched record in registers at this point.  Without it the
 // compiler splits a 64-B record fetch and sinks the loads of the fields a test
 // needs late (z planes, the cone's W / max_d) below the test's early-out
 // branches, which turns one memory round trip per record into two or three
 // dependent ones (seen in the gfx950 ISA).
-#ifndef KHP_PIN1
-#define KHP_PIN1 1   // pin the one-fetch record (same speed, no scratch in k_extend)
-#endif
-__device__ __forceinline__ void pin(float4& v) {
-#if KHP_PIN || KHP_PIN1
-    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
-#endif
-}
-__device__ __forceinline__ void pin(int4& v) {
-#if KHP_PIN || KHP_PIN1
-    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
-#endif
-}
-
-#ifndef KHP_LEAF_PAIR
-#define KHP_LEAF_PAIR 0   // 1: fetch a leaf's first two records together (spills at 96 VGPRs)
-#endif
+__device__ __forceinline__ void pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+__device__ __forceinline__ void pin(int4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
 
 // The entry a lane processes next lives in registers (Cur); the stack holds
 // only the deferred far children.  When both children of a node are hit,
@@ -258,8 +160,6 @@ __device__ __forceinline__ void cur_next(Stack& stk, Cur& c) {
     }
 }
 
-__device__ __forceinline__ bool cur_interior(const Cur& c) { return c.valid && !ref_leaf(c.ref); }
-__device__ __forceinline__ bool cur_leaf(const Cur& c) { return c.valid && ref_leaf(c.ref); }
 
 // Root box test (BVH::closestIntersection / isIntersection pre-test).
 template <class Stack>
@@ -280,47 +180,9 @@ __device__ __forceinline__ uint32_t leaf_count(const DevScene& S, uint32_t ref) 
     return c;
 }
 
-#ifndef KHP_PAIR
-#define KHP_PAIR 0   // 1: expand an interior far sibling from the near child's 128-B line (exact; measured 10 % slower)
-#endif
-// Cursor-only flag: the entry on top of the stack is this node's interior
-// sibling, whose record shares this node's 128-B line (records 2k, 2k+1).
-constexpr uint32_t SIB_BIT = 0x40000000u;
-
-// Push the two children of one record in KIRK's order (near popped first).
-template <class Stack>
-__device__ __forceinline__ void push_children(Stack& stk, bool lh, bool rh, float l0, float l1, float r0, float r1,
-                                              int4 rf) {
-    if (lh && rh) {
-        if (l0 < r0) {
-            stk.push((uint32_t)rf.y, r0, r1);
-            stk.push((uint32_t)rf.x, l0, l1);
-        } else {
-            stk.push((uint32_t)rf.x, l0, l1);
-            stk.push((uint32_t)rf.y, r0, r1);
-        }
-    } else if (lh) {
-        stk.push((uint32_t)rf.x, l0, l1);
-    } else if (rh) {
-        stk.push((uint32_t)rf.y, r0, r1);
-    }
-}
-
 // Interior entry: prune test (BVHNode::traverse, CPU_BVH.cpp:151-153) at the
 // moment KIRK would pop it, then both child boxes, near child first.
 // tlimit = current closest t (closest hit) or the ray's tMax (any hit).
-//
-// PAIR: if the cursor carries SIB_BIT, the sibling's record is read from the
-// same line and the sibling's stack entry is replaced by the sibling's two
-// children (far, then near).  KIRK would pop the sibling later, test its
-// prune condition, and continue with its near child: popping the near child
-// at that same moment tests the near child's own interval instead, which
-// prunes whenever the sibling's would -- a child box lies inside its parent
-// box (boxes are unions), and the slab entry/exit distances are monotone in
-// the box under IEEE rounding.  So the visit order and every result are
-// unchanged; only the sibling's own pop and its line fetch disappear.
-// The instrumented kernels (STATS) keep plain BVH2 steps so node-visit counts
-// stay KIRK's.
 template <bool STATS, class Stack>
 __device__ __forceinline__ void interior_step(const DevScene& S, const TravRay& tr, float tlimit, Stack& stk, Cur& c,
                                               TravStats& st) {
@@ -329,38 +191,23 @@ __device__ __forceinline__ void interior_step(const DevScene& S, const TravRay& 
         return;
     }
     if (STATS) st.nodes++;
-    const uint32_t idx = c.ref & ~SIB_BIT;
-    const float4* np = reinterpret_cast<const float4*>(S.nodes + idx);
+    const float4* np = reinterpret_cast<const float4*>(S.nodes + c.ref);
     float4 a = np[0], b = np[1], cc = np[2];
     int4 rf = reinterpret_cast<const int4*>(np)[3];
     pin(a);
     pin(b);
     pin(cc);
     pin(rf);
-    if (!STATS && KHP_PAIR && (c.ref & SIB_BIT)) {
-        const float4* sp = reinterpret_cast<const float4*>(S.nodes + (idx ^ 1u));
-        float4 sa = sp[0], sb = sp[1], sc = sp[2];
-        int4 srf = reinterpret_cast<const int4*>(sp)[3];
-        float sl0, sl1, sr0, sr1;
-        bool slh = slab(sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, tr.r, tr.inv, sl0, sl1);
-        bool srh = slab(sb.z, sb.w, sc.x, sc.y, sc.z, sc.w, tr.r, tr.inv, sr0, sr1);
-        uint32_t dref;
-        float d0, d1;
-        stk.pop(dref, d0, d1);  // the sibling's own entry
-        push_children(stk, slh, srh, sl0, sl1, sr0, sr1, srf);
-    }
     float l0, l1, r0, r1;
     bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, l0, l1);
     bool rh = slab(b.z, b.w, cc.x, cc.y, cc.z, cc.w, tr.r, tr.inv, r0, r1);
     if (lh && rh) {
-        // both children interior -> they are a record pair; flag the near one
-        const uint32_t sib = (!STATS && KHP_PAIR && !ref_leaf((uint32_t)rf.x) && !ref_leaf((uint32_t)rf.y)) ? SIB_BIT : 0u;
         if (l0 < r0) {
             stk.push((uint32_t)rf.y, r0, r1);
-            c = Cur{(uint32_t)rf.x | sib, l0, l1, true};
+            c = Cur{(uint32_t)rf.x, l0, l1, true};
         } else {
             stk.push((uint32_t)rf.x, l0, l1);
-            c = Cur{(uint32_t)rf.y | sib, r0, r1, true};
+            c = Cur{(uint32_t)rf.y, r0, r1, true};
         }
     } else if (lh) {
         c = Cur{(uint32_t)rf.x, l0, l1, true};
@@ -378,14 +225,6 @@ __device__ __forceinline__ void leaf_candidate(float4 p0, float4 p1, float4 p2, 
                                                float& lv) {
     float t, u = 0.0f, v = 0.0f;
     bool ok;
-#if KHP_EXP_DOUBLE_CONE
-    {   // timing experiment only: an extra, discarded cone test
-        float tx;
-        bool okx = cone_closest(p0, p1, p2, p3, r, 0.0f, tMax + (float)slot * 0.0f, tx);
-        float sink = okx ? tx : 0.0f;
-        asm volatile("" : "+v"(sink));
-    }
-#endif
     if (is_tri(p0)) ok = tri_test(p0, p1, p2, r, 0.0f, tMax, t, u, v);
     else ok = cone_closest(p0, p1, p2, p3, r, 0.0f, tMax, t);
     if (ok) {
@@ -398,8 +237,7 @@ __device__ __forceinline__ void leaf_candidate(float4 p0, float4 p1, float4 p2, 
 }
 
 // Leaf entry, closest hit: prune test, then every candidate with tMin = 0 and
-// tMax = the leaf's exit distance (CPU_BVH.cpp:155-167).  The first two
-// records are fetched together, so a two-candidate leaf costs one round trip.
+// tMax = the leaf's exit distance (CPU_BVH.cpp:155-167).
 template <bool STATS, class Stack>
 __device__ __forceinline__ void leaf_step_closest(const DevScene& S, const TravRay& tr, Hit& h, Stack& stk, Cur& c,
                                                   TravStats& st) {
@@ -410,21 +248,7 @@ __device__ __forceinline__ void leaf_step_closest(const DevScene& S, const TravR
         float tl = FLT_MAX_, lu = 0.0f, lv = 0.0f, tMax = c.t1;
         int32_t sl = -1;
         if (STATS) st.prims += cnt;
-#if KHP_LEAF_PAIR
-        float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-        float4 b0, b1, b2, b3;
-        if (cnt > 1) {
-            b0 = p[4];
-            b1 = p[5];
-            b2 = p[6];
-            b3 = p[7];
-        }
-        leaf_candidate(a0, a1, a2, a3, (int32_t)first, tr.r, tMax, tl, sl, lu, lv);
-        if (cnt > 1) leaf_candidate(b0, b1, b2, b3, (int32_t)first + 1, tr.r, tMax, tl, sl, lu, lv);
-        for (uint32_t k = 2; k < cnt; ++k) {
-#else
         for (uint32_t k = 0; k < cnt; ++k) {
-#endif
             const float4* q = p + 4 * k;
             float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
             pin(q0);
@@ -461,25 +285,7 @@ __device__ __forceinline__ bool leaf_step_any(const DevScene& S, const TravRay& 
         if (STATS) st.nodes++;
         const uint32_t first = c.ref & 0x00FFFFFFu, cnt = leaf_count(S, c.ref);
         const float4* p = S.prims + 4 * (size_t)first;
-#if KHP_LEAF_PAIR
-        float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-        float4 b0, b1, b2, b3;
-        if (cnt > 1) {
-            b0 = p[4];
-            b1 = p[5];
-            b2 = p[6];
-            b3 = p[7];
-        }
-        if (STATS) st.prims++;
-        if (any_candidate(a0, a1, a2, a3, tr.r, tMaxRay)) return true;
-        if (cnt > 1) {
-            if (STATS) st.prims++;
-            if (any_candidate(b0, b1, b2, b3, tr.r, tMaxRay)) return true;
-        }
-        for (uint32_t k = 2; k < cnt; ++k) {
-#else
         for (uint32_t k = 0; k < cnt; ++k) {
-#endif
             const float4* q = p + 4 * k;
             float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
             pin(q0);
@@ -494,222 +300,15 @@ __device__ __forceinline__ bool leaf_step_any(const DevScene& S, const TravRay& 
     return false;
 }
 
-// ---- one-fetch-per-iteration traversal (the production kernels) -------------------------
-// A lane holds either an interior entry (cursor) or a partly tested leaf
-// (LeafCur).  Each wave iteration resolves the lane's next unit of work
-// (popping pruned entries, opening leaves), then fetches exactly ONE 64-B
-// record -- a node or a candidate primitive, from the same instruction
-// stream -- and then runs the slab pair or the one candidate test.  Every
-// iteration thus costs one memory round trip, whatever mix of interior and
-// leaf work its lanes carry.  Visit order and arithmetic are those of
-// interior_step / leaf_step_*: candidates of a leaf are tested in order with
-// the leaf's window, and entries are prune-tested when they are popped.
-struct LeafCur {
-    uint32_t slot, left;  // next candidate slot, candidates still to test (0: not in a leaf)
-    float tmax;           // closest: the leaf window (shrinks on hits); any: unused
-    float tl, lu, lv;     // closest: best candidate of this leaf so far
-    int32_t sl;
-};
-
-// Open the leaf in the cursor: KIRK's leaf prologue (CPU_BVH.cpp:155-159).
-template <bool STATS>
-__device__ __forceinline__ void leaf_open(const DevScene& S, const Cur& c, LeafCur& lf, TravStats& st) {
-    if (STATS) st.nodes++;
-    lf.slot = c.ref & 0x00FFFFFFu;
-    lf.left = leaf_count(S, c.ref);
-    lf.tmax = c.t1;
-    lf.tl = FLT_MAX_;
-    lf.lu = lf.lv = 0.0f;
-    lf.sl = -1;
-}
-
-// Resolve the lane's next unit of work against `tlimit` (closest: current hit
-// t; any: the ray's tMax).  Returns false when the ray is finished.
-template <bool STATS, class Stack>
-__device__ __forceinline__ bool resolve(const DevScene& S, float tlimit, Stack& stk, Cur& c, LeafCur& lf,
-                                        TravStats& st) {
-    if (lf.left > 0) return true;
-    while (c.valid) {
-        if (c.t1 < 0.0f || c.t0 > tlimit) {  // pruned at pop time
-            if (STATS) st.pruned++;
-            cur_next(stk, c);
-            continue;
-        }
-        if (ref_leaf(c.ref)) {
-            leaf_open<STATS>(S, c, lf, st);
-            return true;
-        }
-        return true;  // interior: fetched this iteration
-    }
-    return false;
-}
-
-// The record this lane needs this iteration.
-__device__ __forceinline__ const float4* work_record(const DevScene& S, const Cur& c, const LeafCur& lf) {
-    return lf.left > 0 ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
-}
-
-// Interior work on a fetched record (prune test already done in resolve).
-#ifndef KHP_PUSH_PRUNE
-#define KHP_PUSH_PRUNE 1   // apply the pop-time prune test to children before they are pushed
-#endif
-// PUSH_PRUNE: a child that would fail the prune test `t1 < 0 || t0 > tlimit`
-// when popped is dropped now.  tlimit only ever decreases (closest hit) or is
-// fixed (any hit), so such a child is certain to be pruned later; the live
-// entries, their order and every visit (the counts included) are unchanged.
-template <bool STATS, class Stack>
-__device__ __forceinline__ void interior_apply(const TravRay& tr, float4 a, float4 b, float4 cc, int4 rf, Stack& stk,
-                                               Cur& c, TravStats& st, float tlimit) {
-    if (STATS) st.nodes++;
-    float l0, l1, r0, r1;
-#if KHP_EXP_DOUBLE_SLAB
-    {   // timing experiment only: an extra, discarded slab pair
-        float x0, x1, y0, y1;
-        bool xa = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, x0, x1);
-        bool ya = slab(b.z, b.w, cc.x, cc.y, cc.z, cc.w, tr.r, tr.inv, y0, y1);
-        float sink = (xa ? x0 : x1) + (ya ? y0 : y1);
-        asm volatile("" : "+v"(sink));
-    }
-#endif
-    bool lh = slab(a.x, a.y, a.z, a.w, b.x, b.y, tr.r, tr.inv, l0, l1);
-    bool rh = slab(b.z, b.w, cc.x, cc.y, cc.z, cc.w, tr.r, tr.inv, r0, r1);
-#if KHP_PUSH_PRUNE
-    lh = lh && !(l1 < 0.0f || l0 > tlimit);
-    rh = rh && !(r1 < 0.0f || r0 > tlimit);
-#else
-    (void)tlimit;
-#endif
-    if (lh && rh) {
-        if (l0 < r0) {
-            stk.push((uint32_t)rf.y, r0, r1);
-            c = Cur{(uint32_t)rf.x, l0, l1, true};
-        } else {
-            stk.push((uint32_t)rf.x, l0, l1);
-            c = Cur{(uint32_t)rf.y, r0, r1, true};
-        }
-    } else if (lh) {
-        c = Cur{(uint32_t)rf.x, l0, l1, true};
-    } else if (rh) {
-        c = Cur{(uint32_t)rf.y, r0, r1, true};
-    } else {
-        cur_next(stk, c);
-    }
-}
-
-#ifndef KHP_PREFETCH
-#define KHP_PREFETCH 0   // 1: child-line prefetch (exact; measured 12 % slower, single-ray latency unchanged)
-#endif
-// Child-line prefetch.  As soon as an interior record arrives, one 4-B load
-// per child pulls the line the next iteration will fetch (a node record, or
-// the leaf's first candidate) towards the CU, so that latency overlaps this
-// iteration's slab work.  The loads are inline asm so the compiler does not
-// wait for them; their destination registers (Prefetch) stay live until the
-// next fetch has been waited for, and vmcnt retires in order, so the
-// registers cannot be reused while a load is still in flight.
-struct Prefetch {
-    float d0, d1;
-};
-__device__ __forceinline__ const void* child_line(const DevScene& S, uint32_t ref) {
-    return ref_leaf(ref) ? (const void*)(S.prims + 4 * (size_t)(ref & 0x00FFFFFFu))
-                         : (const void*)(S.nodes + ref);
-}
-__device__ __forceinline__ void prefetch_children(const DevScene& S, int4 rf, Prefetch& pf) {
-#if KHP_PREFETCH
-    asm volatile("global_load_dword %0, %1, off" : "=v"(pf.d0) : "v"(child_line(S, (uint32_t)rf.x)) : "memory");
-    asm volatile("global_load_dword %0, %1, off" : "=v"(pf.d1) : "v"(child_line(S, (uint32_t)rf.y)) : "memory");
-#endif
-}
-// After a fetch has been waited for (pin): older prefetches are complete.
-__device__ __forceinline__ void prefetch_retire(Prefetch& pf) {
-#if KHP_PREFETCH
-    asm volatile("" : "+v"(pf.d0), "+v"(pf.d1));
-#endif
-}
-
-// One closest-hit iteration for a lane that resolved to work.
-template <bool STATS, class Stack>
-__device__ __forceinline__ void step1_closest(const DevScene& S, const TravRay& tr, Hit& h, Stack& stk, Cur& c,
-                                              LeafCur& lf, TravStats& st, Prefetch& pf) {
-    const float4* p = work_record(S, c, lf);
-    float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-#if KHP_PIN1 || KHP_PREFETCH
-    pin(q0); pin(q1); pin(q2); pin(q3);
-#endif
-    prefetch_retire(pf);
-    if (lf.left > 0) {
-        if (STATS) st.prims++;
-        leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);
-        ++lf.slot;
-        if (--lf.left == 0) {
-            if (lf.sl >= 0 && lf.tl < h.t) {
-                h.t = lf.tl;
-                h.slot = lf.sl;
-                h.u = lf.lu;
-                h.v = lf.lv;
-            }
-            cur_next(stk, c);
-        }
-    } else {
-        int4 rf = make_int4(__float_as_int(q3.x), __float_as_int(q3.y), __float_as_int(q3.z), __float_as_int(q3.w));
-        prefetch_children(S, rf, pf);
-        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st, h.t);
-    }
-}
-
-// step1_closest on an already fetched record (diagnostic timing build).
-template <bool STATS, class Stack>
-__device__ __forceinline__ void step1_closest_rec(const TravRay& tr, Hit& h, Stack& stk, Cur& c, LeafCur& lf,
-                                                  TravStats& st, float4 q0, float4 q1, float4 q2, float4 q3) {
-    if (lf.left > 0) {
-        if (STATS) st.prims++;
-        leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);
-        ++lf.slot;
-        if (--lf.left == 0) {
-            if (lf.sl >= 0 && lf.tl < h.t) {
-                h.t = lf.tl;
-                h.slot = lf.sl;
-                h.u = lf.lu;
-                h.v = lf.lv;
-            }
-            cur_next(stk, c);
-        }
-    } else {
-        int4 rf = make_int4(__float_as_int(q3.x), __float_as_int(q3.y), __float_as_int(q3.z), __float_as_int(q3.w));
-        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st, h.t);
-    }
-}
-
-// One any-hit iteration; returns true when an occluder is found.
-template <bool STATS, class Stack>
-__device__ __forceinline__ bool step1_any(const DevScene& S, const TravRay& tr, float tMaxRay, Stack& stk, Cur& c,
-                                          LeafCur& lf, TravStats& st, Prefetch& pf) {
-    const float4* p = work_record(S, c, lf);
-    float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-#if KHP_PIN1 || KHP_PREFETCH
-    pin(q0); pin(q1); pin(q2); pin(q3);
-#endif
-    prefetch_retire(pf);
-    if (lf.left > 0) {
-        if (STATS) st.prims++;
-        if (any_candidate(q0, q1, q2, q3, tr.r, tMaxRay)) return true;
-        ++lf.slot;
-        if (--lf.left == 0) cur_next(stk, c);
-    } else {
-        int4 rf = make_int4(__float_as_int(q3.x), __float_as_int(q3.y), __float_as_int(q3.z), __float_as_int(q3.w));
-        prefetch_children(S, rf, pf);
-        interior_apply<STATS>(tr, q0, q1, q2, rf, stk, c, st, tMaxRay);
-    }
-    return false;
-}
-
 // ---- select-based one-fetch loop (the production kernels) -------------------------------
-// The same visit order and arithmetic as resolve + step1_*, restructured so
-// that a wave iteration has one fetch site, one push site and one pop site
-// instead of a pop inside every branch (interior miss, leaf done, pruned
-// entry) and a pop loop in resolve.  The compiler turns each divergent
-// branch into exec-mask bookkeeping on the scalar unit, and the old shape
-// cost ~185 SALU instructions per wave iteration -- the scalar unit, which
-// the 4 SIMDs of a CU share, was ~75 % busy (profiles/r01g, `mix` pass).
+// A lane holds either an interior entry (cursor) or a partly tested leaf
+// (LeafCur).  Each wave iteration loads exactly ONE 64-B record -- a node or
+// a candidate primitive -- through one instruction stream, runs the slab pair
+// or the one candidate test, and does at most one push and one pop, with every
+// branch written as selects.  The divergent form this replaced (a pop inside
+// every branch and a pop loop) cost ~185 SALU instructions per wave iteration
+// on exec-mask bookkeeping; the scalar unit, which the 4 SIMDs of a CU share,
+// was ~75 % busy (profiles/r01g, `mix` pass).
 // A lane is in one of four modes:
 //   M_NODE  the cursor (c) is an interior entry that passed its prune test;
 //   M_LEAF  the lane is testing the candidates of an opened leaf (lf);
@@ -717,11 +316,20 @@ __device__ __forceinline__ bool step1_any(const DevScene& S, const TravRay& tr, 
 //           its prune test: instead of looping, the lane pops again in the
 //           next iteration -- 1.2 such pops per ray against ~110 iterations);
 //   M_IDLE  no ray.
-// Entries are prune-tested exactly when KIRK would pop them, and
-// push-time pruning (KHP_PUSH_PRUNE) applies as in interior_apply.
-#ifndef KHP_LOOP2
-#define KHP_LOOP2 1
-#endif
+// Visit order and arithmetic are those of interior_step / leaf_step_*:
+// candidates of a leaf are tested in order with the leaf's window, and entries
+// are prune-tested exactly when KIRK would pop them.  Push-time pruning: a
+// child that would fail the prune test `t1 < 0 || t0 > tlimit` when popped is
+// dropped at once -- tlimit only ever decreases (closest hit) or is fixed (any
+// hit), so it is certain to be pruned later; the live entries, their order and
+// every visit (the counts included) are unchanged.
+struct LeafCur {
+    uint32_t slot, left;  // next candidate slot, candidates still to test (0: not in a leaf)
+    float tmax;           // closest: the leaf window (shrinks on hits); any: unused
+    float tl, lu, lv;     // closest: best candidate of this leaf so far
+    int32_t sl;
+};
+
 enum : uint32_t { M_IDLE = 0u, M_NODE = 1u, M_LEAF = 2u, M_POP = 3u };
 
 // BoundingVolume::intersects as selects: every IEEE operation of slab() is
@@ -753,9 +361,6 @@ __device__ __forceinline__ bool slab_sel(float mnx, float mny, float mnz, float 
 // (each axis' own entry <= exit).  t0/t1 are bit-identical up to the sign of a
 // zero, which no comparison downstream distinguishes.  Rays with an infinite
 // component (0 * inf = NaN cases) take slab_sel.
-#ifndef KHP_FAST_SLAB
-#define KHP_FAST_SLAB 1
-#endif
 __device__ __forceinline__ bool slab_fast(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
                                           const TravRay& tr, float& t0, float& t1) {
     const float ax = (mnx - tr.r.o.x) * tr.inv.x, bx = (mxx - tr.r.o.x) * tr.inv.x;
@@ -764,18 +369,6 @@ __device__ __forceinline__ bool slab_fast(float mnx, float mny, float mnz, float
     t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
     t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
     return t0 <= t1;
-}
-
-#ifndef KHP_SLAB_SEL
-#define KHP_SLAB_SEL 1
-#endif
-__device__ __forceinline__ bool slab2(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
-                                      const TravRay& tr, float& t0, float& t1) {
-#if KHP_SLAB_SEL
-    return slab_sel(mnx, mny, mnz, mxx, mxy, mxz, tr, t0, t1);
-#else
-    return slab(mnx, mny, mnz, mxx, mxy, mxz, tr.r, tr.inv, t0, t1);
-#endif
 }
 
 // A new entry that passed its prune test becomes the lane's work: an interior
@@ -820,35 +413,30 @@ __device__ __forceinline__ bool trav2_begin(const DevScene& S, const TravRay& tr
     return true;
 }
 
-// One wave iteration of one lane (mode != M_IDLE).  ANY: any-hit with the
-// fixed limit tlimit = the ray's tMax; else closest hit, tlimit = h.t.
-// Returns true when the ray is finished; for ANY, `occluded` tells the result.
-// Tail prefetch (KHP_TAIL_PF): once a launch's queue is drained, the few
-// rays still running decide its duration, and each of their iterations waits
-// a full HBM round trip for the record it fetches.  In that phase the memory
-// system is idle, so as soon as an interior record's child boxes are tested,
-// the lines of the children that will be visited (the near one next
-// iteration, the pushed far one later) are requested with plain dword loads
-// whose results are discarded (`tail_pf` set by the caller, wave-uniform).
-// The loaded registers stay live until the next fetch has been waited for;
-// vmcnt retires loads in order, so they cannot be reused while in flight.
-// Exactness is unaffected: nothing reads the prefetched values.
-#ifndef KHP_TAIL_PF
-#define KHP_TAIL_PF 1
-#endif
-#ifndef KHP_ANY_ORDER
-#define KHP_ANY_ORDER 0  // any-hit child order: 0 KIRK's (near first), 1 far, 2 leaf, 3 longer overlap
-#endif
-#ifndef KHP_ANY_PAIR
-#define KHP_ANY_PAIR 0
-#endif
-#ifndef KHP_TAIL_PF_LANES
-#define KHP_TAIL_PF_LANES 64   // prefetch when the queue is drained and at most this many lanes are busy
-#endif
+// Tail prefetch: once a launch's queue is drained, the few rays still running
+// decide its duration, and each of their iterations waits a full HBM round
+// trip for the record it fetches.  In that phase the memory system is idle,
+// so as soon as an interior record's child boxes are tested, the lines of the
+// children that will be visited (the near one next iteration, the pushed far
+// one later) are requested with plain dword loads whose results are
+// discarded (`tail_pf` set by the caller, wave-uniform).  The loaded
+// registers stay live until the next fetch has been waited for; vmcnt retires
+// loads in order, so they cannot be reused while in flight.  Exactness is
+// unaffected: nothing reads the prefetched values.
+struct Prefetch {
+    float d0, d1;
+};
+__device__ __forceinline__ const void* child_line(const DevScene& S, uint32_t ref) {
+    return ref_leaf(ref) ? (const void*)(S.prims + 4 * (size_t)(ref & 0x00FFFFFFu))
+                         : (const void*)(S.nodes + ref);
+}
 __device__ __forceinline__ void pf_line(const DevScene& S, uint32_t ref, float& d) {
     asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(child_line(S, ref)) : "memory");
 }
 
+// One wave iteration of one lane (mode != M_IDLE).  ANY: any-hit with the
+// fixed limit tlimit = the ray's tMax; else closest hit, tlimit = h.t.
+// Returns true when the ray is finished; for ANY, `occluded` tells the result.
 template <bool ANY, bool STATS, class Stack>
 __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
                                       uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded,
@@ -857,31 +445,14 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
     const bool fetch = in_leaf || mode == M_NODE;
     const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
     float4 q0, q1, q2, q3;
-    // KHP_ANY_PAIR: an any-hit lane in a leaf with >= 2 candidates left loads
-    // and tests the next candidate too (same 128-B line for even-aligned leaf
-    // pairs).  Any-hit results do not depend on the order of tests, and the
-    // instrumented count stops at the first occluder as KIRK's loop does.
-    const bool pair = KHP_ANY_PAIR && ANY && in_leaf && lf.left >= 2u;
-    float4 q4, q5, q6, q7;
     if (fetch) {
         q0 = p[0];
         q1 = p[1];
         q2 = p[2];
         q3 = p[3];
-        if (pair) {
-            q4 = p[4];
-            q5 = p[5];
-            q6 = p[6];
-            q7 = p[7];
-        }
         pin(q0); pin(q1); pin(q2); pin(q3);
-        if (pair) {
-            pin(q4); pin(q5); pin(q6); pin(q7);
-        }
     }
-#if KHP_TAIL_PF
     asm volatile("" : "+v"(pf.d0), "+v"(pf.d1));  // prefetches issued last iteration are complete here
-#endif
     bool need_pop = mode == M_POP;
     bool have = false;  // a new entry (ref, t0, t1) for take_entry
     uint32_t eref = 0u;
@@ -895,15 +466,6 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
             if (any_candidate(q0, q1, q2, q3, tr.r, tmax_any)) {
                 occluded = true;
                 return true;
-            }
-            if (pair) {
-                if (STATS) st.prims++;
-                if (any_candidate(q4, q5, q6, q7, tr.r, tmax_any)) {
-                    occluded = true;
-                    return true;
-                }
-                ++lf.slot;
-                --lf.left;
             }
         } else {
             leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);
@@ -924,31 +486,17 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
         const float tlimit = ANY ? tmax_any : h.t;
         float l0, l1, r0, r1;
         bool lh, rh;
-        if (KHP_FAST_SLAB && __ballot(!tr.fin) == 0ull) {  // wave-uniform
+        if (__ballot(!tr.fin) == 0ull) {  // wave-uniform
             lh = slab_fast(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, tr, l0, l1);
             rh = slab_fast(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, tr, r0, r1);
         } else {
-            lh = slab2(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, tr, l0, l1);
-            rh = slab2(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, tr, r0, r1);
+            lh = slab_sel(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, tr, l0, l1);
+            rh = slab_sel(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, tr, r0, r1);
         }
         lh = lh && !(l1 < 0.0f || l0 > tlimit);
         rh = rh && !(r1 < 0.0f || r0 > tlimit);
         const uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
-        bool nearl = lh && (!rh || l0 < r0);  // KIRK: left first iff l0 < r0 (ties: right)
-#if KHP_ANY_ORDER
-        // any-hit: the boolean does not depend on the visiting order (every
-        // entry KIRK would test is still tested until the first hit)
-        if (ANY && lh && rh) {
-#if KHP_ANY_ORDER == 1
-            nearl = !nearl;  // far child first
-#elif KHP_ANY_ORDER == 2
-            const bool ll = ref_leaf(lref), rl = ref_leaf(rref);
-            if (ll != rl) nearl = ll;  // a leaf child first
-#elif KHP_ANY_ORDER == 3
-            nearl = (l1 - l0) >= (r1 - r0);  // longer overlap first
-#endif
-        }
-#endif
+        const bool nearl = lh && (!rh || l0 < r0);  // KIRK: left first iff l0 < r0 (ties: right)
         have = lh || rh;
         need_pop = !have;
         push = lh && rh;
@@ -958,12 +506,10 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
         pref = nearl ? rref : lref;
         pt0 = nearl ? r0 : l0;
         pt1 = nearl ? r1 : l1;
-#if KHP_TAIL_PF
         if (tail_pf) {
             if (have) pf_line(S, eref, pf.d0);
             if (push) pf_line(S, pref, pf.d1);
         }
-#endif
     }
     if (push) stk.push(pref, pt0, pt1);
     if (need_pop) {

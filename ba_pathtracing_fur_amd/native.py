@@ -86,11 +86,20 @@ class Stats(ctypes.Structure):
                 ("flatten_ms", c_double), ("bvh_ms", c_double), ("bvh_kernel_ms", c_double), ("layout_ms", c_double),
                 ("flatten_kernel_ms", c_double), ("layout_kernel_ms", c_double),
                 ("extend_pruned_pops", c_uint64), ("shadow_pruned_pops", c_uint64), ("frames", c_uint64),
-                ("extend_busy_ms", c_double)]
+                ("extend_busy_ms", c_double), ("shadow_finish_ms", c_double), ("shadow_launches", c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if not isinstance(getattr(self, k), (int, float)) else getattr(self, k))
                 for k, _ in self._fields_}
+
+
+class CtxParams(ctypes.Structure):
+    """khp_ctx_params (ABI 6): scheduling knobs of a context; no value changes any result."""
+    _fields_ = [("fuse_frames", c_uint32), ("frames_in_flight", c_uint32), ("chunk_paths", c_uint64),
+                ("heavy_iters", c_uint32), ("dump_bounce", c_int32), ("trace_kernels", c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class Tonemap(ctypes.Structure):
@@ -119,7 +128,7 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_read_rgba8", "khp_tonemap_defaults", "khp_read_bvh",
             "khp_read_layout", "khp_set_scene_device", "khp_gen_hairball_device", "khp_device_alloc",
             "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device",
-            "khp_sync"]
+            "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params"]
 
 _lib = None
 
@@ -151,6 +160,9 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_build_accel": (c_int, [c_void_p]),
         "khp_render": (c_int, [c_void_p, P(RenderParams), c_void_p]),
         "khp_sync": (c_int, [c_void_p]),
+        "khp_ctx_params_defaults": (None, [P(CtxParams)]),
+        "khp_set_params": (c_int, [c_void_p, P(CtxParams)]),
+        "khp_get_params": (c_int, [c_void_p, P(CtxParams)]),
         "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
         "khp_read_rgba8": (c_int, [c_void_p, P(Tonemap), P(c_uint8)]),
         "khp_tonemap_defaults": (None, [P(Tonemap)]),

@@ -158,6 +158,25 @@ class HipContext:
     def build_accel(self):
         N.check(self.lib, self.lib.khp_build_accel(self.ptr), "khp_build_accel")
 
+    def params(self) -> dict:
+        """khp_get_params: the context's scheduling parameters (khp_ctx_params)."""
+        prm = N.CtxParams()
+        N.check(self.lib, self.lib.khp_get_params(self.ptr, ctypes.byref(prm)), "khp_get_params")
+        return prm.as_dict()
+
+    def set_params(self, **kw) -> dict:
+        """khp_set_params with the given fields changed (fuse_frames, frames_in_flight,
+        chunk_paths, heavy_iters, dump_bounce, trace_kernels); returns the previous values."""
+        prm = N.CtxParams()
+        N.check(self.lib, self.lib.khp_get_params(self.ptr, ctypes.byref(prm)), "khp_get_params")
+        old = prm.as_dict()
+        for k, v in kw.items():
+            if k not in old:
+                raise AttributeError(f"khp_ctx_params has no field {k}")
+            setattr(prm, k, int(v))
+        N.check(self.lib, self.lib.khp_set_params(self.ptr, ctypes.byref(prm)), "khp_set_params")
+        return old
+
     def render(self, width, height, spp, depth, seed=0x4B49524B, first_sample=0, tile_size=64, tile_rank=0,
                tile_nranks=1, out: np.ndarray | None = None, readback=True, stats=False,
                async_: bool = False) -> np.ndarray | None:

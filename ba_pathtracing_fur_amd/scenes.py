@@ -367,6 +367,20 @@ def config5(width=3840, height=2160, n_strands=1_000_000, torus_grid=500, glass_
     return sd
 
 
+def config5_device(ctx, width=3840, height=2160, n_strands=1_000_000, torus_grid=500,
+                   glass_subdiv=5) -> SceneData:
+    """config5 with the hairball generated and flattened on the GPU of `ctx`
+    (as config3_device); the torus and the glass sphere come from the host.
+    The same objects in the same order as config5 (triangles, then cones)."""
+    sd = config5(width, height, 0, torus_grid, glass_subdiv)
+    sd.name = f"mixed_{n_strands}_device"
+    base, apex, nc = ctx.hairball_device(n_strands, (0.0, 1.0, 0.0), 1.0)
+    ctx.set_scene_device(sd, cones=(base, apex, nc, 1))
+    base.free()
+    apex.free()
+    return sd
+
+
 def zoo(width=64, height=48, n_strands=400) -> SceneData:
     """Every BSDF of the zoo (Bsdf.cpp) and every light kind (Light.cpp) in one frame.
 

@@ -2,73 +2,138 @@
 """Headline benchmark: Msamples/s at 1080p 8 spp on the 1M-strand hairball.
 
 BASELINE.json metric: "Msamples/s at 1080p 8spp, 1M-strand hairball; achieved
-HBM GB/s vs peak".  Workload = config 3's scene (1M strands -> 9M cone frusta
-on a 2-triangle plane, 2x2 quad light, sky environment) rendered at
-1920x1080, 8 spp, depth 5 (SURVEY §8(d) "Metric row").
+HBM GB/s vs peak".  Default workload (--config metric) = config 3's scene (1M
+strands -> 9M cone frusta on a 2-triangle plane, 2x2 quad light, sky
+environment) at 1920x1080, 8 spp, depth 5 (SURVEY §8(d) "Metric row").  The
+other BASELINE configs run with --config 1 | 2 | 3 | 5 (their own scene, size
+and spp).
 
-One step = one full frame (16.6M camera samples) through the HIP wavefront
-core, inputs (scene + BVH) resident in HBM, framebuffer left in HBM.  With
---gpus N (torchrun, one process per GPU) the frame is tile-sharded
-(64x64 tiles, tile_id % N) and each step ends with the RCCL framebuffer
-gather to rank 0; total work is fixed, so scaling is "strong".
+One step = one progressive pass of KIRK's PathTracer::render loop
+(CPU_PathTracer.cpp:17-52) over the whole frame: step k renders samples
+[k*spp, (k+1)*spp) of every pixel and folds them into the running mean, so
+every step traces new samples.  Inputs (scene + BVH) are resident in HBM, the
+framebuffer stays in HBM.  Steps are enqueued asynchronously (KHP_RENDER_ASYNC)
+and consecutive passes with equal parameters are fused into one wavefront
+(khp_ctx_params.fuse_frames, default 32); the timed region ends with khp_sync +
+a barrier, so every pass is complete.  `sync_steps` in the JSON line is the
+same workload with a host wait after every pass (no fusion, no overlap).
 
-Steps are pipelined (default): each frame is enqueued asynchronously
-(KHP_RENDER_ASYNC) and up to two frames run on the device at once, so one
-frame's chain of 2 x depth persistent launches -- each ending only when its
-slowest ray does -- overlaps the other frame's work; frames still complete and
-accumulate in order, and the timed region ends with khp_sync + a barrier.
---sync-steps waits for every frame before starting the next.
+--gpus N: one process per GPU.  Under torchrun (WORLD_SIZE set) each rank
+renders the 64x64 tiles t with t % N == rank and every step ends with the RCCL
+framebuffer gather to rank 0; total work is fixed, so scaling is "strong".
+Without WORLD_SIZE, `python bench.py --gpus N` starts those N ranks itself
+(torch.distributed.run as a child process, before this process touches a GPU)
+and exits with its status.
 
 The JSON line also carries:
   roofline     -- the extend (closest-hit) kernel: algorithmic bytes
                   (28 B ray + 32 B per visited node + 32 B per
                   primitive test + 16 B hit, visit counts from an instrumented
-                  frame) of all timed launches / the time during which at
+                  pass) of all timed launches / the time during which at
                   least one of them was running (union of their HIP-event
-                  intervals), against 8 TB/s HBM.  Without overlap
-                  (--sync-steps) that is bytes per launch / average launch
-                  time; avg_launch_ms and achieved_per_launch give the
-                  per-launch view (launch durations include the time the
-                  other frame's kernels shared the chip);
-  cpu_baseline -- the C restatement (oracle/) timed on this host's cores on a
-                  bounded sample of the same frame: progressive full-frame
-                  samples 0, 1, ... until --cpu-seconds or the workload's spp.
+                  intervals), against 8 TB/s HBM; roofline.shadow is the same
+                  for the any-hit kernel (28 B + 32 B per node/prim + 4 B);
+  cpu_baseline -- the C restatement (oracle/) timed on the host cores this
+                  process may use, on a bounded sample of the same frame.
 """
 from __future__ import annotations
 
 import argparse
 import glob
 import json
+import math
 import os
+import subprocess
 import sys
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "Msamples/s at 1080p 8spp, 1M-strand hairball; achieved HBM GB/s vs peak"
+
+# BASELINE.json configs (SURVEY §8(d)): scene builder, width, height, spp, default steps/warmup
+CONFIGS = {
+    "metric": dict(scene="config3", width=1920, height=1080, spp=8, strands=1_000_000, steps=32, warmup=16,
+                   what="config 3 scene at the metric row: 1M-strand hairball on a diffuse plane + 2x2 area light"),
+    "1": dict(scene="config1", width=256, height=256, spp=4, strands=0, steps=64, warmup=16,
+              what="config 1: Cornell box + 1 Lambert icosphere (5,120 tris)"),
+    "2": dict(scene="config2", width=1920, height=1080, spp=8, strands=10_000, steps=32, warmup=16,
+              what="config 2: Cornell box + 10k-strand procedural hairball (90k cones), Marschner fur"),
+    "3": dict(scene="config3", width=1920, height=1080, spp=16, strands=1_000_000, steps=32, warmup=16,
+              what="config 3: 1M-strand hairball on a diffuse plane + 2x2 area light, 16 spp"),
+    "5": dict(scene="config5", width=3840, height=2160, spp=32, strands=1_000_000, steps=4, warmup=2,
+              what="config 5: 1M-strand hairball + 500k-tri torus + glass icosphere (20,480 tris), 4K"),
+}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
-    ap.add_argument("--warmup", type=int, default=16)
-    ap.add_argument("--strands", type=int, default=1_000_000)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--strands", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--sync-check-steps", type=int, default=4,
+                    help="passes timed with a host wait after each (the sync_steps field; 0: skip)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--sync-steps", action="store_true",
-                    help="wait for each frame before the next (no frame pipelining)")
     ap.add_argument("--host-scene", action="store_true",
                     help="generate + flatten + build on the host (the pre-(f)1/(f)2 path) instead of in HBM")
-    return ap.parse_args()
+    a = ap.parse_args()
+    cfg = CONFIGS[a.config]
+    for k in ("steps", "warmup", "strands", "width", "height", "spp"):
+        if getattr(a, k) is None:
+            setattr(a, k, cfg[k])
+    return a
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without torchrun: run N ranks as a child process group
+    (no GPU has been touched in this process) and return their exit status."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench: launching", " ".join(cmd))
+    return subprocess.call(cmd)
+
+
+def available_cores() -> tuple[int, str]:
+    """Host cores this process may use: the CPU affinity set, capped by a cgroup
+    CPU quota when one is set (cpu.max), and where the figure came from."""
+    n = len(os.sched_getaffinity(0))
+    src = "sched_getaffinity"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, math.floor(int(quota) / int(period)))
+            if q < n:
+                n, src = q, "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    return n, src
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(sd, args, budget_s):
@@ -76,7 +141,7 @@ def cpu_baseline(sd, args, budget_s):
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle_ffi  # test infrastructure: only bench's cpu_baseline leg uses it
 
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads, cores_src = available_cores()
     t0 = time.time()
     o = oracle_ffi.Oracle(sd)
     build_s = time.time() - t0
@@ -109,16 +174,19 @@ def cpu_baseline(sd, args, budget_s):
         samples = rows * W
         what = f"{rows} of {H} rows (every {step}th) x {W} px x 1 spp"
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{what} of the same frame = {samples} samples in {dt:.1f} s ({threads} threads, "
-                      f"CPU restatement oracle/, -O3 x86-64-v3, same seeds); throughput is spp-linear; "
-                      f"oracle BVH build {build_s:.1f} s excluded"}
+            "cpu": cpu_model(), "cores_from": cores_src,
+            "sample": f"{what} of the same frame = {samples} samples in {dt:.1f} s ({threads} threads = every "
+                      f"core this process may use, {cpu_model()}; CPU restatement oracle/, -O3 x86-64-v3, same "
+                      f"seeds); throughput is spp-linear; oracle BVH build {build_s:.1f} s excluded"}
 
 
-def pmc_traffic(frames_per_launch: float):
-    """HBM bytes per k_extend launch from the committed PMC profile, scaled to
-    this run's frames per launch (the profile records how many fused frames
-    its launches carried), or None."""
+def pmc_traffic(frames_per_launch: float, config: str):
+    """HBM bytes per k_extend launch from the committed PMC profile of this
+    workload, scaled to this run's frames per launch (the profile records how
+    many fused frames its launches carried), or None."""
     files = sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_extend_*.json")))
+    files = [f for f in files if ("_cfg" not in f) == (config == "metric") and
+             (config == "metric" or f"_cfg{config}_" in f)]
     if not files:
         return None
     try:
@@ -129,12 +197,39 @@ def pmc_traffic(frames_per_launch: float):
         return None
 
 
+def build_scene(ctx, args, scenes):
+    """The configured scene, in HBM.  The hairball of configs 3/5/metric is
+    generated and flattened on the device unless --host-scene."""
+    name = CONFIGS[args.config]["scene"]
+    W, H = args.width, args.height
+    if args.host_scene or name in ("config1", "config2"):
+        kw = {} if name == "config1" else {"n_strands": args.strands}
+        sd = scenes.build_config(name, width=W, height=H, **kw)
+        ctx.set_scene(sd)
+        return sd, "host"
+    if name == "config3":
+        return scenes.config3_device(ctx, W, H, n_strands=args.strands), "device"
+    return scenes.config5_device(ctx, W, H, n_strands=args.strands), "device"
+
+
+def host_scene_for_oracle(sd, args, scenes):
+    name = CONFIGS[args.config]["scene"]
+    if args.host_scene or name in ("config1", "config2"):
+        return sd
+    kw = {"n_strands": args.strands}
+    return scenes.build_config(name, width=args.width, height=args.height, **kw)
+
+
 def main():
     args = parse()
     sys.path.insert(0, HERE)
     from ba_pathtracing_fur_amd.sharding import ShardedFrame, env_ranks
 
     rank, local_rank, world = env_ranks()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if world != args.gpus:
+        log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; the line reports the {world} ranks that ran")
     dist = None
     if world > 1:
         import torch  # noqa: F401  (load torch's HIP runtime before libkirk_hip.so)
@@ -146,20 +241,14 @@ def main():
     W, H, spp, depth = args.width, args.height, args.spp, args.depth
     ctx = HipContext(device=local_rank, host_build=args.host_scene)
     t0 = time.time()
-    if args.host_scene:
-        sd = scenes.config3(W, H, n_strands=args.strands)
-        gen_s = time.time() - t0
-        t0 = time.time()
-        ctx.set_scene(sd)
-    else:  # hairball generated and flattened in HBM
-        sd = scenes.config3_device(ctx, W, H, n_strands=args.strands)
-        gen_s = time.time() - t0
-        t0 = time.time()
+    sd, path = build_scene(ctx, args, scenes)
+    gen_s = time.time() - t0
+    t0 = time.time()
     ctx.build_accel()
     build_s = time.time() - t0
     st0 = ctx.stats()
     n_objects = st0["n_objects"]
-    setup = {"path": "host" if args.host_scene else "device", "gen_s": round(gen_s, 4),
+    setup = {"path": path, "gen_s": round(gen_s, 4),
              "flatten_ms": round(st0["flatten_ms"], 2), "bvh_ms": round(st0["bvh_ms"], 2),
              "bvh_kernel_ms": round(st0["bvh_kernel_ms"], 2), "layout_ms": round(st0["layout_ms"], 2),
              "upload_ms": round(st0["upload_ms"], 2), "build_accel_s": round(build_s, 4)}
@@ -167,21 +256,18 @@ def main():
         log(f"scene: {n_objects} objects, gen+flatten {gen_s:.3f}s, BVH+layout {build_s:.3f}s "
             f"({setup}), depth {st0['bvh_depth']}, nodes {st0['n_nodes']}, HBM {st0['device_bytes'] / 1e9:.2f} GB")
     frame = ShardedFrame(ctx, rank, world, dist, tile=args.tile)
-    ext_ms_acc = []
+    params = ctx.params()
+    k = 0  # progressive pass counter: pass k renders samples [k*spp, (k+1)*spp)
 
-    pipelined = not args.sync_steps
-
-    def step(stats=False):
-        # pipelined (default): the frame and its gather are enqueued and the next
-        # step starts at once, so consecutive frames overlap on the device (each
-        # frame alone is a chain of 2 x depth persistent launches that each wait
-        # for their slowest ray); frames still complete and accumulate in order.
-        frame.render(W, H, spp, depth, stats=stats, async_=pipelined and not stats)
+    def step(stats=False, async_=True):
+        nonlocal k
+        frame.render(W, H, spp, depth, first_sample=k * spp, stats=stats, async_=async_ and not stats)
+        k += 1
 
     for _ in range(args.warmup):
         step()
     frame.sync()
-    # one instrumented frame (outside the timed region): exact visit counts
+    # one instrumented pass (outside the timed region): exact visit counts
     step(stats=True)
     cnt = ctx.stats()
 
@@ -190,45 +276,52 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        if not pipelined:
-            s = ctx.stats()
-            ext_ms_acc.append((s["extend_ms"], s["extend_launches"], s["extend_busy_ms"]))
-    frame.sync()   # every frame and gather of the timed region is complete
+    frame.sync()   # every pass and gather of the timed region is complete
     frame.barrier()
     elapsed = frame.max_over_ranks(time.perf_counter() - t0)
-    last = ctx.stats()   # pipelined: sums over the timed frames (khp_sync report)
-    if pipelined:
-        ext_ms, ext_launches, busy_ms = last["extend_ms"], last["extend_launches"], last["extend_busy_ms"]
-        nfr = max(1, last["frames"])
-    else:
-        ext_ms = sum(a for a, _, _ in ext_ms_acc)
-        ext_launches = sum(b for _, b, _ in ext_ms_acc)
-        busy_ms = sum(c for _, _, c in ext_ms_acc)
-        nfr = 1
+    last = ctx.stats()   # sums over the timed passes (khp_sync report)
+    ext_ms, ext_launches, busy_ms = last["extend_ms"], last["extend_launches"], last["extend_busy_ms"]
+    nfr = max(1, last["frames"])
     samples_per_step = W * H * spp
     value = args.steps * samples_per_step / elapsed / 1e6
+
+    # the same workload with a host wait after every pass (no fusion, no overlap)
+    sync_line = None
+    if args.sync_check_steps > 0:
+        frame.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.sync_check_steps):
+            step(async_=False)
+            frame.sync()
+        frame.barrier()
+        sync_el = frame.max_over_ranks(time.perf_counter() - t1)
+        sync_line = {"value": round(args.sync_check_steps * samples_per_step / sync_el / 1e6, 3),
+                     "ms_per_step": round(sync_el / args.sync_check_steps * 1e3, 3), "steps": args.sync_check_steps,
+                     "def": "one synchronous khp_render per pass (+ gather), no frame fusion"}
+
     # roofline of the extend kernel (this rank's launches)
     rays = cnt["extend_rays"]
     alg_bytes_frame = 44 * rays + 32 * (cnt["node_visits"] + cnt["prim_tests"])
     launches_frame = max(1, cnt["extend_launches"])
     avg_launch_ms = ext_ms / max(1, ext_launches)
-    # timed launches may carry several fused frames (KHP_FUSE_FRAMES): bytes per
-    # timed launch = the frames' algorithmic bytes / the launches they took
-    frames_timed = nfr if pipelined else args.steps
-    bytes_per_launch = alg_bytes_frame * frames_timed / max(1, ext_launches) if ext_launches else \
-        alg_bytes_frame / launches_frame
+    # timed launches carry several fused passes: bytes per timed launch = the
+    # passes' algorithmic bytes / the launches they took
+    bytes_per_launch = alg_bytes_frame * nfr / max(1, ext_launches)
     per_launch = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
-    # Pipelined frames run two frames' launches side by side, so a launch's own
-    # duration also counts time the chip spent on the other frame.  `achieved`
-    # divides the algorithmic bytes of every timed k_extend launch by the time
-    # during which at least one of them was running (union of their HIP-event
-    # intervals, khp_stats.extend_busy_ms); without overlap (--sync-steps) the
-    # union is the sum of the launch durations and this is bytes/launch over
-    # the average launch duration.
     achieved = (bytes_per_launch * ext_launches) / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
-    traffic = pmc_traffic(frames_timed * launches_frame / max(1, ext_launches))
+    frames_per_launch = nfr * launches_frame / max(1, ext_launches)
+    traffic = pmc_traffic(frames_per_launch, args.config)
+    # the any-hit kernel (k_shadow alone; the finish is a separate streaming kernel)
+    sh_rays = cnt["shadow_rays"]
+    sh_bytes_frame = 32 * sh_rays + 32 * (cnt["shadow_node_visits"] + cnt["shadow_prim_tests"])
+    sh_ms = last["shadow_ms"] - last["shadow_finish_ms"]
+    sh_launches = max(1, last["shadow_launches"])
+    sh_bytes_per_launch = sh_bytes_frame * nfr / sh_launches
+    sh_avg_ms = sh_ms / sh_launches
+    sh_achieved = sh_bytes_per_launch / (sh_avg_ms * 1e-3) / 1e9 if sh_avg_ms > 0 else 0.0
+    cfg = CONFIGS[args.config]
     out = {
-        "metric": "Msamples/s at 1080p 8spp, 1M-strand hairball; achieved HBM GB/s vs peak",
+        "metric": METRIC if args.config == "metric" else f"Msamples/s, {cfg['what']}, {W}x{H} {spp}spp",
         "value": round(value, 3),
         "unit": "Msamples/s",
         "n_gpus": world,
@@ -239,13 +332,14 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: seeded hairball (khp_gen_hairball[_device], seed 0x4B49524B), scene built in-process",
+        "data": "synthetic: seeded hairball (khp_gen_hairball[_device], seed 0x4B49524B), scene built in-process; "
+                "step k = progressive pass k (samples k*spp .. (k+1)*spp-1)",
         "config": {
-            "workload": f"config3 scene at the metric row: {args.strands} strands ({n_objects - 2} cone frusta) "
-                        f"on a 2-tri plane + 2x2 quad light, {W}x{H}, {spp} spp, depth {depth}",
-            "width": W, "height": H, "spp": spp, "depth": depth, "strands": args.strands,
+            "workload": f"{cfg['what']} ({n_objects} objects), {W}x{H}, {spp} spp, depth {depth}, progressive passes",
+            "config": args.config, "width": W, "height": H, "spp": spp, "depth": depth, "strands": args.strands,
             "objects": n_objects, "parallelism": f"tile-sharded {args.tile}px tiles x{world}, RCCL gather",
         },
+        "sync_steps": sync_line,
         "roofline": {
             "bound": "hbm",
             "kernel": "k_extend (closest-hit BVH2 traversal)",
@@ -257,25 +351,36 @@ def main():
             "bytes_per_launch": int(bytes_per_launch),
             "avg_launch_ms": round(avg_launch_ms, 4),
             "achieved_per_launch": round(per_launch, 1),
-            "frames_per_launch": round(frames_timed * launches_frame / max(1, ext_launches), 3),
+            "frames_per_launch": round(frames_per_launch, 3),
             "alg_bytes_per_frame": int(alg_bytes_frame),
-            "extend_busy_ms_per_frame": round(busy_ms / max(1, nfr if pipelined else args.steps), 3),
+            "extend_busy_ms_per_frame": round(busy_ms / nfr, 3),
             "achieved_def": "algorithmic bytes of all timed k_extend launches / union of their HIP-event "
                             "intervals (= bytes per launch / avg launch duration when launches do not overlap)",
             "per_ray": {"nodes": round(cnt["node_visits"] / max(1, rays), 2),
                         "prims": round(cnt["prim_tests"] / max(1, rays), 2)},
+            "shadow": {
+                "kernel": "k_shadow (any-hit BVH2 traversal)",
+                "achieved": round(sh_achieved, 1), "frac": round(sh_achieved / HBM_PEAK_GBPS, 4),
+                "bytes_per_launch": int(sh_bytes_per_launch), "avg_launch_ms": round(sh_avg_ms, 4),
+                "alg_bytes_per_frame": int(sh_bytes_frame),
+                "per_ray": {"nodes": round(cnt["shadow_node_visits"] / max(1, sh_rays), 2),
+                            "prims": round(cnt["shadow_prim_tests"] / max(1, sh_rays), 2)},
+                "records_per_s": round((cnt["shadow_node_visits"] + cnt["shadow_prim_tests"]) * nfr /
+                                       max(1e-9, sh_ms * 1e-3), 1),
+            },
         },
         "frame": {
-            "extend_rays": rays, "shadow_rays": cnt["shadow_rays"],
+            "extend_rays": rays, "shadow_rays": sh_rays,
             "extend_ms": round(last["extend_ms"] / nfr, 3), "shade_ms": round(last["shade_ms"] / nfr, 3),
-            "shadow_ms": round(last["shadow_ms"] / nfr, 3), "other_ms": round(last["other_ms"] / nfr, 3),
+            "shadow_ms": round(last["shadow_ms"] / nfr, 3),
+            "shadow_finish_ms": round(last["shadow_finish_ms"] / nfr, 3),
+            "other_ms": round(last["other_ms"] / nfr, 3),
             "device_ms": round(last["render_ms"] / nfr, 3),
-            "shadow_nodes_per_ray": round(cnt["shadow_node_visits"] / max(1, cnt["shadow_rays"]), 2),
-            "stack_spills_per_ray": round(cnt["stack_spills"] / max(1, rays + cnt["shadow_rays"]), 4),
+            "extend_records_per_s": round((cnt["node_visits"] + cnt["prim_tests"]) * nfr / max(1e-9, ext_ms * 1e-3), 1),
+            "stack_spills_per_ray": round(cnt["stack_spills"] / max(1, rays + sh_rays), 4),
             "pruned_pops_per_ray": round(cnt["extend_pruned_pops"] / max(1, rays), 3),
-            "shadow_pruned_pops_per_ray": round(cnt["shadow_pruned_pops"] / max(1, cnt["shadow_rays"]), 3),
-            "subframes": last.get("subframes"),
-            "pipelined": pipelined, "fused_frames": min(args.steps, int(os.environ.get("KHP_FUSE_FRAMES", "32"))) if pipelined else 1,
+            "shadow_pruned_pops_per_ray": round(cnt["shadow_pruned_pops"] / max(1, sh_rays), 3),
+            "fused_frames": min(args.steps, params["fuse_frames"]), "params": params,
             "build_s": round(build_s, 3),
             "setup": setup,
             "per_bounce": [
@@ -285,10 +390,12 @@ def main():
                  "extend_ms": round(last["bounce_extend_ms"][b] / nfr, 3),
                  "shadow_rays": cnt["bounce_shadow_rays"][b],
                  "shadow_nodes_per_ray": round(cnt["bounce_shadow_nodes"][b] / max(1, cnt["bounce_shadow_rays"][b]), 2),
+                 "shadow_prims_per_ray": round(cnt["bounce_shadow_prims"][b] / max(1, cnt["bounce_shadow_rays"][b]), 2),
                  "shadow_ms": round(last["bounce_shadow_ms"][b] / nfr, 3),
                  "wave_iters": cnt["bounce_wave_iters"][b],
                  "lane_use": round(cnt["bounce_lanes_busy"][b] / max(1, 64 * cnt["bounce_wave_iters"][b]), 3),
-                 "shadow_lane_use": round(cnt["bounce_shadow_lanes_busy"][b] / max(1, 64 * cnt["bounce_shadow_wave_iters"][b]), 3)}
+                 "shadow_lane_use": round(cnt["bounce_shadow_lanes_busy"][b] /
+                                          max(1, 64 * cnt["bounce_shadow_wave_iters"][b]), 3)}
                 for b in range(min(depth, 16))],
         },
     }
@@ -309,9 +416,7 @@ def main():
         out["output_stage"] = o
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            # the oracle reads host arrays: the same scene generated on the host
-            host_sd = sd if args.host_scene else scenes.config3(W, H, n_strands=args.strands)
-            out["cpu_baseline"] = cpu_baseline(host_sd, args, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(host_scene_for_oracle(sd, args, scenes), args, args.cpu_seconds)
         except Exception as e:  # reported, never silently replaced
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

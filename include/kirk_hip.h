@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 5
+#define KHP_ABI_VERSION 6
 
 typedef struct khp_ctx khp_ctx;
 
@@ -188,7 +188,7 @@ typedef struct {
     uint64_t step_cycles[4];
     /* ABI 3: where khp_build_accel built the BVH and how long it took */
     uint32_t bvh_on_device;          /* 1: device build (default), 0: host   */
-    uint32_t subframes;              /* last khp_render: concurrent path sets (KHP_SUBFRAMES) */
+    uint32_t subframes;              /* always 1 (ABI 6: one path set per frame slot) */
     double flatten_ms;               /* khp_set_scene (flatten, incl. copies) */
     double bvh_ms;                   /* BVH build wall time incl. transfers   */
     double bvh_kernel_ms;            /* device build: GPU time of its kernels  */
@@ -205,6 +205,11 @@ typedef struct {
      * was running (union of the launches' HIP-event intervals); equals extend_ms
      * when launches do not overlap (synchronous renders) */
     double extend_busy_ms;
+    /* ABI 6: the shadow stage split -- shadow_ms above is k_shadow + the shadow
+     * finish; shadow_finish_ms is the finish alone, shadow_launches counts the
+     * any-hit (k_shadow) launches */
+    double shadow_finish_ms;
+    uint64_t shadow_launches;
 } khp_stats;
 #define KHP_MAX_BOUNCE_STATS 16
 
@@ -212,12 +217,36 @@ typedef struct {
 #define KHP_CTX_HOST_BUILD (1u << 1) /* khp_build_accel builds the BVH on the host
                                        (default: on the device, the same tree)   */
 
+/* ABI 6: scheduling parameters of a context.  They decide how the wavefront
+ * is cut and overlapped on the device, never what it computes: every value
+ * gives the same frames bit for bit.  khp_ctx_params_defaults() fills the
+ * measured defaults; khp_set_params completes in-flight frames
+ * first.  (KIRK has no counterpart: its PathTracer segments by the GUI's
+ * maxBufferSize, CPU_PathTracer.cpp:211-241, which chunk_paths mirrors.) */
+typedef struct {
+    uint32_t fuse_frames;        /* asynchronous frames with equal parameters fused into one batch,
+                                    1..32 (default 32)                                               */
+    uint32_t frames_in_flight;   /* batches in flight at once, 1..3 (default 1)                     */
+    uint64_t chunk_paths;        /* paths per wavefront chunk, >= 4096; 0 (default): the smaller of
+                                    2^27 and what fits in half the free HBM                         */
+    uint32_t heavy_iters;        /* longest-first queues: a path whose last traversal took more
+                                    iterations has its next rays claimed first (default 160)        */
+    int32_t dump_bounce;         /* debug: keep the extension rays of this bounce of the next
+                                    synchronous render for khp_debug_queue (-1: off, default)       */
+    uint32_t trace_kernels;      /* khp_trace_closest / khp_trace_any run on 0: one-ray-per-thread
+                                    kernels (default), 1: the instrumented persistent kernels (KIRK's
+                                    visit counts), 2: the production persistent kernels             */
+} khp_ctx_params;
+
 /* ---- context --------------------------------------------------------------- */
 /* device: HIP device ordinal (one process per GPU). */
 khp_status khp_create(khp_ctx** out, int device, uint32_t flags);
 void khp_destroy(khp_ctx* ctx);
 const char* khp_last_error(void);
 int khp_abi_version(void);
+void khp_ctx_params_defaults(khp_ctx_params* out);
+khp_status khp_set_params(khp_ctx* ctx, const khp_ctx_params* params);
+khp_status khp_get_params(khp_ctx* ctx, khp_ctx_params* out);
 
 /* Replaces CPU::Scene::setSceneGraph (CPU_Scene.cpp:25-43) + the Triangle and
  * Cylinder constructors (Triangle.cpp:3-129, Cylinder.cpp:5-67). Copies. */
@@ -338,8 +367,8 @@ khp_status khp_host_build(const khp_scene* scene, uint32_t* n_nodes, uint32_t* d
                           int32_t* node_first, int32_t* node_count, int32_t* object_ids, float* obj_bounds,
                           float* records);
 
-/* Debug introspection: when the last khp_render ran with the environment
- * variable KHP_DUMP_BOUNCE=b, the extension rays of bounce b (queue order) are
+/* Debug introspection: when the last synchronous khp_render ran with
+ * khp_ctx_params.dump_bounce = b, the extension rays of bounce b (queue order) are
  * kept on the host.  Call with null arrays to get *n, then with [n][3] arrays. */
 khp_status khp_debug_queue(khp_ctx* ctx, uint32_t* n, float* orig, float* dir);
 

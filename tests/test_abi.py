@@ -6,6 +6,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -121,10 +122,21 @@ def test_product_does_not_link_the_oracle():
     assert "import oracle" not in src and "oracle_ffi" not in src
 
 
-def test_package_exports_and_queue_default():
-    import ba_pathtracing_fur_amd as P
-    for name in P.__all__:
-        assert getattr(P, name) is not None
-    # two frames in flight need more than HIP's default 4 hardware queues (see __init__)
-    if os.environ.get("KHP_KEEP_HW_QUEUES") != "1":
-        assert int(os.environ["GPU_MAX_HW_QUEUES"]) >= 8
+def test_package_exports_and_leaves_hw_queues_alone():
+    """Importing the package changes no process setting: GPU_MAX_HW_QUEUES is set
+    only by an explicit set_hw_queues() call of the host program."""
+    code = ("import os, sys; sys.path.insert(0, %r); os.environ.pop('GPU_MAX_HW_QUEUES', None); "
+            "import ba_pathtracing_fur_amd as P; [getattr(P, n) for n in P.__all__]; "
+            "assert 'GPU_MAX_HW_QUEUES' not in os.environ; P.set_hw_queues(8); "
+            "assert os.environ['GPU_MAX_HW_QUEUES'] == '8'") % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.check_call([sys.executable, "-c", code])
+
+
+def test_ctx_params_struct_matches_header():
+    """khp_ctx_params defaults (no device needed) and the ctypes layout."""
+    lib = N.load_library()
+    prm = N.CtxParams()
+    lib.khp_ctx_params_defaults(prm)
+    assert prm.as_dict() == {"fuse_frames": 32, "frames_in_flight": 1, "chunk_paths": 0, "heavy_iters": 160,
+                             "dump_bounce": -1, "trace_kernels": 0}
+    assert ctypes.sizeof(N.CtxParams) == 32

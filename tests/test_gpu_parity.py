@@ -93,63 +93,64 @@ def test_tile_shards_match_oracle(hip_ctx, nranks):
 
 
 def test_path_chunking(hip_ctx):
-    """KHP_MAX_PATHS forces pixel and sample chunking of the wavefront; frames must not change."""
+    """khp_ctx_params.chunk_paths forces pixel and sample chunking of the wavefront; frames must not change."""
     sd = S.config2(128, 96, n_strands=1500)
     hip_ctx.set_scene(sd)
     hip_ctx.build_accel()
     ref = hip_ctx.render(128, 96, 3, 5)
-    os.environ["KHP_MAX_PATHS"] = "4096"
+    old = hip_ctx.set_params(chunk_paths=4096)
     try:
         got = hip_ctx.render(128, 96, 3, 5)
     finally:
-        del os.environ["KHP_MAX_PATHS"]
+        hip_ctx.set_params(**old)
     assert np.array_equal(ref.view(np.uint32), got.view(np.uint32))
     assert_parity(got, oracle_ffi.Oracle(sd).render(128, 96, 3, 5, threads=16), exact=True)
 
 
-SET_MODES = [dict(KHP_SUBFRAMES="1"), dict(KHP_SUBFRAMES="3"), dict(KHP_SUBFRAMES="4", KHP_STAGGER="1"),
-             dict(KHP_SUBFRAMES="3", KHP_SPLIT="p"), dict(KHP_SUBFRAMES="4", KHP_STAGGER="1", KHP_SET_STREAMS="1")]
-
-
-@pytest.mark.parametrize("env", SET_MODES, ids=["-".join(f"{k[4:]}{v}" for k, v in m.items()) for m in SET_MODES])
-def test_path_sets_do_not_change_the_frame(hip_ctx, env):
-    """Path sets (KHP_SUBFRAMES: sample passes or pixel ranges on their own
-    streams, optionally staggered; also combined with path chunking) leave the
-    frame equal to the oracle's, bit for bit."""
+@pytest.mark.parametrize("chunk", [0, 5000])
+def test_chunked_and_instrumented_frames(hip_ctx, chunk):
+    """Chunked wavefronts (chunk_paths 5000: pixel and sample chunks) and the
+    instrumented kernels (one stream, per-bounce snapshots) leave the frame
+    equal to the oracle's, bit for bit."""
     sd = S.config2(120, 72, n_strands=1500)
     hip_ctx.set_scene(sd)
     hip_ctx.build_accel()
     spp = 5
     want = oracle_ffi.Oracle(sd).render(120, 72, spp, 5, threads=16)
-    os.environ.update(env)
+    old = hip_ctx.set_params(chunk_paths=chunk)
     try:
         got = hip_ctx.render(120, 72, spp, 5)
-        assert hip_ctx.stats()["subframes"] == int(env["KHP_SUBFRAMES"])
+        assert hip_ctx.stats()["subframes"] == 1
         assert_parity(got, want, exact=True)
-        os.environ["KHP_MAX_PATHS"] = "5000"
-        got = hip_ctx.render(120, 72, spp, 5)
-        assert_parity(got, want, exact=True)
-        got = hip_ctx.render(120, 72, spp, 5, stats=True)   # instrumented: one stream, per-set snapshots
+        got = hip_ctx.render(120, 72, spp, 5, stats=True)
         st = hip_ctx.stats()
         assert sum(st["bounce_rays"]) == st["extend_rays"] > 0
         assert_parity(got, want, exact=True)
     finally:
-        for k in list(env) + ["KHP_MAX_PATHS"]:
-            os.environ.pop(k, None)
+        hip_ctx.set_params(**old)
+
+
+def test_params_are_validated(hip_ctx):
+    for bad in (dict(fuse_frames=0), dict(fuse_frames=33), dict(frames_in_flight=4), dict(chunk_paths=100),
+                dict(trace_kernels=3)):
+        with pytest.raises(N.KhpError) as e:
+            hip_ctx.set_params(**bad)
+        assert e.value.status == N.KHP_EINVAL
+    assert hip_ctx.params()["fuse_frames"] == 32
 
 
 @pytest.mark.parametrize("fif", ["1", "2", "3"])
 def test_async_frames_in_flight(hip_ctx, fif):
     """KHP_RENDER_ASYNC: progressive passes enqueued back to back (up to
-    KHP_FRAMES_IN_FLIGHT overlapping on the device) accumulate in call order;
+    frames_in_flight overlapping on the device) accumulate in call order;
     after khp_sync the framebuffer is the oracle's 5-spp frame, and the report
     covers every pass."""
     sd = S.config2(96, 64, n_strands=1500)
     hip_ctx.set_scene(sd)
     hip_ctx.build_accel()
     want = oracle_ffi.Oracle(sd).render(96, 64, 5, 5, threads=16)
-    os.environ["KHP_FRAMES_IN_FLIGHT"] = fif
-    os.environ["KHP_FUSE_FRAMES"] = "1"   # frames in flight without fusion (test_fused_frames covers fusion)
+    # frames in flight without fusion (test_fused_frames covers fusion)
+    old = hip_ctx.set_params(frames_in_flight=int(fif), fuse_frames=1)
     try:
         for first, n in ((0, 1), (1, 2), (3, 1), (4, 1)):
             hip_ctx.render(96, 64, n, 5, first_sample=first, async_=True)
@@ -164,8 +165,7 @@ def test_async_frames_in_flight(hip_ctx, fif):
         with pytest.raises(N.KhpError):
             hip_ctx.render(96, 64, 1, 5, async_=True, stats=True)
     finally:
-        os.environ.pop("KHP_FRAMES_IN_FLIGHT", None)
-        os.environ.pop("KHP_FUSE_FRAMES", None)
+        hip_ctx.set_params(**old)
 
 
 def test_deterministic_across_runs(hip_ctx):
@@ -255,16 +255,16 @@ def test_single_rank_communicator():
 
 @pytest.mark.parametrize("fuse", ["2", "4", "3"])
 def test_fused_frames(fuse):
-    """KHP_FUSE_FRAMES: asynchronous passes with equal parameters run as one
+    """fuse_frames: asynchronous passes with equal parameters run as one
     batch (one launch per bounce for all of them) and accumulate in call order
     -- the framebuffer is the oracle's 8-spp frame; with a (1-rank) gather
     after every pass, as bench.py does at N > 1, the gathers keep their place."""
     from ba_pathtracing_fur_amd.pathtracer import comm_unique_id
     sd = S.config2(72, 48, n_strands=1500)
     want = oracle_ffi.Oracle(sd).render(72, 48, 8, 5, threads=16)
-    os.environ["KHP_FUSE_FRAMES"] = fuse
     ctx = HipContext(0)
     try:
+        ctx.set_params(fuse_frames=int(fuse))
         ctx.set_scene(sd)
         ctx.build_accel()
         for first in range(0, 8, 2):
@@ -285,7 +285,6 @@ def test_fused_frames(fuse):
         ctx.sync()
         assert_parity(ctx.read_framebuffer(72, 48), want, exact=True)
     finally:
-        os.environ.pop("KHP_FUSE_FRAMES", None)
         ctx.close()
 
 
@@ -301,15 +300,11 @@ def test_fused_full_size_matches_passes():
         for k in range(16):
             ctx.render(1920, 1080, 4, 5, first_sample=4 * k, readback=False)
         want = ctx.read_framebuffer(1920, 1080)
-        for cap in (None, str(1 << 26)):
-            if cap:
-                os.environ["KHP_MAX_PATHS"] = cap
-            try:
-                for k in range(16):
-                    ctx.render(1920, 1080, 4, 5, first_sample=4 * k, async_=True)
-                ctx.sync()
-            finally:
-                os.environ.pop("KHP_MAX_PATHS", None)
+        for cap in (0, 1 << 26):
+            ctx.set_params(chunk_paths=cap)
+            for k in range(16):
+                ctx.render(1920, 1080, 4, 5, first_sample=4 * k, async_=True)
+            ctx.sync()
             assert ctx.stats()["frames"] == 16
             assert np.array_equal(ctx.read_framebuffer(1920, 1080).view(np.uint32), want.view(np.uint32)), cap
         host = S.config3(1920, 1080, n_strands=1_000_000)
@@ -327,9 +322,9 @@ def test_fused_frames_with_gathers_split(max_paths):
     from ba_pathtracing_fur_amd.pathtracer import comm_unique_id
     sd = S.config2(72, 48, n_strands=1500)
     want = oracle_ffi.Oracle(sd).render(72, 48, 8, 5, threads=16)
-    os.environ.update(KHP_FUSE_FRAMES="4", KHP_MAX_PATHS=max_paths)
     ctx = HipContext(0)
     try:
+        ctx.set_params(fuse_frames=4, chunk_paths=int(max_paths))
         ctx.set_scene(sd)
         ctx.build_accel()
         ctx.comm_init(1, 0, comm_unique_id())
@@ -340,8 +335,6 @@ def test_fused_frames_with_gathers_split(max_paths):
         assert ctx.stats()["frames"] == 4
         assert_parity(ctx.read_framebuffer(72, 48), want, exact=True)
     finally:
-        for k in ("KHP_FUSE_FRAMES", "KHP_MAX_PATHS"):
-            os.environ.pop(k, None)
         ctx.close()
 
 
@@ -399,7 +392,7 @@ def test_cpp_host_program_matches(hip_ctx, tmp_path):
 @pytest.mark.parametrize("name,kw", [("config2", dict(n_strands=3000)), ("config5", dict(n_strands=2000,
                                                                                           torus_grid=30))])
 def test_production_traversal_kernels_ray_by_ray(hip_ctx, mode, name, kw):
-    """KHP_TRACE_PERSISTENT routes the batch queries through the renderer's own
+    """khp_ctx_params.trace_kernels routes the batch queries through the renderer's own
     persistent kernels: 1 = instrumented (KIRK's node/candidate visit counts must
     match the oracle's), 2 = the production build used in timed frames."""
     sd = S.build_config(name, width=32, height=32, **kw)
@@ -414,13 +407,13 @@ def test_production_traversal_kernels_ray_by_ray(hip_ctx, mode, name, kw):
     tmax = rng.uniform(0.01, 2.0, n).astype(np.float32)
     t0, obj0, uv0, nodes, prims = o.trace_closest(orig, d)
     any0 = o.trace_any(orig, d, tmax)
-    os.environ["KHP_TRACE_PERSISTENT"] = mode
+    old = hip_ctx.set_params(trace_kernels=int(mode))
     try:
         t, obj, uv = hip_ctx.trace_closest(orig, d)
         st = hip_ctx.stats()
         a = hip_ctx.trace_any(orig, d, tmax)
     finally:
-        del os.environ["KHP_TRACE_PERSISTENT"]
+        hip_ctx.set_params(**old)
     assert np.array_equal(obj, obj0)
     assert np.array_equal(t.view(np.uint32), t0.view(np.uint32))
     assert np.array_equal(uv.view(np.uint32), uv0.view(np.uint32))
