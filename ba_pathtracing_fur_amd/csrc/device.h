@@ -31,7 +31,109 @@ struct DevScene {
     float root_box[6];
     khp_environment env;
     khp_camera cam;
+    // ABI 6 textures (null / 0 when the scene has none)
+    const float* __restrict__ tri_uv;    // object-id order, 6 floats per triangle (reordered tca tcb tcc)
+    const float* __restrict__ cone_h;    // cone order (object id - n_tris): Cylinder::m_height
+    const DevTexture* __restrict__ tex;
+    const uint8_t* __restrict__ texels;
+    const DevMatTex* __restrict__ mtex;  // per material
+    uint32_t n_tris;
+    int32_t textured;
+    khp_env_map env_map;
 };
+
+// ---- textures (ABI 6) -------------------------------------------------------------------
+// Texture::getColor (Texture.cpp:243-287): NaN -> red; a coordinate outside
+// [0, 1] becomes pow(frac, wrap_mode) -- glm::pow resolves to std::pow(double,
+// double) for the uchar mode, so TILE (1) gives the fraction and CLAMP (0)
+// gives 1; then the nearest texel (int)(u * (w - 1)), channel expansion
+// rrrr / rrrg / rgb1 / rgba and /255.  Texel indices are clamped into the
+// image, where KIRK would read out of bounds (infinite coordinates).
+__device__ __forceinline__ float tex_wrap(float x, uint32_t mode) {
+    if (x > 1.0f || x < 0.0f) {
+        const float f = x - floorf(x);
+        if (mode == 1u) return f;
+        if (mode == 0u) return 1.0f;
+        return (float)pow((double)f, (double)mode);
+    }
+    return x;
+}
+__device__ __forceinline__ float4 tex_color(const DevScene& S, int32_t ti, float x, float y) {
+    if (x != x || y != y) return make_float4(1.0f, 0.0f, 0.0f, 1.0f);  // Color::RED
+    const DevTexture t = S.tex[ti];
+    const float ux = tex_wrap(x, t.wrap), uy = tex_wrap(y, t.wrap);
+    int sx = (int)(ux * (float)((int)t.w - 1)), sy = (int)(uy * (float)((int)t.h - 1));
+    sx = sx < 0 ? 0 : (sx >= (int)t.w ? (int)t.w - 1 : sx);
+    sy = sy < 0 ? 0 : (sy >= (int)t.h ? (int)t.h - 1 : sy);
+    const uint8_t* p = S.texels + t.off + (size_t)t.ch * ((size_t)sy * t.w + (size_t)sx);
+    const float r = p[0] / 255.0f;
+    switch (t.ch) {
+        case 4: return make_float4(r, p[1] / 255.0f, p[2] / 255.0f, p[3] / 255.0f);
+        case 3: return make_float4(r, p[1] / 255.0f, p[2] / 255.0f, 1.0f);
+        case 2: return make_float4(r, r, r, p[1] / 255.0f);
+        default: return make_float4(r, r, r, r);
+    }
+}
+
+// Material::getFromParam (Material.cpp:15-23) for every parameter the path
+// tracer fetches: textured colours take the texel's rgb, textured roughness
+// the length of its rgba (glm::length(vec4): sqrt((x*x + y*y) + (z*z + w*w))).
+__device__ __forceinline__ void resolve_material(const DevScene& S, uint32_t mat, float tu, float tv,
+                                                 khp_material& m) {
+    m = S.mats[mat];
+    const DevMatTex mt = S.mtex[mat];
+    float* cols[4] = {m.diffuse, m.specular, m.volume, m.emission};
+    for (int k = 0; k < 4; ++k) {
+        if (mt.t[k] >= 0) {
+            const float4 c = tex_color(S, mt.t[k], tu, tv);
+            cols[k][0] = c.x;
+            cols[k][1] = c.y;
+            cols[k][2] = c.z;
+        }
+    }
+    if (mt.t[MT_ROUGHNESS] >= 0) {
+        const float4 c = tex_color(S, mt.t[MT_ROUGHNESS], tu, tv);
+        m.roughness = sqrtf((c.x * c.x + c.y * c.y) + (c.z * c.z + c.w * c.w));
+    }
+}
+
+// Environment::getColor (Environment.cpp:91-133).  Cube map: the face of the
+// dominant axis (side = 1.5 -/+ 1.5 sign, the z faces with the opposite sign
+// convention of KIRK's code), uv from the ratios as written there; sphere map:
+// m = 2 sqrt(x^2 + y^2 + (z + 1)^2) with the z term in double, uv = d/m + 0.5.
+__device__ __forceinline__ v3 env_color(const DevScene& S, v3 dir_in) {
+    if (S.env_map.type == KHP_ENV_COLOR) return mk(S.env.color[0], S.env.color[1], S.env.color[2]);
+    const v3 d = normalize(dir_in);
+    float4 c;
+    if (S.env_map.type == KHP_ENV_CUBE_MAP) {
+        const float sx = (float)((0.0f < d.x) - (d.x < 0.0f)), sy = (float)((0.0f < d.y) - (d.y < 0.0f));
+        const float sz = (float)((0.0f < d.z) - (d.z < 0.0f));
+        const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+        const float mx = gmax(gmax(ax, ay), az);
+        int side;
+        float u, v;
+        if (mx == ax) {
+            side = (int)(0.0f + 1.5f - 1.5f * sx);
+            u = (d.z / d.x + 1.0f) / 2.0f;
+            v = (d.y / ax + 1.0f) / 2.0f;
+        } else if (mx == ay) {
+            side = (int)(1.0f + 1.5f - 1.5f * sy);
+            u = (d.x / ay + 1.0f) / 2.0f;
+            v = (d.z / d.y + 1.0f) / 2.0f;
+        } else {
+            side = (int)(2.0f + 1.5f + 1.5f * sz);
+            u = -(d.x / d.z + 1.0f) / 2.0f;
+            v = (d.y / az + 1.0f) / 2.0f;
+        }
+        c = tex_color(S, S.env_map.tex[side], u, v);
+    } else {
+        const double zz = (double)d.z + 1.0;
+        const float m = (float)(2.0 * sqrt((double)(d.x * d.x + d.y * d.y) + zz * zz));
+        const float u = (float)((double)(d.x / m) + 0.5), v = (float)((double)(d.y / m) + 0.5);
+        c = tex_color(S, S.env_map.tex[0], u, v);
+    }
+    return mk(c.x, c.y, c.z);
+}
 
 struct Ray {
     v3 o, d;

@@ -47,6 +47,8 @@ struct DeviceObjects {
     DevMem centroid;  // float[3 * n_obj]
     DevMem tri_nrm;   // float[9 * n_tris]
     DevMem tri_frame; // float[9 * n_tris] hair frame (zeros unless fiberToTriangles)
+    DevMem tri_uv;    // float[6 * n_tris] texcoords after the ctor's reordering (textured scenes)
+    DevMem cone_h;    // float[n_cones] Cylinder::m_height (textured scenes)
     uint32_t n_obj = 0, n_tris = 0, n_cones = 0;
     void release() {
         rec.release();
@@ -55,6 +57,8 @@ struct DeviceObjects {
         centroid.release();
         tri_nrm.release();
         tri_frame.release();
+        tri_uv.release();
+        cone_h.release();
         n_obj = n_tris = n_cones = 0;
     }
 };
@@ -82,7 +86,9 @@ struct DeviceLayout {
 // CPU::Scene::flattenNode per-object state on the device (flatten.hip).
 // device_ptrs: the scene's geometry arrays are device pointers (else host,
 // copied).  Errors starting "EINVAL:" are input errors.
-std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_materials, DeviceObjects& o,
+// textured: also write tri_uv / cone_h; models: HostScene::models (25 floats per model) or empty.
+std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_materials, bool textured,
+                           const std::vector<float>& models, DeviceObjects& o,
                            hipStream_t st, double* kernel_ms);
 
 // khp_gen_hairball + khp_fibers_to_cones on the device, into device arrays of

@@ -15,15 +15,17 @@ namespace khp {
 namespace fl {
 
 __global__ void k_flatten_tris(const float* __restrict__ tv, const float* __restrict__ tn,
-                               const uint32_t* __restrict__ tm, uint32_t n_tris, uint32_t n_mat, float4* rec,
-                               Aux* aux, float* bounds, float* cen, float* nrm, uint32_t* err) {
+                               const uint32_t* __restrict__ tm, const float* __restrict__ uv_in, uint32_t n_tris,
+                               uint32_t n_mat, float4* rec, Aux* aux, float* bounds, float* cen, float* nrm,
+                               float* uv_out, uint32_t* err) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_tris) return;
     const float* v = tv + 9 * (size_t)i;
     const float* n = tn + 9 * (size_t)i;
     float r[16];
     tri_object(ld3(v), ld3(v + 3), ld3(v + 6), ld3(n), ld3(n + 3), ld3(n + 6), r, bounds + 6 * (size_t)i,
-               cen + 3 * (size_t)i, nrm + 9 * (size_t)i);
+               cen + 3 * (size_t)i, nrm + 9 * (size_t)i, uv_in ? uv_in + 6 * (size_t)i : nullptr,
+               uv_out ? uv_out + 6 * (size_t)i : nullptr);
     float4* o = rec + 4 * (size_t)i;
     o[0] = make_float4(r[0], r[1], r[2], r[3]);
     o[1] = make_float4(r[4], r[5], r[6], r[7]);
@@ -34,16 +36,31 @@ __global__ void k_flatten_tris(const float* __restrict__ tv, const float* __rest
     aux[i] = Aux{0.0f, m, i, 0u};
 }
 
+// models: n_models x (M, inverse transpose) = 25 floats each, or null (world-space cones)
 __global__ void k_flatten_cones(const float4* __restrict__ b, const float4* __restrict__ a,
-                                const uint32_t* __restrict__ cm, uint32_t n_cones, uint32_t id0, uint32_t n_mat,
-                                float4* rec, Aux* aux, float* bounds, float* cen, uint32_t* err) {
+                                const uint32_t* __restrict__ cm, const uint32_t* __restrict__ cmod,
+                                const float* __restrict__ models, uint32_t n_models, uint32_t n_cones, uint32_t id0,
+                                uint32_t n_mat, float4* rec, Aux* aux, float* bounds, float* cen, float* cone_h,
+                                uint32_t* err) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_cones) return;
     const uint32_t id = id0 + i;
     const float4 bb = b[i], aa = a[i];
+    const v3 base = mk(bb.x, bb.y, bb.z), apex = mk(aa.x, aa.y, aa.z);
     float r[16];
-    const float base_d =
-        cone_object(mk(bb.x, bb.y, bb.z), mk(aa.x, aa.y, aa.z), bb.w, aa.w, r, bounds + 6 * (size_t)id, cen + 3 * (size_t)id);
+    float base_d;
+    if (models) {
+        uint32_t k = cmod ? cmod[i] : 0u;
+        if (k >= n_models) {
+            atomicOr(err, 4u);
+            k = 0;
+        }
+        const float* M = models + 25 * (size_t)k;
+        base_d = cone_object_xf(base, apex, bb.w, aa.w, M, M + 16, r, bounds + 6 * (size_t)id, cen + 3 * (size_t)id);
+    } else {
+        base_d = cone_object(base, apex, bb.w, aa.w, r, bounds + 6 * (size_t)id, cen + 3 * (size_t)id);
+    }
+    if (cone_h) cone_h[i] = length(apex - base);  // Cylinder::m_height (pre-transform)
     float4* o = rec + 4 * (size_t)id;
     o[0] = make_float4(r[0], r[1], r[2], r[3]);
     o[1] = make_float4(r[4], r[5], r[6], r[7]);
@@ -99,8 +116,8 @@ static uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b - 1) /
 
 }  // namespace fl
 
-std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_materials, DeviceObjects& o,
-                           hipStream_t st, double* kernel_ms) {
+std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_materials, bool textured,
+                           const std::vector<float>& models, DeviceObjects& o, hipStream_t st, double* kernel_ms) {
     using namespace fl;
     const uint32_t nt = s->n_tris, nc = s->n_cones, N = nt + nc;
     o.n_obj = N;
@@ -117,9 +134,21 @@ std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_mate
                              device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
     else
         FLCHK(hipMemsetAsync(o.tri_frame.p, 0, 36 * (size_t)std::max(nt, 1u), st));
-    DevMem tv, tn, tm, cb, ca, cm, err;
+    if (textured) {
+        FLCHK(o.tri_uv.ensure(24 * (size_t)std::max(nt, 1u)));
+        FLCHK(o.cone_h.ensure(4 * (size_t)std::max(nc, 1u)));
+    } else {
+        o.tri_uv.release();
+        o.cone_h.release();
+    }
+    DevMem tv, tn, tm, tuv, cb, ca, cm, cmod, dmodels, err;
     const float *dtv = s->tri_v, *dtn = s->tri_n, *dcb = s->cone_base_r0, *dca = s->cone_apex_r1;
-    const uint32_t *dtm = s->tri_mat, *dcm = s->cone_mat;
+    const float* duv = textured ? s->tri_uv : nullptr;
+    const uint32_t *dtm = s->tri_mat, *dcm = s->cone_mat, *dcmod = s->cone_model;
+    if (!models.empty()) {
+        FLCHK(dmodels.ensure(4 * models.size()));
+        FLCHK(hipMemcpyAsync(dmodels.p, models.data(), 4 * models.size(), hipMemcpyHostToDevice, st));
+    }
     if (!device_ptrs) {  // the library copies the caller's host arrays (khp_set_scene contract)
         if (nt) {
             FLCHK(tv.ensure(36 * (size_t)nt));
@@ -131,6 +160,11 @@ std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_mate
             dtv = tv.as<float>();
             dtn = tn.as<float>();
             dtm = tm.as<uint32_t>();
+            if (duv) {
+                FLCHK(tuv.ensure(24 * (size_t)nt));
+                FLCHK(hipMemcpyAsync(tuv.p, s->tri_uv, 24 * (size_t)nt, hipMemcpyHostToDevice, st));
+                duv = tuv.as<float>();
+            }
         }
         if (nc) {
             FLCHK(cb.ensure(16 * (size_t)nc));
@@ -142,6 +176,11 @@ std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_mate
             dcb = cb.as<float>();
             dca = ca.as<float>();
             dcm = cm.as<uint32_t>();
+            if (s->cone_model) {
+                FLCHK(cmod.ensure(4 * (size_t)nc));
+                FLCHK(hipMemcpyAsync(cmod.p, s->cone_model, 4 * (size_t)nc, hipMemcpyHostToDevice, st));
+                dcmod = cmod.as<uint32_t>();
+            }
         }
     }
     FLCHK(err.ensure(4));
@@ -151,13 +190,16 @@ std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_mate
     FLCHK(hipEventCreate(&e1));
     FLCHK(hipEventRecord(e0, st));
     if (nt)
-        hipLaunchKernelGGL(k_flatten_tris, dim3(blocks(nt, 256)), dim3(256), 0, st, dtv, dtn, dtm, nt, n_materials,
-                           o.rec.as<float4>(), o.aux.as<Aux>(), o.bounds.as<float>(), o.centroid.as<float>(),
-                           o.tri_nrm.as<float>(), err.as<uint32_t>());
+        hipLaunchKernelGGL(k_flatten_tris, dim3(blocks(nt, 256)), dim3(256), 0, st, dtv, dtn, dtm, duv, nt,
+                           n_materials, o.rec.as<float4>(), o.aux.as<Aux>(), o.bounds.as<float>(),
+                           o.centroid.as<float>(), o.tri_nrm.as<float>(), textured ? o.tri_uv.as<float>() : nullptr,
+                           err.as<uint32_t>());
     if (nc)
         hipLaunchKernelGGL(k_flatten_cones, dim3(blocks(nc, 256)), dim3(256), 0, st, (const float4*)dcb,
-                           (const float4*)dca, dcm, nc, nt, n_materials, o.rec.as<float4>(), o.aux.as<Aux>(),
-                           o.bounds.as<float>(), o.centroid.as<float>(), err.as<uint32_t>());
+                           (const float4*)dca, dcm, models.empty() ? nullptr : dcmod,
+                           models.empty() ? nullptr : dmodels.as<float>(), (uint32_t)(models.size() / 25), nc, nt,
+                           n_materials, o.rec.as<float4>(), o.aux.as<Aux>(), o.bounds.as<float>(),
+                           o.centroid.as<float>(), textured ? o.cone_h.as<float>() : nullptr, err.as<uint32_t>());
     FLCHK(hipGetLastError());
     FLCHK(hipEventRecord(e1, st));
     uint32_t herr = 0;
@@ -170,6 +212,7 @@ std::string device_flatten(const khp_scene* s, bool device_ptrs, uint32_t n_mate
     if (kernel_ms) *kernel_ms = ms;
     if (herr & 1u) return "EINVAL:triangle material index out of range";
     if (herr & 2u) return "EINVAL:cone material index out of range";
+    if (herr & 4u) return "EINVAL:cone model index out of range";
     return std::string();
 }
 

@@ -471,7 +471,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                 light_hit = true;
             }
             if (lambda == FLT_MAX_) {  // EnvironmentShader::shade
-                C = C + mk(S.env.color[0], S.env.color[1], S.env.color[2]) * T;
+                C = C + env_color(S, r.d) * T;
                 T = mk(0, 0, 0);
             } else if (light_hit) {    // LightShader::shade
                 C = C + light_emit(S.lights[t_index], r.d) * T;
@@ -504,8 +504,30 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                     s.W = ld3(tf + 6);
                 }
                 s.n = nrm;
-                const khp_material* m = s.m;
                 v3 loc = follow(r, lambda);
+                khp_material mres;
+                if (S.textured) {  // calcTcoord (traceRay, CPU_PathTracer.cpp:178-179), then the textured parameters
+                    float tu, tv;
+                    if (ax.flags & 1u) {  // Cylinder::calcTcoord (Cylinder.cpp:239-260)
+                        const float4 c0 = pr[0];
+                        const v3 Q = loc - mk(c0.x, c0.y, c0.z);
+                        const float qu = dot(Q, s.U), qv = dot(Q, s.V), qw = dot(Q, s.W);
+                        const float rr = c0.w - pr[1].w * qv;
+                        const float tmp = gclamp(qw / rr, -1.0f, 1.0f);
+                        const float phi = qu < 0.0f ? 2.0f * PIF - k_acosf(tmp) : k_acosf(tmp);
+                        tu = phi / 2.0f / PIF;
+                        tv = qv / S.cone_h[ax.obj - S.n_tris];
+                    } else {              // Triangle::calcTcoord (Triangle.cpp:250-254)
+                        const float* tc = S.tri_uv + 6 * (size_t)ax.obj;
+                        const float bu = Wv.hu[i], bv = Wv.hv[i];
+                        const float bx = (1.0f - bu) - bv;
+                        tu = (bx * tc[0] + bu * tc[2]) + bv * tc[4];
+                        tv = (bx * tc[1] + bu * tc[3]) + bv * tc[5];
+                    }
+                    resolve_material(S, ax.mat, tu, tv, mres);
+                    s.m = &mres;
+                }
+                const khp_material* m = s.m;
                 float h0 = draw_u01(key, dim_of(bounce, P_HAIR_ALPHA)), h1 = draw_u01(key, dim_of(bounce, P_HAIR_BETA));
                 v3 counter = -normalize(r.d);
                 // NEE setup: SimpleShader::calcDirectLight (SimpleShader.h:101-152) and
@@ -1012,6 +1034,7 @@ struct khp_ctx {
     HostScene hs;
     bool scene_set = false, built = false;
     DevMem prims, aux, trinrm, trifrm, nodes, mats, lights;
+    DevMem triuv, coneh, texd, texels, mtex;   // ABI 6 textures
     DevScene S{};
     khp_ctx_params prm{};
     size_t auto_chunk = 0;         // chunk_paths() when prm.chunk_paths == 0
@@ -1173,7 +1196,8 @@ static khp_status set_scene_impl(khp_ctx* c, const khp_scene* s, bool device_ptr
         c->obj.release();
     } else {
         HIPCHK(hipSetDevice(c->device));
-        err = device_flatten(s, device_ptrs, s->n_materials, c->obj, c->stream, &c->st.flatten_kernel_ms);
+        err = device_flatten(s, device_ptrs, s->n_materials, c->hs.textured, c->hs.models, c->obj, c->stream,
+                             &c->st.flatten_kernel_ms);
         if (!err.empty()) {
             if (err.rfind("EINVAL:", 0) == 0) return fail(KHP_EINVAL, err.substr(7));
             return fail(KHP_EDEVICE, err);
@@ -1330,6 +1354,15 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     }
     HIPCHK(upload(c->mats, hs.mats.data(), hs.mats.size(), c->stream));
     HIPCHK(upload(c->lights, hs.lights.data(), hs.lights.size(), c->stream));
+    if (hs.textured) {
+        if (host_build) {
+            HIPCHK(upload(c->triuv, hs.tri_uv.data(), hs.tri_uv.size(), c->stream));
+            HIPCHK(upload(c->coneh, hs.cone_h.data(), hs.cone_h.size(), c->stream));
+        }
+        HIPCHK(upload(c->texd, hs.tex.data(), hs.tex.size(), c->stream));
+        HIPCHK(upload(c->texels, hs.texels.data(), hs.texels.size(), c->stream));
+        HIPCHK(upload(c->mtex, hs.mtex.data(), hs.mtex.size(), c->stream));
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     c->st.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     DevScene& S = c->S;
@@ -1348,6 +1381,14 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     c->n_slots = n_slots;
     S.env = hs.env;
     S.cam = hs.cam;
+    S.textured = hs.textured ? 1 : 0;
+    S.n_tris = hs.n_tris;
+    S.env_map = hs.env_map;
+    S.tri_uv = !hs.textured ? nullptr : host_build ? c->triuv.as<float>() : c->obj.tri_uv.as<float>();
+    S.cone_h = !hs.textured ? nullptr : host_build ? c->coneh.as<float>() : c->obj.cone_h.as<float>();
+    S.tex = hs.textured ? c->texd.as<DevTexture>() : nullptr;
+    S.texels = hs.textured ? c->texels.as<uint8_t>() : nullptr;
+    S.mtex = hs.textured ? c->mtex.as<DevMatTex>() : nullptr;
     c->st.n_objects = hs.n_obj;
     c->st.n_leaves = (c->st.n_nodes + 1) / 2;
     c->st.bvh_depth = hs.depth;

@@ -58,17 +58,83 @@ void light_init(DevLight& L, const khp_light& in) {
 }
 
 // Triangle::Triangle / Cylinder::Cylinder (objects.h, shared with the device flatten).
-static void tri_ctor(HostScene& hs, uint32_t id, v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc, uint32_t mat) {
+static void tri_ctor(HostScene& hs, uint32_t id, v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc, uint32_t mat,
+                     const float* uv) {
     tri_object(a, b, c, na, nb, nc, &hs.rec[16 * (size_t)id], &hs.bounds[6 * (size_t)id],
-               &hs.centroid[3 * (size_t)id], &hs.tri_nrm[9 * (size_t)id]);
+               &hs.centroid[3 * (size_t)id], &hs.tri_nrm[9 * (size_t)id], uv,
+               hs.tri_uv.empty() ? nullptr : &hs.tri_uv[6 * (size_t)id]);
     hs.aux[id] = Aux{0.0f, mat, id, 0u};  // flags: triangle
 }
 
-static void cone_ctor(HostScene& hs, uint32_t id, uint32_t ci, v3 base, v3 apex, float r0, float r1, uint32_t mat) {
-    const float base_d = cone_object(base, apex, r0, r1, &hs.rec[16 * (size_t)id], &hs.bounds[6 * (size_t)id],
-                                     &hs.centroid[3 * (size_t)id]);
-    (void)ci;
+static void cone_ctor(HostScene& hs, uint32_t id, uint32_t ci, v3 base, v3 apex, float r0, float r1, uint32_t mat,
+                      int model) {
+    float* rec = &hs.rec[16 * (size_t)id];
+    float* bnd = &hs.bounds[6 * (size_t)id];
+    float* cen = &hs.centroid[3 * (size_t)id];
+    const float base_d = model < 0 ? cone_object(base, apex, r0, r1, rec, bnd, cen)
+                                   : cone_object_xf(base, apex, r0, r1, &hs.models[25 * (size_t)model],
+                                                    &hs.models[25 * (size_t)model + 16], rec, bnd, cen);
+    if (!hs.cone_h.empty()) hs.cone_h[ci] = length(apex - base);  // Cylinder::m_height (pre-transform)
     hs.aux[id] = Aux{base_d, mat, id, 1u};  // flags: cone
+}
+
+std::string scene_models(const khp_scene* s, HostScene& hs) {
+    hs.models.clear();
+    if (s->n_cone_models == 0) {
+        if (s->cone_model) return "cone_model given without cone_models";
+        return std::string();
+    }
+    if (!s->cone_models) return "cone_models missing";
+    hs.models.resize(25 * (size_t)s->n_cone_models);
+    for (uint32_t k = 0; k < s->n_cone_models; ++k) {
+        float* o = &hs.models[25 * (size_t)k];
+        memcpy(o, s->cone_models + 16 * (size_t)k, 16 * sizeof(float));
+        mat4_inverse_transpose3(o, o + 16);
+    }
+    return std::string();
+}
+
+std::string scene_textures(const khp_scene* s, HostScene& hs) {
+    hs.tex.clear();
+    hs.texels.clear();
+    hs.mtex.clear();
+    hs.env_map = s->env_map;
+    hs.textured = false;
+    if (s->n_textures && !s->textures) return "textures missing";
+    size_t off = 0;
+    for (uint32_t i = 0; i < s->n_textures; ++i) {
+        const khp_texture& t = s->textures[i];
+        if (t.width == 0 || t.height == 0 || !t.data) return "texture without texels";
+        if (t.channels < 1 || t.channels > 4) return "texture channels must be 1..4";
+        if ((uint64_t)t.width * t.height >= (1ull << 31)) return "texture too large";
+        hs.tex.push_back(DevTexture{t.width, t.height, t.channels, t.wrap_mode, (uint64_t)off});
+        off += (size_t)t.width * t.height * t.channels;
+    }
+    hs.texels.resize(off);
+    for (uint32_t i = 0; i < s->n_textures; ++i) {
+        const khp_texture& t = s->textures[i];
+        memcpy(hs.texels.data() + hs.tex[i].off, t.data, (size_t)t.width * t.height * t.channels);
+    }
+    auto valid = [&](int32_t k) { return k >= -1 && k < (int32_t)s->n_textures; };
+    hs.mtex.assign(s->n_materials, DevMatTex{{-1, -1, -1, -1, -1}});
+    if (s->material_textures) {
+        for (uint32_t m = 0; m < s->n_materials; ++m) {
+            const khp_material_textures& mt = s->material_textures[m];
+            const int32_t k[5] = {mt.diffuse, mt.specular, mt.volume, mt.emission, mt.roughness};
+            for (int j = 0; j < 5; ++j) {
+                if (!valid(k[j])) return "material texture index out of range";
+                hs.mtex[m].t[j] = k[j];
+                hs.textured = hs.textured || k[j] >= 0;
+            }
+        }
+    }
+    const khp_env_map& e = s->env_map;
+    if (e.type < KHP_ENV_COLOR || e.type > KHP_ENV_SPHERE_MAP) return "unknown environment type";
+    const int nmaps = e.type == KHP_ENV_CUBE_MAP ? 6 : e.type == KHP_ENV_SPHERE_MAP ? 1 : 0;
+    for (int j = 0; j < nmaps; ++j)
+        if (e.tex[j] < 0 || e.tex[j] >= (int32_t)s->n_textures) return "environment map texture index out of range";
+    hs.textured = hs.textured || nmaps > 0;
+    return std::string();
 }
 
 std::string flatten_scene(const khp_scene* s, HostScene& hs, bool objects) {
@@ -91,6 +157,10 @@ std::string flatten_scene(const khp_scene* s, HostScene& hs, bool objects) {
     hs.n_tris = s->n_tris;
     hs.n_cones = s->n_cones;
     hs.n_obj = (uint32_t)n;
+    std::string err = scene_textures(s, hs);
+    if (!err.empty()) return err;
+    err = scene_models(s, hs);
+    if (!err.empty()) return err;
     if (!objects) {  // the device flattens the objects (flatten.hip)
         hs.mats.assign(s->materials, s->materials + s->n_materials);
         hs.lights.resize(s->n_lights);
@@ -110,17 +180,26 @@ std::string flatten_scene(const khp_scene* s, HostScene& hs, bool objects) {
         if (s->tri_mat[i] >= s->n_materials) return "triangle material index out of range";
     for (uint32_t i = 0; i < s->n_cones; ++i)
         if (s->cone_mat[i] >= s->n_materials) return "cone material index out of range";
+    if (s->cone_model)
+        for (uint32_t i = 0; i < s->n_cones; ++i)
+            if (s->cone_model[i] >= s->n_cone_models) return "cone model index out of range";
+    if (hs.textured) {
+        hs.tri_uv.assign(6 * (size_t)s->n_tris, 0.0f);
+        hs.cone_h.assign(s->n_cones, 0.0f);
+    }
     unsigned nt = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
     auto work = [&](unsigned t) {
         for (uint32_t i = t; i < s->n_tris; i += nt) {
             const float* v = s->tri_v + 9 * (size_t)i;
             const float* nn = s->tri_n + 9 * (size_t)i;
-            tri_ctor(hs, i, ld3(v), ld3(v + 3), ld3(v + 6), ld3(nn), ld3(nn + 3), ld3(nn + 6), s->tri_mat[i]);
+            tri_ctor(hs, i, ld3(v), ld3(v + 3), ld3(v + 6), ld3(nn), ld3(nn + 3), ld3(nn + 6), s->tri_mat[i],
+                     s->tri_uv ? s->tri_uv + 6 * (size_t)i : nullptr);
         }
         for (uint32_t i = t; i < s->n_cones; i += nt) {
             const float* b = s->cone_base_r0 + 4 * (size_t)i;
             const float* a = s->cone_apex_r1 + 4 * (size_t)i;
-            cone_ctor(hs, s->n_tris + i, i, ld3(b), ld3(a), b[3], a[3], s->cone_mat[i]);
+            const int model = s->n_cone_models == 0 ? -1 : s->cone_model ? (int)s->cone_model[i] : 0;
+            cone_ctor(hs, s->n_tris + i, i, ld3(b), ld3(a), b[3], a[3], s->cone_mat[i], model);
         }
     };
     if (n < 65536) nt = 1;

@@ -48,6 +48,17 @@ struct DevLight {
     float vert[4][3];
 };
 
+// ABI 6 textures: one entry per khp_texture, texels packed into one byte pool
+struct DevTexture {
+    uint32_t w, h, ch, wrap;
+    uint64_t off;   // byte offset of texel (0, 0) in the pool
+};
+// per material: texture of diffuse, specular, volume, emission, roughness (-1: value)
+struct DevMatTex {
+    int32_t t[5];
+};
+enum : int { MT_DIFFUSE = 0, MT_SPECULAR = 1, MT_VOLUME = 2, MT_EMISSION = 3, MT_ROUGHNESS = 4 };
+
 struct BuildNode {
     v3 mn, mx;
     int32_t left, right, first, count;
@@ -62,6 +73,16 @@ struct HostScene {
     std::vector<float> centroid;   // n_obj * 3
     std::vector<float> tri_nrm;    // n_tris * 9 (na, nb, nc after ctor reordering)
     std::vector<float> tri_frame;  // n_tris * 9 (hair frame u, v, w; fiberToTriangles) or zeros
+    // ABI 6 textures (empty when the scene has none)
+    std::vector<float> tri_uv;     // n_tris * 6 (tca, tcb, tcc after the ctor's reordering)
+    std::vector<float> cone_h;     // n_cones (Cylinder::m_height, pre-transform)
+    std::vector<DevTexture> tex;
+    std::vector<uint8_t> texels;
+    std::vector<DevMatTex> mtex;   // n_materials
+    khp_env_map env_map{};
+    bool textured = false;         // any textured material parameter or environment map
+    // ABI 6 cone node transforms: per model M (16) then mat3(transpose(inverse(M))) (9)
+    std::vector<float> models;
     std::vector<khp_material> mats;
     std::vector<DevLight> lights;
     khp_environment env{};
@@ -83,6 +104,11 @@ struct HostScene {
 // objects=false: validate and keep materials/lights/env/camera only (the
 // device flattens the objects).
 std::string flatten_scene(const khp_scene* s, HostScene& hs, bool objects = true);
+// Validates and copies the scene's textures / material texture indices /
+// environment map into hs (both flatten paths); empty string on success.
+std::string scene_textures(const khp_scene* s, HostScene& hs);
+// Per-model M and inverse-transpose table (both flatten paths).
+std::string scene_models(const khp_scene* s, HostScene& hs);
 void build_bvh(HostScene& hs, int n_threads);
 void make_device_layout(HostScene& hs);
 void light_init(DevLight& L, const khp_light& in);

@@ -55,12 +55,36 @@ class Camera(ctypes.Structure):
     _fields_ = [("position", F3), ("bottom_left", F3), ("axis_x", F3), ("axis_y", F3), ("pixel_size", c_float)]
 
 
+TEX_WRAP_CLAMP, TEX_WRAP_TILE = 0, 1
+ENV_COLOR, ENV_CUBE_MAP, ENV_SPHERE_MAP = 0, 1, 2
+
+
+class Texture(ctypes.Structure):
+    """khp_texture (ABI 6): KIRK::Texture's 8-bit texels."""
+    _fields_ = [("width", c_uint32), ("height", c_uint32), ("channels", c_uint32), ("wrap_mode", c_uint32),
+                ("data", POINTER(c_uint8))]
+
+
+class MaterialTextures(ctypes.Structure):
+    """khp_material_textures (ABI 6): texture index per parameter, -1 = the material value."""
+    _fields_ = [("diffuse", c_int32), ("specular", c_int32), ("volume", c_int32), ("emission", c_int32),
+                ("roughness", c_int32)]
+
+
+class EnvMap(ctypes.Structure):
+    """khp_env_map (ABI 6): Environment::m_type and its textures."""
+    _fields_ = [("type", c_int32), ("tex", c_int32 * 6)]
+
+
 class SceneDesc(ctypes.Structure):
     _fields_ = [("n_tris", c_uint32), ("tri_v", POINTER(c_float)), ("tri_n", POINTER(c_float)),
                 ("tri_mat", POINTER(c_uint32)), ("n_cones", c_uint32), ("cone_base_r0", POINTER(c_float)),
                 ("cone_apex_r1", POINTER(c_float)), ("cone_mat", POINTER(c_uint32)), ("n_materials", c_uint32),
                 ("materials", POINTER(Material)), ("n_lights", c_uint32), ("lights", POINTER(Light)),
-                ("env", Environment), ("camera", Camera), ("tri_frame", POINTER(c_float))]
+                ("env", Environment), ("camera", Camera), ("tri_frame", POINTER(c_float)),
+                ("n_cone_models", c_uint32), ("cone_models", POINTER(c_float)), ("cone_model", POINTER(c_uint32)),
+                ("n_textures", c_uint32), ("textures", POINTER(Texture)),
+                ("material_textures", POINTER(MaterialTextures)), ("tri_uv", POINTER(c_float)), ("env_map", EnvMap)]
 
 
 class RenderParams(ctypes.Structure):

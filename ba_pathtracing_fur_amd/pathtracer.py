@@ -137,6 +137,8 @@ class HipContext:
             d.tri_n = ctypes.cast(dev(scene.tri_n), ctypes.POINTER(ctypes.c_float))
             d.tri_mat = ctypes.cast(dev(scene.tri_mat), ctypes.POINTER(ctypes.c_uint32))
             d.tri_frame = ctypes.cast(dev(scene.frames()), ctypes.POINTER(ctypes.c_float))
+            if scene.textures:
+                d.tri_uv = ctypes.cast(dev(scene.uvs()), ctypes.POINTER(ctypes.c_float))
         if cones is not None:
             if len(scene.cone_base_r0):
                 raise ValueError("scene already has cones")
@@ -149,6 +151,8 @@ class HipContext:
             d.cone_base_r0 = ctypes.cast(dev(scene.cone_base_r0), ctypes.POINTER(ctypes.c_float))
             d.cone_apex_r1 = ctypes.cast(dev(scene.cone_apex_r1), ctypes.POINTER(ctypes.c_float))
             d.cone_mat = ctypes.cast(dev(scene.cone_mat), ctypes.POINTER(ctypes.c_uint32))
+            if len(scene.cone_models):
+                d.cone_model = ctypes.cast(dev(scene.cone_model), ctypes.POINTER(ctypes.c_uint32))
         N.check(self.lib, self.lib.khp_set_scene_device(self.ptr, ctypes.byref(d)), "khp_set_scene_device")
         for b in keep:
             b.free()

@@ -124,23 +124,73 @@ class SceneData:
     env_ambient: tuple = (0.1, 0.1, 0.1)  # Environment.h:158 default
     cam: N.Camera | None = None
     name: str = "scene"
+    # ABI 6: cone node transforms (glm::mat4, column-major) and per-cone model index
+    cone_models: np.ndarray = field(default_factory=lambda: np.zeros((0, 16), np.float32))
+    cone_model: np.ndarray = field(default_factory=lambda: np.zeros((0,), np.uint32))
+    # ABI 6: textures [(texels (H, W, C) uint8, wrap_mode)], per-material texture ids (n_mat, 5)
+    # (diffuse, specular, volume, emission, roughness; -1 = value), texcoords, environment map
+    textures: list = field(default_factory=list)
+    material_textures: np.ndarray | None = None
+    tri_uv: np.ndarray = field(default_factory=lambda: np.zeros((0, 3, 2), np.float32))
+    env_map: tuple = (0, (-1, -1, -1, -1, -1, -1))
 
     # --- building ------------------------------------------------------------
     def add_material(self, m: N.Material) -> int:
         self.materials.append(m)
         return len(self.materials) - 1
 
-    def add_triangles(self, v: np.ndarray, n: np.ndarray, mat: int, frame: np.ndarray | None = None):
+    def add_triangles(self, v: np.ndarray, n: np.ndarray, mat: int, frame: np.ndarray | None = None,
+                      uv: np.ndarray | None = None):
         """Triangles (a, b, c) with vertex normals; frame: optional hair frame u, v, w per
-        triangle (Object::setU/V/W, fiberToTriangles fur), zero otherwise."""
+        triangle (Object::setU/V/W, fiberToTriangles fur), zero otherwise; uv: optional
+        texcoords tca, tcb, tcc per triangle (zero otherwise)."""
         v = np.ascontiguousarray(v, np.float32).reshape(-1, 3, 3)
         n = np.ascontiguousarray(n, np.float32).reshape(-1, 3, 3)
+        old_uv = self.uvs()
+        self.tri_uv = np.concatenate([old_uv, np.zeros((len(v), 3, 2), np.float32) if uv is None
+                                      else np.asarray(uv, np.float32).reshape(-1, 3, 2)])
         old = self.frames()
         self.tri_v = np.concatenate([self.tri_v, v])
         self.tri_n = np.concatenate([self.tri_n, n])
         self.tri_mat = np.concatenate([self.tri_mat, np.full(len(v), mat, np.uint32)])
         f = np.zeros((len(v), 3, 3), np.float32) if frame is None else np.asarray(frame, np.float32).reshape(-1, 3, 3)
         self.tri_frame = np.concatenate([old, f])
+
+    def uvs(self) -> np.ndarray:
+        """tri_uv padded with zero texcoords to one triple per triangle."""
+        u = np.asarray(self.tri_uv, np.float32).reshape(-1, 3, 2)
+        if len(u) < len(self.tri_v):
+            u = np.concatenate([u, np.zeros((len(self.tri_v) - len(u), 3, 2), np.float32)])
+        return u
+
+    def add_texture(self, texels: np.ndarray, wrap_mode: int = N.TEX_WRAP_TILE) -> int:
+        """A KIRK::Texture: (H, W, C) uint8, C in 1..4, row y = texture row y."""
+        t = np.ascontiguousarray(texels, np.uint8)
+        if t.ndim == 2:
+            t = t[:, :, None]
+        self.textures.append((t, int(wrap_mode)))
+        return len(self.textures) - 1
+
+    def set_material_texture(self, mat: int, param: str, tex: int):
+        """Textures material parameter `param` (diffuse | specular | volume | emission | roughness)."""
+        keys = ["diffuse", "specular", "volume", "emission", "roughness"]
+        if self.material_textures is None or len(self.material_textures) < len(self.materials):
+            mt = np.full((len(self.materials), 5), -1, np.int32)
+            if self.material_textures is not None:
+                mt[:len(self.material_textures)] = self.material_textures
+            self.material_textures = mt
+        self.material_textures[mat, keys.index(param)] = tex
+
+    def set_environment_map(self, kind: int, tex):
+        """Environment::loadCubeMap (6 textures: posx, posy, posz, negx, negy, negz) or loadSphereMap."""
+        t = list(tex) + [-1] * (6 - len(tex))
+        self.env_map = (int(kind), tuple(int(x) for x in t))
+
+    def add_cone_model(self, M: np.ndarray) -> int:
+        """A node transform (4x4, row-major numpy matrix acting on column vectors) for cones."""
+        m = np.asarray(M, np.float32).reshape(4, 4)
+        self.cone_models = np.concatenate([self.cone_models, m.T.reshape(1, 16)])  # glm: column-major
+        return len(self.cone_models) - 1
 
     def frames(self) -> np.ndarray:
         """tri_frame padded with zero frames to one per triangle."""
@@ -150,7 +200,7 @@ class SceneData:
         return f
 
     def add_fibers(self, positions: np.ndarray, radii: np.ndarray, mat: int, as_triangles: bool = False,
-                   resolution: int = 5):
+                   resolution: int = 5, model: int | None = None):
         """Fur fibers -> cones exactly as CPU_Scene::flattenNode (khp_fibers_to_cones), or, with
         as_triangles (m_fiberAsCylinder = false), -> triangle tubes as fiberToTriangles
         (khp_fibers_to_triangles, CPU_Scene.cpp:232-345)."""
@@ -171,12 +221,23 @@ class SceneData:
         apex = np.empty((nf * (nv - 1), 4), np.float32)
         N.check(lib, lib.khp_fibers_to_cones(nf, nv, N.fptr(positions), N.fptr(radii), N.fptr(base), N.fptr(apex)),
                 "khp_fibers_to_cones")
-        self.add_cones(base, apex, mat)
+        self.add_cones(base, apex, mat, model)
 
-    def add_cones(self, base_r0: np.ndarray, apex_r1: np.ndarray, mat: int):
+    def add_cones(self, base_r0: np.ndarray, apex_r1: np.ndarray, mat: int, model: int | None = None):
+        """Cones (Cylinder ctor args); model: index of a node transform (add_cone_model),
+        None = world space (an identity model once any cone of the scene has one)."""
+        n_old = len(self.cone_base_r0)
         self.cone_base_r0 = np.concatenate([self.cone_base_r0, np.asarray(base_r0, np.float32).reshape(-1, 4)])
         self.cone_apex_r1 = np.concatenate([self.cone_apex_r1, np.asarray(apex_r1, np.float32).reshape(-1, 4)])
         self.cone_mat = np.concatenate([self.cone_mat, np.full(len(base_r0), mat, np.uint32)])
+        if model is None and len(self.cone_models) == 0:
+            return
+        if len(self.cone_model) < n_old:  # earlier world-space cones: the identity model
+            ident = self.add_cone_model(np.eye(4))
+            self.cone_model = np.concatenate([self.cone_model, np.full(n_old - len(self.cone_model), ident, np.uint32)])
+        if model is None:
+            model = self.add_cone_model(np.eye(4))
+        self.cone_model = np.concatenate([self.cone_model, np.full(len(base_r0), model, np.uint32)])
 
     @property
     def n_objects(self) -> int:
@@ -213,6 +274,32 @@ class SceneData:
         if self.cam is None:
             raise ValueError("scene has no camera")
         d.camera = self.cam
+        # ABI 6
+        self.cone_models = np.ascontiguousarray(self.cone_models, np.float32).reshape(-1, 16)
+        d.n_cone_models = len(self.cone_models)
+        d.cone_models = N.fptr(self.cone_models)
+        if len(self.cone_models):
+            if len(self.cone_model) != len(self.cone_base_r0):
+                raise ValueError("cone_model must name a model for every cone")
+            self.cone_model = np.ascontiguousarray(self.cone_model, np.uint32)
+            d.cone_model = N.uptr(self.cone_model)
+        self._tex = [np.ascontiguousarray(t, np.uint8) for t, _ in self.textures]
+        self._texs = (N.Texture * max(1, len(self.textures)))()
+        for i, ((t, wrap), data) in enumerate(zip(self.textures, self._tex)):
+            self._texs[i] = N.Texture(t.shape[1], t.shape[0], t.shape[2], wrap,
+                                      data.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+        d.n_textures = len(self.textures)
+        d.textures = ctypes.cast(self._texs, ctypes.POINTER(N.Texture))
+        if self.material_textures is not None:
+            mt = np.full((len(self.materials), 5), -1, np.int32)
+            mt[:len(self.material_textures)] = self.material_textures
+            self._mtex = (N.MaterialTextures * len(self.materials))(*[N.MaterialTextures(*map(int, r)) for r in mt])
+            d.material_textures = ctypes.cast(self._mtex, ctypes.POINTER(N.MaterialTextures))
+        if self.textures:
+            self.tri_uv = np.ascontiguousarray(self.uvs(), np.float32)
+            d.tri_uv = N.fptr(self.tri_uv)
+        d.env_map.type = self.env_map[0]
+        d.env_map.tex[:] = self.env_map[1]
         self._desc = d
         return d
 
@@ -224,7 +311,14 @@ class SceneData:
                 "cone_base_r0": self.cone_base_r0, "cone_apex_r1": self.cone_apex_r1, "cone_mat": self.cone_mat,
                 "materials": raw(self.materials, N.Material), "lights": raw(self.lights, N.Light),
                 "env": np.float32([*self.env_color, *self.env_ambient]),
-                "camera": np.frombuffer(bytes(self.cam), np.uint8).copy(), "name": np.array(self.name)}
+                "camera": np.frombuffer(bytes(self.cam), np.uint8).copy(), "name": np.array(self.name),
+                "cone_models": self.cone_models, "cone_model": self.cone_model, "tri_uv": self.uvs(),
+                "material_textures": (np.zeros((0, 5), np.int32) if self.material_textures is None
+                                      else self.material_textures),
+                "env_map": np.int32([self.env_map[0], *self.env_map[1]]),
+                "n_textures": np.int32(len(self.textures)),
+                **{f"texture{i}": t for i, (t, _) in enumerate(self.textures)},
+                "texture_wrap": np.int32([w for _, w in self.textures])}
 
     @classmethod
     def from_arrays(cls, a) -> "SceneData":
@@ -232,18 +326,30 @@ class SceneData:
             buf = np.ascontiguousarray(buf, np.uint8).tobytes()
             n = len(buf) // ctypes.sizeof(T)
             return list((T * n).from_buffer_copy(buf)) if n else []
+        files = set(getattr(a, "files", a))
+        get = lambda k, default: a[k] if k in files else default
         env = np.asarray(a["env"], np.float32)
-        return cls(tri_v=np.asarray(a["tri_v"], np.float32), tri_n=np.asarray(a["tri_n"], np.float32),
-                   tri_mat=np.asarray(a["tri_mat"], np.uint32),
-                   tri_frame=np.asarray(a["tri_frame"], np.float32) if "tri_frame" in getattr(a, "files", a)
-                   else np.zeros((0, 3, 3), np.float32),
-                   cone_base_r0=np.asarray(a["cone_base_r0"], np.float32),
-                   cone_apex_r1=np.asarray(a["cone_apex_r1"], np.float32),
-                   cone_mat=np.asarray(a["cone_mat"], np.uint32),
-                   materials=structs(a["materials"], N.Material), lights=structs(a["lights"], N.Light),
-                   env_color=tuple(float(x) for x in env[:3]), env_ambient=tuple(float(x) for x in env[3:]),
-                   cam=N.Camera.from_buffer_copy(np.ascontiguousarray(a["camera"], np.uint8).tobytes()),
-                   name=str(a["name"]))
+        sd = cls(tri_v=np.asarray(a["tri_v"], np.float32), tri_n=np.asarray(a["tri_n"], np.float32),
+                 tri_mat=np.asarray(a["tri_mat"], np.uint32),
+                 tri_frame=np.asarray(get("tri_frame", np.zeros((0, 3, 3), np.float32)), np.float32),
+                 cone_base_r0=np.asarray(a["cone_base_r0"], np.float32),
+                 cone_apex_r1=np.asarray(a["cone_apex_r1"], np.float32),
+                 cone_mat=np.asarray(a["cone_mat"], np.uint32),
+                 materials=structs(a["materials"], N.Material), lights=structs(a["lights"], N.Light),
+                 env_color=tuple(float(x) for x in env[:3]), env_ambient=tuple(float(x) for x in env[3:]),
+                 cam=N.Camera.from_buffer_copy(np.ascontiguousarray(a["camera"], np.uint8).tobytes()),
+                 name=str(a["name"]))
+        sd.cone_models = np.asarray(get("cone_models", np.zeros((0, 16), np.float32)), np.float32).reshape(-1, 16)
+        sd.cone_model = np.asarray(get("cone_model", np.zeros((0,), np.uint32)), np.uint32)
+        sd.tri_uv = np.asarray(get("tri_uv", np.zeros((0, 3, 2), np.float32)), np.float32)
+        mt = np.asarray(get("material_textures", np.zeros((0, 5), np.int32)), np.int32)
+        sd.material_textures = mt if len(mt) else None
+        em = np.asarray(get("env_map", np.int32([0, -1, -1, -1, -1, -1, -1])), np.int32)
+        sd.env_map = (int(em[0]), tuple(int(x) for x in em[1:7]))
+        wraps = np.asarray(get("texture_wrap", np.zeros((0,), np.int32)), np.int32)
+        sd.textures = [(np.asarray(a[f"texture{i}"], np.uint8), int(wraps[i]))
+                       for i in range(int(get("n_textures", 0)))]
+        return sd
 
 
 # ---- generators (libkirk_hip host code) -------------------------------------------
@@ -419,5 +525,103 @@ def zoo(width=64, height=48, n_strands=400) -> SceneData:
     return sd
 
 
+def checker(h: int, w: int, channels: int, cells: int = 4, seed: int = 7) -> np.ndarray:
+    """Seeded checkerboard texels (H, W, C) uint8: `cells` x `cells` blocks of random colours."""
+    rng = np.random.default_rng(seed)
+    cols = rng.integers(0, 256, (cells, cells, channels), dtype=np.uint8)
+    yy = (np.arange(h) * cells // h)[:, None]
+    xx = (np.arange(w) * cells // w)[None, :]
+    return np.ascontiguousarray(cols[yy, xx])
+
+
+def rotation(axis, angle_rad: float) -> np.ndarray:
+    a = np.asarray(axis, np.float64)
+    a /= np.linalg.norm(a)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    R = np.eye(3) + np.sin(angle_rad) * K + (1 - np.cos(angle_rad)) * K @ K
+    M = np.eye(4)
+    M[:3, :3] = R
+    return M
+
+
+def node_transform(translate=(0, 0, 0), axis=(0, 1, 0), angle_rad=0.0, scale=(1, 1, 1)) -> np.ndarray:
+    """T * R * S as a scene node's model matrix (float32)."""
+    T = np.eye(4)
+    T[:3, 3] = translate
+    S = np.diag([*scale, 1.0])
+    return (T @ rotation(axis, angle_rad) @ S).astype(np.float32)
+
+
+def transformed_hairball(width=64, height=48, n_strands=1500, bsdf="MarschnerHairBSDF") -> SceneData:
+    """Coverage scene for the Cylinder node transform (Cylinder.cpp:5-29): two
+    hairball nodes in object space, one rotated about a tilted axis and scaled
+    non-uniformly, one translated only, on a plane under a quad light."""
+    sd = SceneData(name="transformed_hairball")
+    v, n = quad((-6, 0, -6), (-6, 0, 6), (6, 0, 6), (6, 0, -6), (0, 1, 0))
+    sd.add_triangles(v, n, sd.add_material(material(diffuse=(0.5, 0.5, 0.5))))
+    fur = sd.add_material(fiber_material(bsdf))
+    pos, rad = hairball(n_strands, (0.0, 0.0, 0.0), 0.35)
+    m0 = sd.add_cone_model(node_transform((-0.45, 0.55, 0.0), (0.3, 1.0, 0.2), 0.7, (1.3, 0.8, 1.1)))
+    sd.add_fibers(pos, rad, fur, model=m0)
+    m1 = sd.add_cone_model(node_transform((0.5, 0.45, 0.1)))
+    pos2, rad2 = hairball(n_strands // 2, (0.0, 0.0, 0.0), 0.3, seed=SEED + 1)
+    sd.add_fibers(pos2, rad2, fur, model=m1)
+    sd.lights.append(quad_light((0.0, 3.0, 0.0), (0.0, -1.0, 0.0), (2.0, 2.0), (5.0, 5.0, 5.0), att_const=1.0))
+    sd.env_color = (0.6, 0.7, 0.9)
+    sd.cam = camera((0.0, 0.8, 2.6), (0.0, -0.15, -1.0), (0.0, 1.0, 0.0), width, height)
+    return sd
+
+
+def textured(width=64, height=48, n_strands=600, env: str = "cube") -> SceneData:
+    """Coverage scene for textures (Texture::getColor, Material::getFromParam,
+    calcTcoord of triangles and cones, Environment cube / sphere maps): a
+    diffuse-textured floor (tiled uv beyond [0, 1]), a glossy panel with
+    textured specular + roughness, an emission-textured quad, a glass sphere
+    with a textured volume colour, fur with a textured diffuse colour, and
+    an environment map."""
+    sd = SceneData(name=f"textured_{env}")
+    t_floor = sd.add_texture(checker(32, 48, 3, 6, seed=1))
+    t_spec = sd.add_texture(checker(16, 16, 4, 4, seed=2), N.TEX_WRAP_CLAMP)
+    t_rough = sd.add_texture(checker(8, 8, 1, 2, seed=3))
+    t_emit = sd.add_texture(checker(24, 24, 2, 3, seed=4))
+    t_fur = sd.add_texture(checker(16, 64, 3, 8, seed=5))
+    t_vol = sd.add_texture(checker(8, 8, 3, 2, seed=6))
+    floor = sd.add_material(material(diffuse=(0.5, 0.5, 0.5)))
+    sd.set_material_texture(floor, "diffuse", t_floor)
+    v, n = quad((-4, 0, -4), (-4, 0, 4), (4, 0, 4), (4, 0, -4), (0, 1, 0))
+    sd.add_triangles(v, n, floor, uv=np.float32([[[-1.5, -1.5], [-1.5, 2.5], [2.5, 2.5]],
+                                                 [[-1.5, -1.5], [2.5, 2.5], [2.5, -1.5]]]))
+    glossy = sd.add_material(material("GlossyBSDF", diffuse=(0.2, 0.3, 0.6), roughness=0.4))
+    sd.set_material_texture(glossy, "specular", t_spec)
+    sd.set_material_texture(glossy, "roughness", t_rough)
+    v, n = quad((-1.8, 0, -1.5), (0.2, 0, -1.5), (0.2, 1.6, -1.5), (-1.8, 1.6, -1.5), (0, 0, 1))
+    sd.add_triangles(v, n, glossy, uv=np.float32([[[0, 0], [1, 0], [1, 1]], [[0, 0], [1, 1], [0, 1]]]))
+    emit = sd.add_material(material("EmissionBSDF", emission=(1.0, 1.0, 1.0)))
+    sd.set_material_texture(emit, "emission", t_emit)
+    v, n = quad((0.6, 0.2, -1.4), (1.8, 0.2, -1.4), (1.8, 1.4, -1.4), (0.6, 1.4, -1.4), (0, 0, 1))
+    sd.add_triangles(v, n, emit, uv=np.float32([[[0, 0], [1, 0], [1, 1]], [[0, 0], [1, 1], [0, 1]]]))
+    glass = sd.add_material(material("GlassBSDF", ior=1.45))
+    sd.set_material_texture(glass, "volume", t_vol)
+    gv, gn = icosphere(2, (1.3, 0.35, 0.3), 0.35)
+    uv = np.stack([0.5 + 0.5 * np.arctan2(gv[..., 2] - 0.3, gv[..., 0] - 1.3) / np.pi, (gv[..., 1] - 0.0) / 0.7],
+                  axis=-1).astype(np.float32)
+    sd.add_triangles(gv, gn, glass, uv=uv)
+    fur = sd.add_material(fiber_material())
+    sd.set_material_texture(fur, "diffuse", t_fur)
+    pos, rad = hairball(n_strands, (-0.3, 0.45, 0.2), 0.3, root_radius=0.006)
+    sd.add_fibers(pos, rad, fur)
+    sd.lights.append(quad_light((0.0, 2.8, 0.0), (0.0, -1.0, 0.0), (1.2, 1.2), (4.0, 4.0, 4.0), att_const=1.0))
+    sd.lights.append(point_light((2.0, 2.0, 2.0), (2.0, 1.8, 1.5), radius=0.2))
+    if env == "cube":
+        faces = [sd.add_texture(checker(8, 8, 3, 2, seed=20 + k)) for k in range(6)]
+        sd.set_environment_map(N.ENV_CUBE_MAP, faces)
+    elif env == "sphere":
+        sd.set_environment_map(N.ENV_SPHERE_MAP, [sd.add_texture(checker(32, 32, 3, 4, seed=30))])
+    sd.env_ambient = (0.05, 0.05, 0.05)
+    sd.cam = camera((0.0, 1.3, 3.4), (0.0, -0.25, -1.0), (0.0, 1.0, 0.0), width, height)
+    return sd
+
+
 def build_config(name: str, **kw) -> SceneData:
-    return {"config1": config1, "config2": config2, "config3": config3, "config5": config5, "zoo": zoo}[name](**kw)
+    return {"config1": config1, "config2": config2, "config3": config3, "config5": config5, "zoo": zoo,
+            "transformed": transformed_hairball, "textured": textured}[name](**kw)

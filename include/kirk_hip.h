@@ -70,7 +70,9 @@ typedef enum {
     KHP_SHADER_COUNT = 2
 } khp_shader_kind;
 
-/* KIRK::Material (Material.h:53-152), untextured values only (a17 in SURVEY §8). */
+/* KIRK::Material (Material.h:53-152): the parameter values.  Textured
+ * parameters (MatParamColor/MatParamFloat with a texture) are given by
+ * khp_scene.material_textures below (ABI 6). */
 typedef struct {
     int32_t bsdf;          /* khp_bsdf_kind   */
     int32_t shader;        /* khp_shader_kind */
@@ -103,11 +105,40 @@ typedef struct {
     float inner_angle, outer_angle;   /* SpotLight, degrees                  */
 } khp_light;
 
-/* KIRK::Environment (Environment.h), COLOR type: background + ambient. */
+/* KIRK::Environment (Environment.h): background colour + ambient.  The
+ * CUBE_MAP / SPHERE_MAP types are khp_scene.env_map (ABI 6). */
 typedef struct {
     float color[3];
     float ambient[3];
 } khp_environment;
+
+/* ABI 6: KIRK::Texture as the CPU path tracer reads it (Texture.cpp:243-287):
+ * 8-bit texels, 1..4 channels, row y at data + y * width * channels (KIRK's
+ * m_texture_data), looked up nearest-texel with KIRK's wrap rule. */
+#define KHP_TEX_WRAP_CLAMP 0   /* TEXTURE_WRAP_MODE_CLAMP (Texture.h:34) */
+#define KHP_TEX_WRAP_TILE 1    /* TEXTURE_WRAP_MODE_TILE  (Texture.h:35), KIRK's default */
+typedef struct {
+    uint32_t width, height;
+    uint32_t channels;         /* 1 (rrrr), 2 (rrrg), 3 (rgb1) or 4 (rgba)         */
+    uint32_t wrap_mode;        /* m_texture_wrap_mode                              */
+    const uint8_t* data;       /* width * height * channels bytes, copied          */
+} khp_texture;
+
+/* ABI 6: which material parameters are textured (index into khp_scene.textures,
+ * -1: the khp_material value).  Material::getFromParam (Material.cpp:15-23):
+ * colours take the texel's rgb, roughness takes the length of its rgba. */
+typedef struct {
+    int32_t diffuse, specular, volume, emission, roughness;
+} khp_material_textures;
+
+/* ABI 6: Environment::m_type (Environment.h:25-30, getColor Environment.cpp:91-133). */
+#define KHP_ENV_COLOR 0
+#define KHP_ENV_CUBE_MAP 1     /* tex: posx, posy, posz, negx, negy, negz (loadCubeMap order) */
+#define KHP_ENV_SPHERE_MAP 2   /* tex[0] */
+typedef struct {
+    int32_t type;
+    int32_t tex[6];            /* indices into khp_scene.textures                  */
+} khp_env_map;
 
 /* The state KIRK::Camera::applyParameters derives (Camera.cpp:6-37). */
 typedef struct {
@@ -141,6 +172,21 @@ typedef struct {
      * 232-345, for fur drawn as triangle tubes; read by the hair BSDFs).
      * NULL: zero frames (KIRK leaves them uninitialised on plain triangles). */
     const float* tri_frame;
+    /* ABI 6: node transforms of the cones.  flattenNode hands each fiber's
+     * Cylinder the transform base_transform * child->m_transform
+     * (CPU_Scene.cpp:119, 136-137); the ctor maps base/apex by it and the frame
+     * by its inverse transpose (Cylinder.cpp:5-29).  cone_base_r0/apex_r1 are
+     * then the PRE-transform points.  n_cone_models = 0: world-space cones
+     * (identity, the ctor's arithmetic without the matrix products). */
+    uint32_t n_cone_models;
+    const float* cone_models;     /* [n_cone_models][16] glm::mat4, column-major             */
+    const uint32_t* cone_model;   /* [n_cones] index into cone_models; NULL: model 0 for all */
+    /* ABI 6: textures (a17 / a16 / a9 in SURVEY §8) */
+    uint32_t n_textures;
+    const khp_texture* textures;
+    const khp_material_textures* material_textures;  /* [n_materials], or NULL: untextured */
+    const float* tri_uv;          /* [n_tris][3][2] texcoords tca, tcb, tcc, or NULL: zeros   */
+    khp_env_map env_map;          /* type KHP_ENV_COLOR: env.color (zero-initialised = COLOR) */
 } khp_scene;
 
 #define KHP_RENDER_OUT_DEVICE   (1u << 0)  /* out_rgb is a device pointer        */

@@ -294,10 +294,13 @@ typedef struct {
     /* cone */
     v3 base, apex, u, v, w;
     float r0, r1, height, slope, base_d, min_d, max_d;
+    /* texcoords m_tca, m_tcb, m_tcc after the ctor's vertex reordering (triangles) */
+    float tc[6];
 } obj_t;
 
-/* Triangle::Triangle (Common/Triangle.cpp:3-129), identity model matrix. */
-static void tri_ctor(obj_t* o, v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc) {
+/* Triangle::Triangle (Common/Triangle.cpp:3-129), identity model matrix.  The
+ * texcoords tca/tcb/tcc (uv: 6 floats or NULL) follow the vertex reordering. */
+static void tri_ctor(obj_t* o, v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc, const float* uv) {
     memset(o, 0, sizeof(*o));
     o->bmin = vsub(v3min(v3min(a, b), c), V(RAY_EPS, RAY_EPS, RAY_EPS));
     o->bmax = vadd(v3max(v3max(a, b), c), V(RAY_EPS, RAY_EPS, RAY_EPS));
@@ -310,12 +313,17 @@ static void tri_ctor(obj_t* o, v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc) {
     v3 Na = normalize(na), Nb = normalize(nb), Nc = normalize(nc);
     o->A = a; o->B = b; o->C = c; o->na = Na; o->nb = Nb; o->nc = Nc;
     float ca = comp(a, lA), cb = comp(b, lA), cc = comp(c, lA);
-    if (ca <= cb && cb <= cc) { o->A = a; o->B = b; o->C = c; o->na = Na; o->nb = Nb; o->nc = Nc; }
-    if (cb <= ca && ca <= cc) { o->A = b; o->B = a; o->C = c; o->na = Nb; o->nb = Na; o->nc = Nc; }
-    if (ca <= cc && cc <= cb) { o->A = a; o->B = c; o->C = b; o->na = Na; o->nb = Nc; o->nc = Nb; }
-    if (cc <= ca && ca <= cb) { o->A = c; o->B = a; o->C = b; o->na = Nc; o->nb = Na; o->nc = Nb; }
-    if (cb <= cc && cc <= ca) { o->A = b; o->B = c; o->C = a; o->na = Nb; o->nb = Nc; o->nc = Na; }
-    if (cc <= cb && cb <= ca) { o->A = c; o->B = b; o->C = a; o->na = Nc; o->nb = Nb; o->nc = Na; }
+    static const float zero_uv[6] = {0, 0, 0, 0, 0, 0};
+    const float* t = uv ? uv : zero_uv;
+    float ta[2] = {t[0], t[1]}, tb[2] = {t[2], t[3]}, tcc[2] = {t[4], t[5]};
+    const float *TA = ta, *TB = tb, *TC = tcc;
+    if (ca <= cb && cb <= cc) { o->A = a; o->B = b; o->C = c; o->na = Na; o->nb = Nb; o->nc = Nc; TA = ta; TB = tb; TC = tcc; }
+    if (cb <= ca && ca <= cc) { o->A = b; o->B = a; o->C = c; o->na = Nb; o->nb = Na; o->nc = Nc; TA = tb; TB = ta; TC = tcc; }
+    if (ca <= cc && cc <= cb) { o->A = a; o->B = c; o->C = b; o->na = Na; o->nb = Nc; o->nc = Nb; TA = ta; TB = tcc; TC = tb; }
+    if (cc <= ca && ca <= cb) { o->A = c; o->B = a; o->C = b; o->na = Nc; o->nb = Na; o->nc = Nb; TA = tcc; TB = ta; TC = tb; }
+    if (cb <= cc && cc <= ca) { o->A = b; o->B = c; o->C = a; o->na = Nb; o->nb = Nc; o->nc = Na; TA = tb; TB = tcc; TC = ta; }
+    if (cc <= cb && cb <= ca) { o->A = c; o->B = b; o->C = a; o->na = Nc; o->nb = Nb; o->nc = Na; TA = tcc; TB = tb; TC = ta; }
+    o->tc[0] = TA[0]; o->tc[1] = TA[1]; o->tc[2] = TB[0]; o->tc[3] = TB[1]; o->tc[4] = TC[0]; o->tc[5] = TC[1];
     o->ab = vsub(o->B, o->A);
     o->ac = vsub(o->C, o->A);
     o->bc = vsub(o->C, o->B);
@@ -326,18 +334,83 @@ static void tri_ctor(obj_t* o, v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc) {
     o->centroid = vdivs(vadd(vadd(o->A, o->B), o->C), 3.0f);
 }
 
-/* Cylinder::Cylinder + computeBounds (Common/Cylinder.cpp:5-67, 306-336), identity transform. */
-static void cone_ctor(obj_t* o, v3 base, v3 apex, float r0, float r1) {
+/* glm 0.9.9 (func_matrix.inl compute_inverse<4,4>): Coef/Fac/Vec/Inv with
+ * SignA = (+,-,+,-), SignB = (-,+,-,+), determinant = (d0 + d1) + (d2 + d3)
+ * over the first column of M and the first row of the adjugate; returns
+ * mat3(transpose(inverse(M))) column-major in ti.  M column-major, M[4c+r]. */
+static void glm_inverse_transpose3(const float* M, float* ti) {
+    float m[4][4];
+    for (int cc = 0; cc < 4; ++cc) for (int r = 0; r < 4; ++r) m[cc][r] = M[4 * cc + r];
+    float Coef00 = m[2][2] * m[3][3] - m[3][2] * m[2][3];
+    float Coef02 = m[1][2] * m[3][3] - m[3][2] * m[1][3];
+    float Coef03 = m[1][2] * m[2][3] - m[2][2] * m[1][3];
+    float Coef04 = m[2][1] * m[3][3] - m[3][1] * m[2][3];
+    float Coef06 = m[1][1] * m[3][3] - m[3][1] * m[1][3];
+    float Coef07 = m[1][1] * m[2][3] - m[2][1] * m[1][3];
+    float Coef08 = m[2][1] * m[3][2] - m[3][1] * m[2][2];
+    float Coef10 = m[1][1] * m[3][2] - m[3][1] * m[1][2];
+    float Coef11 = m[1][1] * m[2][2] - m[2][1] * m[1][2];
+    float Coef12 = m[2][0] * m[3][3] - m[3][0] * m[2][3];
+    float Coef14 = m[1][0] * m[3][3] - m[3][0] * m[1][3];
+    float Coef15 = m[1][0] * m[2][3] - m[2][0] * m[1][3];
+    float Coef16 = m[2][0] * m[3][2] - m[3][0] * m[2][2];
+    float Coef18 = m[1][0] * m[3][2] - m[3][0] * m[1][2];
+    float Coef19 = m[1][0] * m[2][2] - m[2][0] * m[1][2];
+    float Coef20 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
+    float Coef22 = m[1][0] * m[3][1] - m[3][0] * m[1][1];
+    float Coef23 = m[1][0] * m[2][1] - m[2][0] * m[1][1];
+    float Fac0[4] = {Coef00, Coef00, Coef02, Coef03}, Fac1[4] = {Coef04, Coef04, Coef06, Coef07};
+    float Fac2[4] = {Coef08, Coef08, Coef10, Coef11}, Fac3[4] = {Coef12, Coef12, Coef14, Coef15};
+    float Fac4[4] = {Coef16, Coef16, Coef18, Coef19}, Fac5[4] = {Coef20, Coef20, Coef22, Coef23};
+    float Vec0[4] = {m[1][0], m[0][0], m[0][0], m[0][0]}, Vec1[4] = {m[1][1], m[0][1], m[0][1], m[0][1]};
+    float Vec2[4] = {m[1][2], m[0][2], m[0][2], m[0][2]}, Vec3[4] = {m[1][3], m[0][3], m[0][3], m[0][3]};
+    const float SignA[4] = {1.0f, -1.0f, 1.0f, -1.0f}, SignB[4] = {-1.0f, 1.0f, -1.0f, 1.0f};
+    float inv[4][4];
+    for (int i = 0; i < 4; ++i) {
+        inv[0][i] = ((Vec1[i] * Fac0[i] - Vec2[i] * Fac1[i]) + Vec3[i] * Fac2[i]) * SignA[i];
+        inv[1][i] = ((Vec0[i] * Fac0[i] - Vec2[i] * Fac3[i]) + Vec3[i] * Fac4[i]) * SignB[i];
+        inv[2][i] = ((Vec0[i] * Fac1[i] - Vec1[i] * Fac3[i]) + Vec3[i] * Fac5[i]) * SignA[i];
+        inv[3][i] = ((Vec0[i] * Fac2[i] - Vec1[i] * Fac4[i]) + Vec2[i] * Fac5[i]) * SignB[i];
+    }
+    float Dot0[4] = {m[0][0] * inv[0][0], m[0][1] * inv[1][0], m[0][2] * inv[2][0], m[0][3] * inv[3][0]};
+    float Dot1 = (Dot0[0] + Dot0[1]) + (Dot0[2] + Dot0[3]);
+    float OneOverDeterminant = 1.0f / Dot1;
+    for (int cc = 0; cc < 3; ++cc) for (int r = 0; r < 3; ++r) ti[3 * cc + r] = inv[r][cc] * OneOverDeterminant;
+}
+/* vec3(M * vec4(p, w)), glm's ((m0 x + m1 y) + (m2 z + m3 w)) */
+static v3 glm_m4v(const float* M, v3 p, float w) {
+    return V((M[0] * p.x + M[4] * p.y) + (M[8] * p.z + M[12] * w), (M[1] * p.x + M[5] * p.y) + (M[9] * p.z + M[13] * w),
+             (M[2] * p.x + M[6] * p.y) + (M[10] * p.z + M[14] * w));
+}
+/* mat3 * vec3, glm's (m[0] x + m[1] y) + m[2] z per row */
+static v3 glm_m3v(const float* A, v3 p) {
+    return V((A[0] * p.x + A[3] * p.y) + A[6] * p.z, (A[1] * p.x + A[4] * p.y) + A[7] * p.z,
+             (A[2] * p.x + A[5] * p.y) + A[8] * p.z);
+}
+
+/* Cylinder::Cylinder + computeBounds (Common/Cylinder.cpp:5-67, 306-336).  M:
+ * the node transform (glm::mat4, column-major) or NULL for world-space cones
+ * (then the matrix products are skipped: identity up to the sign of zeros).
+ * Frame and height from the PRE-transform points (Cylinder.cpp:17-25), frame
+ * mapped by mat3(transpose(inverse(M))) (:26-29), base/apex by M (:8-9). */
+static void cone_ctor(obj_t* o, v3 base_in, v3 apex_in, float r0, float r1, const float* M) {
     memset(o, 0, sizeof(*o));
     o->is_cone = 1;
+    v3 base = base_in, apex = apex_in;
+    if (M) { base = glm_m4v(M, base_in, 1.0f); apex = glm_m4v(M, apex_in, 1.0f); }
     o->base = base; o->apex = apex; o->r0 = r0; o->r1 = r1;
-    v3 v = vsub(apex, base);
+    v3 v = vsub(apex_in, base_in);
     o->height = length(v);
     v = normalize(v);
     v3 tmp = V(0.0f, 1.0f, 0.0f);
     if (1.0f - fabsf(dot(tmp, v)) < RAY_EPS) tmp = V(0.0f, 0.0f, 1.0f);
     v3 u = normalize(cross(v, tmp));
     v3 w = normalize(cross(u, v));
+    if (M) {
+        float ti[9];
+        glm_inverse_transpose3(M, ti);
+        u = glm_m3v(ti, u); v = glm_m3v(ti, v); w = glm_m3v(ti, w);
+    }
     o->u = normalize(u); o->v = normalize(v); o->w = normalize(w);
     o->slope = (r0 - r1) / o->height;
     o->base_d = dot(base, o->v);
@@ -364,8 +437,9 @@ static void cone_ctor(obj_t* o, v3 base, v3 apex, float r0, float r1) {
         if (P.z < o->bmin.z) o->bmin.z = P.z;
         if (P.z > o->bmax.z) o->bmax.z = P.z;
     }
-    /* m_centroid = basepoint + 0.4 * (apex - base)  (Cylinder.cpp:50) */
-    o->centroid = vadd(base, vscale(vsub(apex, base), 0.4f));
+    /* m_centroid = m_basepoint + 0.4 * (apexPoint - basePoint): transformed base,
+     * pre-transform axis (Cylinder.cpp:50) */
+    o->centroid = vadd(base, vscale(vsub(apex_in, base_in), 0.4f));
 }
 
 /* Intersection record (Common/Intersection.cpp:12-28) */
@@ -533,10 +607,20 @@ typedef struct {
     int32_t first, count;     /* leaf candidate range into object_ids; count 0 = interior */
 } node_t;
 
+typedef struct {
+    uint32_t w, h, ch, wrap;
+    uint8_t* data;
+} tex_t;
+
 struct ko_ctx {
     uint32_t n_obj, n_tris, n_cones;
     obj_t* obj;
     khp_material* mats; uint32_t n_mats;
+    /* textures (ABI 6): KIRK::Texture, per-material texture indices, environment map */
+    tex_t* tex; uint32_t n_tex;
+    khp_material_textures* mtex;   /* NULL: untextured */
+    khp_env_map env_map;
+    int textured;
     struct ko_light* lights; uint32_t n_lights;
     khp_environment env;
     khp_camera cam;
@@ -1197,6 +1281,111 @@ static v3 bsdf_sample(const shade_ctx_t* s, v3 in, v3 n, float sample[2], const 
 }
 
 /* ======================================================================= */
+/*  textures (ABI 6)                                                        */
+/* ======================================================================= */
+typedef struct { float r, g, b, a; } rgba_t;
+
+/* Texture::getColor (Texture.cpp:243-287).  The wrap `glm::pow(x - floor(x),
+ * m_texture_wrap_mode)` is std::pow on doubles (glm `using std::pow`; the mode
+ * is an unsigned char).  Out-of-image texel indices (infinite coordinates,
+ * undefined in KIRK) are clamped. */
+static rgba_t tex_get(const tex_t* t, float x, float y) {
+    rgba_t red = {1.0f, 0.0f, 0.0f, 1.0f};
+    if (isnan(x) || isnan(y)) return red;
+    float ux = x, uy = y;
+    if (ux > 1.0 || ux < 0.0) ux = (float)pow((double)(x - floorf(x)), (double)t->wrap);
+    if (uy > 1.0 || uy < 0.0) uy = (float)pow((double)(y - floorf(y)), (double)t->wrap);
+    int sx = (int)(ux * (int)(t->w - 1));
+    int sy = (int)(uy * (int)(t->h - 1));
+    if (sx < 0) sx = 0;
+    if (sx >= (int)t->w) sx = (int)t->w - 1;
+    if (sy < 0) sy = 0;
+    if (sy >= (int)t->h) sy = (int)t->h - 1;
+    const uint8_t* px = t->data + (size_t)t->ch * ((size_t)sy * t->w + (size_t)sx);
+    rgba_t c;
+    switch (t->ch) {
+    case 4: c.r = px[0] / 255.f; c.g = px[1] / 255.f; c.b = px[2] / 255.f; c.a = px[3] / 255.f; break;
+    case 3: c.r = px[0] / 255.f; c.g = px[1] / 255.f; c.b = px[2] / 255.f; c.a = 1.f; break;
+    case 2: c.r = c.g = c.b = px[0] / 255.f; c.a = px[1] / 255.f; break;
+    default: c.r = c.g = c.b = c.a = px[0] / 255.f; break;
+    }
+    return c;
+}
+
+/* calcTcoord: Cylinder.cpp:239-260, Triangle.cpp:250-254 (bary (1-u-v, u, v)). */
+static void obj_tcoord(const obj_t* o, const hit_t* h, v3 loc, float* tu, float* tv) {
+    if (o->is_cone) {
+        v3 Q = vsub(loc, o->base);
+        float u = dot(Q, o->u), v = dot(Q, o->v), w = dot(Q, o->w);
+        float r = o->r0 - o->slope * v;
+        float tmp = w / r;
+        if (tmp < -1.f) tmp = -1.f;
+        else if (tmp > 1.f) tmp = 1.f;
+        float phi = (u < 0) ? 2.0f * K_PIF - ko_acosf(tmp) : ko_acosf(tmp);
+        *tu = phi / 2.f / K_PIF;
+        *tv = v / o->height;
+    } else {
+        float bx = (1.0f - h->bu) - h->bv;
+        *tu = (bx * o->tc[0] + h->bu * o->tc[2]) + h->bv * o->tc[4];
+        *tv = (bx * o->tc[1] + h->bu * o->tc[3]) + h->bv * o->tc[5];
+    }
+}
+
+/* Material::getFromParam (Material.cpp:15-23): texel rgb for colours, glm::length
+ * of the rgba texel ((r r + g g) + (b b + a a)) for roughness. */
+static void material_at(const struct ko_ctx* c, uint32_t mi, float tu, float tv, khp_material* out) {
+    *out = c->mats[mi];
+    const khp_material_textures* mt = &c->mtex[mi];
+    int32_t ids[4] = {mt->diffuse, mt->specular, mt->volume, mt->emission};
+    float* dst[4] = {out->diffuse, out->specular, out->volume, out->emission};
+    for (int k = 0; k < 4; ++k) {
+        if (ids[k] < 0) continue;
+        rgba_t t = tex_get(&c->tex[ids[k]], tu, tv);
+        dst[k][0] = t.r; dst[k][1] = t.g; dst[k][2] = t.b;
+    }
+    if (mt->roughness >= 0) {
+        rgba_t t = tex_get(&c->tex[mt->roughness], tu, tv);
+        out->roughness = sqrtf((t.r * t.r + t.g * t.g) + (t.b * t.b + t.a * t.a));
+    }
+}
+
+static float glm_sign(float x) { return (float)((0.0f < x) - (x < 0.0f)); }
+
+/* Environment::getColor (Environment.cpp:91-133). */
+static v3 env_get(const struct ko_ctx* c, v3 ray_direction) {
+    if (c->env_map.type == KHP_ENV_COLOR) return ld3(c->env.color);
+    v3 direction = normalize(ray_direction);
+    rgba_t t;
+    if (c->env_map.type == KHP_ENV_CUBE_MAP) {
+        v3 signs = V(glm_sign(direction.x), glm_sign(direction.y), glm_sign(direction.z));
+        v3 absolutes = V(fabsf(direction.x), fabsf(direction.y), fabsf(direction.z));
+        float max = gmax(gmax(absolutes.x, absolutes.y), absolutes.z);
+        int side;
+        float uvx, uvy;
+        if (max == absolutes.x) {
+            side = (int)(0 + 1.5f - 1.5f * signs.x);
+            uvx = (direction.z / direction.x + 1) / 2;
+            uvy = (direction.y / absolutes.x + 1) / 2;
+        } else if (max == absolutes.y) {
+            side = (int)(1 + 1.5f - 1.5f * signs.y);
+            uvx = (direction.x / absolutes.y + 1) / 2;
+            uvy = (direction.z / direction.y + 1) / 2;
+        } else {
+            side = (int)(2 + 1.5f + 1.5f * signs.z);
+            uvx = -(direction.x / direction.z + 1) / 2;
+            uvy = (direction.y / absolutes.z + 1) / 2;
+        }
+        t = tex_get(&c->tex[c->env_map.tex[side]], uvx, uvy);
+    } else {
+        float m = (float)(2.0 * sqrt(direction.x * direction.x + direction.y * direction.y +
+                                     (direction.z + 1.0) * (direction.z + 1.0)));
+        float uvx = (float)(direction.x / m + 0.5), uvy = (float)(direction.y / m + 0.5);
+        t = tex_get(&c->tex[c->env_map.tex[0]], uvx, uvy);
+    }
+    return V(t.r, t.g, t.b);
+}
+
+/* ======================================================================= */
 /*  shaders + integrator                                                    */
 /* ======================================================================= */
 typedef struct {
@@ -1273,7 +1462,7 @@ static v3 trace_sample(const struct ko_ctx* c, const khp_render_params* p, uint3
         int light_hit = 0;
         if (t_lights < h.lambda) { h.lambda = t_lights; light_hit = 1; }
         if (h.lambda == FLT_MAX) {          /* EnvironmentShader::shade */
-            P.color = vadd(P.color, vmul(ld3(c->env.color), P.T));
+            P.color = vadd(P.color, vmul(env_get(c, P.ray.d), P.T));
             P.T = V(0.0f, 0.0f, 0.0f);
             continue;
         }
@@ -1285,6 +1474,13 @@ static v3 trace_sample(const struct ko_ctx* c, const khp_render_params* p, uint3
         }
         const obj_t* o = &c->obj[h.obj];
         const khp_material* m = &c->mats[o->mat];
+        khp_material mtx;
+        if (c->textured) {   /* traceRay: calcTcoord (CPU_PathTracer.cpp:178-179), then fetchParameter* */
+            float tu, tv;
+            obj_tcoord(o, &h, follow(&P.ray, h.lambda), &tu, &tv);
+            material_at(c, o->mat, tu, tv, &mtx);
+            m = &mtx;
+        }
 #ifdef KO_DEBUG
         if (getenv("KO_DEBUG") && (int)x == atoi(getenv("KO_DEBUG")) && (int)y == atoi(getenv("KO_DEBUGY")))
             fprintf(stderr, "s%u b%u obj %d cone %d lambda %g T %g %g %g C %g %g %g n %g %g %g d %g %g %g dn %g\n", sample, b, h.obj,
@@ -1360,7 +1556,8 @@ int ko_create(ko_ctx** out, const khp_scene* s) {
     for (uint32_t i = 0; i < s->n_tris; ++i) {
         const float* v = s->tri_v + 9 * (size_t)i;
         const float* n = s->tri_n + 9 * (size_t)i;
-        tri_ctor(&c->obj[i], ld3(v), ld3(v + 3), ld3(v + 6), ld3(n), ld3(n + 3), ld3(n + 6));
+        tri_ctor(&c->obj[i], ld3(v), ld3(v + 3), ld3(v + 6), ld3(n), ld3(n + 3), ld3(n + 6),
+                 s->tri_uv ? s->tri_uv + 6 * (size_t)i : NULL);
         c->obj[i].mat = s->tri_mat[i];
         /* Object::setU/V/W: the fiber's frame for fiberToTriangles fur (CPU_Scene.cpp:297-319),
          * zero for plain triangles (uninitialised glm::vec3 in KIRK) */
@@ -1373,7 +1570,13 @@ int ko_create(ko_ctx** out, const khp_scene* s) {
         const float* b = s->cone_base_r0 + 4 * (size_t)i;
         const float* a = s->cone_apex_r1 + 4 * (size_t)i;
         obj_t* o = &c->obj[s->n_tris + i];
-        cone_ctor(o, ld3(b), ld3(a), b[3], a[3]);
+        const float* M = NULL;
+        if (s->n_cone_models) {
+            uint32_t k = s->cone_model ? s->cone_model[i] : 0u;
+            if (k >= s->n_cone_models) { free(c->obj); free(c); return KHP_EINVAL; }
+            M = s->cone_models + 16 * (size_t)k;
+        }
+        cone_ctor(o, ld3(b), ld3(a), b[3], a[3], M);
         o->mat = s->cone_mat[i];
     }
     c->n_mats = s->n_materials;
@@ -1386,6 +1589,34 @@ int ko_create(ko_ctx** out, const khp_scene* s) {
     for (uint32_t i = 0; i < c->n_lights; ++i) light_init(&c->lights[i], &s->lights[i]);
     c->env = s->env;
     c->cam = s->camera;
+    c->env_map = s->env_map;
+    c->n_tex = s->n_textures;
+    c->tex = (tex_t*)calloc(c->n_tex ? c->n_tex : 1, sizeof(tex_t));
+    for (uint32_t i = 0; i < c->n_tex; ++i) {
+        const khp_texture* t = &s->textures[i];
+        size_t nb = (size_t)t->width * t->height * t->channels;
+        c->tex[i].w = t->width; c->tex[i].h = t->height; c->tex[i].ch = t->channels; c->tex[i].wrap = t->wrap_mode;
+        c->tex[i].data = (uint8_t*)malloc(nb ? nb : 1);
+        memcpy(c->tex[i].data, t->data, nb);
+        if (t->channels < 1 || t->channels > 4 || t->width == 0 || t->height == 0) { ko_destroy(c); return KHP_EINVAL; }
+    }
+    c->mtex = (khp_material_textures*)malloc(sizeof(khp_material_textures) * (c->n_mats ? c->n_mats : 1));
+    for (uint32_t i = 0; i < c->n_mats; ++i) {
+        khp_material_textures none = {-1, -1, -1, -1, -1};
+        c->mtex[i] = s->material_textures ? s->material_textures[i] : none;
+        const int32_t* k = &c->mtex[i].diffuse;
+        for (int j = 0; j < 5; ++j) {
+            if (k[j] >= (int32_t)c->n_tex || k[j] < -1) { ko_destroy(c); return KHP_EINVAL; }
+            if (k[j] >= 0) c->textured = 1;
+        }
+    }
+    if (c->env_map.type == KHP_ENV_CUBE_MAP || c->env_map.type == KHP_ENV_SPHERE_MAP) {
+        for (int j = 0; j < (c->env_map.type == KHP_ENV_CUBE_MAP ? 6 : 1); ++j)
+            if (c->env_map.tex[j] < 0 || c->env_map.tex[j] >= (int32_t)c->n_tex) { ko_destroy(c); return KHP_EINVAL; }
+    } else if (c->env_map.type != KHP_ENV_COLOR) {
+        ko_destroy(c);
+        return KHP_EINVAL;
+    }
     /* BVH::addBaseDataStructure (CPU_BVH.cpp:16-44) */
     c->ids = (uint32_t*)malloc(sizeof(uint32_t) * c->n_obj);
     box_t cb = box_empty();
@@ -1398,6 +1629,8 @@ int ko_create(ko_ctx** out, const khp_scene* s) {
 void ko_destroy(ko_ctx* c) {
     if (!c) return;
     free(c->obj); free(c->mats); free(c->lights); free(c->nodes); free(c->ids);
+    for (uint32_t i = 0; i < c->n_tex; ++i) free(c->tex[i].data);
+    free(c->tex); free(c->mtex);
     free(c);
 }
 
@@ -1501,6 +1734,17 @@ void ko_object_bounds(ko_ctx* c, float* o9) {
         d[3] = o->bmax.x; d[4] = o->bmax.y; d[5] = o->bmax.z;
         d[6] = o->centroid.x; d[7] = o->centroid.y; d[8] = o->centroid.z;
     }
+}
+
+/* Test hooks (ABI-6 KATs): Environment::getColor and Texture::getColor of the scene's textures. */
+void ko_env_color(ko_ctx* c, const float* dir, float* rgb) {
+    v3 e = env_get(c, ld3(dir));
+    rgb[0] = e.x; rgb[1] = e.y; rgb[2] = e.z;
+}
+
+void ko_tex_color(ko_ctx* c, uint32_t t, float x, float y, float* rgba) {
+    rgba_t v = tex_get(&c->tex[t], x, y);
+    rgba[0] = v.r; rgba[1] = v.g; rgba[2] = v.b; rgba[3] = v.a;
 }
 
 void ko_cone_records(ko_ctx* c, float* o18) {

@@ -64,6 +64,11 @@ void ko_tri_records(ko_ctx* c, float* out24, int32_t* lA);
 uint32_t ko_bvh_nodes(ko_ctx* c, float* out6, int32_t* first, int32_t* count, int32_t* object_ids);
 uint32_t ko_bvh_depth(ko_ctx* c);
 
+/* ABI-6 test hooks: Environment::getColor (dir: 3 floats -> rgb) and
+ * Texture::getColor of texture t of the scene (-> rgba). */
+void ko_env_color(ko_ctx* c, const float* dir, float* rgb);
+void ko_tex_color(ko_ctx* c, uint32_t t, float x, float y, float* rgba);
+
 /* Direct access to single functions for known-answer tests. */
 float ko_sinf(float x);
 float ko_cosf(float x);

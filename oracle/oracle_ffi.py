@@ -49,6 +49,8 @@ def load():
                                      P(c_float), P(c_uint64), P(c_uint64)]),
         "ko_trace_any": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_uint8)]),
         "ko_n_objects": (c_uint32, [c_void_p]),
+        "ko_env_color": (None, [c_void_p, P(c_float), P(c_float)]),
+        "ko_tex_color": (None, [c_void_p, c_uint32, c_float, c_float, P(c_float)]),
         "ko_object_bounds": (None, [c_void_p, P(c_float)]),
         "ko_cone_records": (None, [c_void_p, P(c_float)]),
         "ko_tri_records": (None, [c_void_p, P(c_float), P(c_int32)]),
@@ -134,6 +136,20 @@ class Oracle:
         hit = np.empty(len(o), np.uint8)
         self.lib.ko_trace_any(self.ptr, len(o), _fp(o), _fp(d), _fp(tm), hit.ctypes.data_as(POINTER(c_uint8)))
         return hit.astype(bool)
+
+    def env_color(self, direction):
+        """Environment::getColor for each direction (n, 3) -> (n, 3)."""
+        d = np.ascontiguousarray(direction, np.float32).reshape(-1, 3)
+        out = np.empty_like(d)
+        for i in range(len(d)):
+            self.lib.ko_env_color(self.ptr, _fp(d[i]), _fp(out[i]))
+        return out
+
+    def tex_color(self, tex, x, y):
+        """Texture::getColor of scene texture `tex` at (x, y) -> rgba."""
+        out = np.empty(4, np.float32)
+        self.lib.ko_tex_color(self.ptr, tex, x, y, _fp(out))
+        return out
 
     def object_bounds(self):
         n = self.lib.ko_n_objects(self.ptr)

@@ -25,6 +25,10 @@ CASES = [
     ("config3", dict(n_strands=20000), 96, 54, 4, 5),
     ("config5", dict(n_strands=5000, torus_grid=40, glass_subdiv=3), 96, 54, 4, 6),
     ("zoo", dict(n_strands=400), 96, 72, 4, 8),
+    ("transformed", dict(n_strands=1500), 64, 48, 4, 5),
+    ("transformed", dict(n_strands=1200, bsdf="DEonHairBSDF"), 48, 40, 3, 5),
+    ("textured", dict(n_strands=600, env="cube"), 80, 60, 4, 6),
+    ("textured", dict(n_strands=600, env="sphere"), 64, 48, 3, 6),
 ]
 
 
@@ -37,12 +41,35 @@ def _render_both(hip_ctx, sd, w, h, spp, depth, **kw):
 
 
 @pytest.mark.parametrize("name,kw,w,h,spp,depth", CASES,
-                         ids=[f"{c[0]}-{c[1].get('bsdf', '')}{c[1].get('n_strands', '')}" for c in CASES])
+                         ids=[f"{c[0]}-{c[1].get('bsdf', '')}{c[1].get('env', '')}{c[1].get('n_strands', '')}"
+                              for c in CASES])
 def test_frame_parity(hip_ctx, name, kw, w, h, spp, depth):
     sd = S.build_config(name, width=w, height=h, **kw)
     got, want = _render_both(hip_ctx, sd, w, h, spp, depth)
     r = assert_parity(got, want, exact=True)
     assert r["n_nonfinite"] < 0.05 * w * h
+
+
+@pytest.mark.parametrize("name,kw", [("transformed", dict(n_strands=1500)), ("textured", dict(n_strands=600))])
+def test_device_flatten_of_abi6_scenes(name, kw):
+    """khp_set_scene_device (geometry, texcoords and cone model indices in HBM,
+    flattened by flatten.hip) gives the frames of khp_set_scene and the oracle."""
+    sd = S.build_config(name, width=64, height=40, **kw)
+    want = oracle_ffi.Oracle(sd).render(64, 40, 3, 5, threads=16)
+    ctx = HipContext(0)
+    try:
+        ctx.set_scene_device(sd)
+        ctx.build_accel()
+        assert_parity(ctx.render(64, 40, 3, 5), want, exact=True)
+    finally:
+        ctx.close()
+    ctx = HipContext(0, host_build=True)
+    try:
+        ctx.set_scene(sd)
+        ctx.build_accel()
+        assert_parity(ctx.render(64, 40, 3, 5), want, exact=True)
+    finally:
+        ctx.close()
 
 
 def test_bvh_is_the_oracle_bvh(hip_ctx):
