@@ -78,19 +78,18 @@ __device__ __forceinline__ float4 tex_color(const DevScene& S, int32_t ti, float
 // Material::getFromParam (Material.cpp:15-23) for every parameter the path
 // tracer fetches: textured colours take the texel's rgb, textured roughness
 // the length of its rgba (glm::length(vec4): sqrt((x*x + y*y) + (z*z + w*w))).
+__device__ __forceinline__ void set_rgb(float* dst, float4 c) {
+    dst[0] = c.x;
+    dst[1] = c.y;
+    dst[2] = c.z;
+}
 __device__ __forceinline__ void resolve_material(const DevScene& S, uint32_t mat, float tu, float tv,
                                                  khp_material& m) {
-    m = S.mats[mat];
     const DevMatTex mt = S.mtex[mat];
-    float* cols[4] = {m.diffuse, m.specular, m.volume, m.emission};
-    for (int k = 0; k < 4; ++k) {
-        if (mt.t[k] >= 0) {
-            const float4 c = tex_color(S, mt.t[k], tu, tv);
-            cols[k][0] = c.x;
-            cols[k][1] = c.y;
-            cols[k][2] = c.z;
-        }
-    }
+    if (mt.t[MT_DIFFUSE] >= 0) set_rgb(m.diffuse, tex_color(S, mt.t[MT_DIFFUSE], tu, tv));
+    if (mt.t[MT_SPECULAR] >= 0) set_rgb(m.specular, tex_color(S, mt.t[MT_SPECULAR], tu, tv));
+    if (mt.t[MT_VOLUME] >= 0) set_rgb(m.volume, tex_color(S, mt.t[MT_VOLUME], tu, tv));
+    if (mt.t[MT_EMISSION] >= 0) set_rgb(m.emission, tex_color(S, mt.t[MT_EMISSION], tu, tv));
     if (mt.t[MT_ROUGHNESS] >= 0) {
         const float4 c = tex_color(S, mt.t[MT_ROUGHNESS], tu, tv);
         m.roughness = sqrtf((c.x * c.x + c.y * c.y) + (c.z * c.z + c.w * c.w));

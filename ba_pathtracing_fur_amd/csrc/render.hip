@@ -313,8 +313,8 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_extend(DevScene S, W
                 h.slot = -1;
                 h.u = h.v = 0.0f;
                 lf.left = 0;
-                has = trav2_begin<STATS>(S, tr, h.t, stk, mode, c, lf, st);
-                if (!has) {  // missed the root box
+                has = (STATS || !ray_has_nan(r)) && trav2_begin<STATS>(S, tr, h.t, stk, mode, c, lf, st);
+                if (!has) {  // missed the root box, or a NaN ray (no hit, see ray_has_nan)
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = -1;
                     Wv.hu[idx] = 0.0f;
@@ -353,6 +353,30 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_extend(DevScene S, W
     if (STATS)
         flush_stats(st, stk, wit, wbusy, &Wv.cnt->node_visits, &Wv.cnt->prim_tests, &Wv.cnt->pruned, &Wv.cnt->iters,
                     &Wv.cnt->lanes_busy, &Wv.cnt->spills);
+}
+
+// Hit texcoord (Cylinder::calcTcoord, Cylinder.cpp:239-260; Triangle::calcTcoord,
+// Triangle.cpp:250-254) and the material with its textured parameters resolved.
+// m holds the material's values on entry (resolve_material overwrites the textured ones).
+__device__ __forceinline__ void textured_material(const DevScene& S, const Aux& ax, const float4* pr, v3 loc,
+                                               const ShadeCtx& s, float bu, float bv, khp_material& out) {
+    float tu, tv;
+    if (ax.flags & 1u) {
+        const float4 c0 = pr[0];
+        const v3 Q = loc - mk(c0.x, c0.y, c0.z);
+        const float qu = dot(Q, s.U), qv = dot(Q, s.V), qw = dot(Q, s.W);
+        const float rr = c0.w - pr[1].w * qv;
+        const float tmp = gclamp(qw / rr, -1.0f, 1.0f);
+        const float phi = qu < 0.0f ? 2.0f * PIF - k_acosf(tmp) : k_acosf(tmp);
+        tu = phi / 2.0f / PIF;
+        tv = qv / S.cone_h[ax.obj - S.n_tris];
+    } else {
+        const float* tc = S.tri_uv + 6 * (size_t)ax.obj;
+        const float bx = (1.0f - bu) - bv;
+        tu = (bx * tc[0] + bu * tc[2]) + bv * tc[4];
+        tv = (bx * tc[1] + bu * tc[3]) + bv * tc[5];
+    }
+    resolve_material(S, ax.mat, tu, tv, out);
 }
 
 // ---- shade: traceRay light test + shaders (CPU_PathTracer.cpp:141-208; SimpleShader.h;
@@ -422,6 +446,9 @@ __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3,
     __syncthreads();  // sh is reused by the next iteration
 }
 
+// TEX: the scene has textured materials or an environment map (a separate
+// instantiation, so untextured scenes keep k_shade's registers).
+template <bool TEX>
 __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
     const uint32_t nf = Wv.cnt->nq[cur], n = nf + Wv.cnt->nqb[cur];
     const int nxt = cur ^ 1;
@@ -471,7 +498,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                 light_hit = true;
             }
             if (lambda == FLT_MAX_) {  // EnvironmentShader::shade
-                C = C + env_color(S, r.d) * T;
+                C = C + (TEX ? env_color(S, r.d) : mk(S.env.color[0], S.env.color[1], S.env.color[2])) * T;
                 T = mk(0, 0, 0);
             } else if (light_hit) {    // LightShader::shade
                 C = C + light_emit(S.lights[t_index], r.d) * T;
@@ -505,26 +532,12 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                 }
                 s.n = nrm;
                 v3 loc = follow(r, lambda);
+                // the material by value; textured scenes: calcTcoord (traceRay,
+                // CPU_PathTracer.cpp:178-179), then the textured parameters
                 khp_material mres;
-                if (S.textured) {  // calcTcoord (traceRay, CPU_PathTracer.cpp:178-179), then the textured parameters
-                    float tu, tv;
-                    if (ax.flags & 1u) {  // Cylinder::calcTcoord (Cylinder.cpp:239-260)
-                        const float4 c0 = pr[0];
-                        const v3 Q = loc - mk(c0.x, c0.y, c0.z);
-                        const float qu = dot(Q, s.U), qv = dot(Q, s.V), qw = dot(Q, s.W);
-                        const float rr = c0.w - pr[1].w * qv;
-                        const float tmp = gclamp(qw / rr, -1.0f, 1.0f);
-                        const float phi = qu < 0.0f ? 2.0f * PIF - k_acosf(tmp) : k_acosf(tmp);
-                        tu = phi / 2.0f / PIF;
-                        tv = qv / S.cone_h[ax.obj - S.n_tris];
-                    } else {              // Triangle::calcTcoord (Triangle.cpp:250-254)
-                        const float* tc = S.tri_uv + 6 * (size_t)ax.obj;
-                        const float bu = Wv.hu[i], bv = Wv.hv[i];
-                        const float bx = (1.0f - bu) - bv;
-                        tu = (bx * tc[0] + bu * tc[2]) + bv * tc[4];
-                        tv = (bx * tc[1] + bu * tc[3]) + bv * tc[5];
-                    }
-                    resolve_material(S, ax.mat, tu, tv, mres);
+                if (TEX) {
+                    mres = S.mats[ax.mat];
+                    textured_material(S, ax, pr, loc, s, Wv.hu[i], Wv.hv[i], mres);
                     s.m = &mres;
                 }
                 const khp_material* m = s.m;
@@ -717,8 +730,13 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, W
                 tmax = a.w;
                 trav_setup(tr, r);
                 lf.left = 0;
-                has = trav2_begin<STATS>(S, tr, tmax, stk, mode, c, lf, st);
-                if (!has) Wv.vis[idx] = 0;
+                if (!STATS && tr.inv.x != tr.inv.x) {  // NaN x direction: occluded iff a triangle exists (ray_has_nan)
+                    has = false;
+                    Wv.vis[idx] = S.n_tris > 0 ? 1 : 0;
+                } else {
+                    has = trav2_begin<STATS>(S, tr, tmax, stk, mode, c, lf, st);
+                    if (!has) Wv.vis[idx] = 0;
+                }
             }
         }
         unsigned long long act = __ballot(has);
@@ -1406,7 +1424,8 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, TRAV_BLOCK, LDS_BYTES));
     c->grid_sh = std::max(1, nb) * c->n_cu;
     nb = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade, 256, 0));
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade<true>, 256, 0));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade<false>, 256, 0));
     c->grid_shade = std::max(1, nb) * c->n_cu;
     c->built = true;
     return KHP_OK;
@@ -1854,7 +1873,10 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 timed(c, f, 0, false, sA);
                 if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
                 timed(c, f, 1, true, sA);
-                hipLaunchKernelGGL(k_shade, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                if (c->S.textured)
+                    hipLaunchKernelGGL(k_shade<true>, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                else
+                    hipLaunchKernelGGL(k_shade<false>, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
                 timed(c, f, 1, false, sA);
                 if (sB != sA) {
                     hipEvent_t shaded = slot_event(f.sync_pool, f.sync_next, true);

@@ -30,13 +30,34 @@ struct TravStats {
 struct TravRay {
     Ray r;
     v3 inv;
-    bool fin;  // all three inverse direction components are finite (fast slab test is exact)
+    bool fin;  // origin and inverse direction finite on every axis (the fast slab test is exact)
 };
 
 __device__ __forceinline__ void trav_setup(TravRay& tr, const Ray& r) {
     tr.r = r;
     tr.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    tr.fin = __builtin_isfinite(tr.inv.x) && __builtin_isfinite(tr.inv.y) && __builtin_isfinite(tr.inv.z);
+    tr.fin = __builtin_isfinite(tr.inv.x) && __builtin_isfinite(tr.inv.y) && __builtin_isfinite(tr.inv.z) &&
+             __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
+}
+
+// NaN rays (a BSDF can return a NaN direction, e.g. at KIRK's grazing-angle
+// divisions; KIRK traces them like any other ray, CPU_PathTracer.cpp:172).
+// Their results follow from IEEE comparisons alone, without the traversal:
+//  * closest hit: every cone test fails (its quadratic is NaN, so no
+//    accept comparison holds) and every triangle test that passes returns
+//    t = NaN, which never satisfies the leaf's `tl < hit.t` -- so a ray with
+//    a NaN in its origin or direction ends with no hit;
+//  * any hit, NaN x direction (inv.x NaN): every slab returns true with
+//    t0 = t1 = NaN (the x entry/exit stay NaN, no later comparison replaces or
+//    rejects them), nothing is pruned, cones fail, and every triangle passes
+//    (det NaN -> u, v, t NaN, no rejecting comparison holds) -- so the ray is
+//    occluded iff the scene has a triangle.
+// KIRK walks the whole BVH for such a ray (about 20M records at config 5:
+// seconds per launch).  The instrumented kernels keep the walk, so KIRK's
+// visit counts stay exact there.
+__device__ __forceinline__ bool ray_has_nan(const Ray& r) {
+    return r.o.x != r.o.x || r.o.y != r.o.y || r.o.z != r.o.z || r.d.x != r.d.x || r.d.y != r.d.y ||
+           r.d.z != r.d.z;
 }
 
 __device__ __forceinline__ bool ref_leaf(uint32_t r) { return (r & LEAF_BIT) != 0u; }

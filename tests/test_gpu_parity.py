@@ -240,6 +240,44 @@ def test_full_size_scene_sampled_rows(hip_ctx):
     assert_parity(got[rows], want[rows], exact=True)
 
 
+def test_config1_full_frame(hip_ctx):
+    """BASELINE config 1 at its stated size: Cornell box + Lambert icosphere, 256x256, 4 spp, every pixel."""
+    sd = S.config1(256, 256)
+    got, want = _render_both(hip_ctx, sd, 256, 256, 4, 5)
+    assert_parity(got, want, exact=True)
+
+
+def test_config2_full_size_sampled_rows(hip_ctx):
+    """BASELINE config 2 at its stated size: 10k-strand hairball in the Cornell
+    box, 1920x1080, 8 spp; every 24th row against the oracle."""
+    sd = S.config2(1920, 1080, n_strands=10_000)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    got = hip_ctx.render(1920, 1080, 8, 5)
+    rows = list(range(5, 1080, 24))
+    want = oracle_ffi.Oracle(sd).render(1920, 1080, 8, 5, threads=16, rows=(5, 1080, 24))
+    assert_parity(got[rows], want[rows], exact=True)
+
+
+def test_config5_full_size_sampled_rows():
+    """BASELINE config 5 at its stated size: 1M strands (9M cones, generated in
+    HBM) + 500x500x2-triangle torus + subdiv-5 glass icosphere at 3840x2160;
+    2 spp (the path is per-sample independent, so 32 spp is 16 such passes),
+    every 216th row against the oracle on the host-generated scene."""
+    ctx = HipContext(0)
+    try:
+        S.config5_device(ctx, 3840, 2160, n_strands=1_000_000)
+        ctx.build_accel()
+        assert ctx.stats()["n_objects"] == 500 * 500 * 2 + 20 * 4 ** 5 + 2 + 9_000_000
+        got = ctx.render(3840, 2160, 2, 5)
+    finally:
+        ctx.close()
+    host = S.config5(3840, 2160, n_strands=1_000_000)
+    rows = list(range(11, 2160, 216))
+    want = oracle_ffi.Oracle(host).render(3840, 2160, 2, 5, threads=16, rows=(11, 2160, 216))
+    assert_parity(got[rows], want[rows], exact=True)
+
+
 def test_errors_are_loud():
     ctx = HipContext(0)
     with pytest.raises(N.KhpError) as e:
@@ -432,6 +470,12 @@ def test_production_traversal_kernels_ray_by_ray(hip_ctx, mode, name, kw):
     d = rng.normal(size=(n, 3)).astype(np.float32)
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     tmax = rng.uniform(0.01, 2.0, n).astype(np.float32)
+    # NaN rays (KIRK traces them; the production kernels answer them without the walk, ray_has_nan)
+    d[:40] = np.nan
+    d[40:60, 0] = np.nan
+    d[60:80, 1] = np.nan
+    orig[80:100, 2] = np.nan
+    orig[100:120] = np.nan
     t0, obj0, uv0, nodes, prims = o.trace_closest(orig, d)
     any0 = o.trace_any(orig, d, tmax)
     old = hip_ctx.set_params(trace_kernels=int(mode))

@@ -1,0 +1,55 @@
+"""The multi-GPU path with real ranks: one process per GPU, tiles t % N, the RCCL
+framebuffer gather (khp_gather_framebuffer: k_pack -> ncclSend/ncclRecv ->
+k_unpack) and bench.py --gpus N launching its own ranks.  Needs >= 2 GPUs on
+one node; skipped (not failed) on a single-GPU box, where tests/test_multirank.py
+covers the sharding logic on gloo and test_gpu_parity.py every rank's tile set."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_ffi
+from _util import assert_parity
+from ba_pathtracing_fur_amd import scenes as S
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _n_gpus() -> int:
+    import torch
+    return torch.cuda.device_count()   # counts devices without initialising HIP
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rccl_gather_assembles_the_single_gpu_frame(tmp_path, world):
+    if _n_gpus() < world:
+        pytest.skip(f"needs {world} GPUs, this box has {_n_gpus()}")
+    W, H = 96, 64
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "_rccl_gather_worker.py"),
+           str(tmp_path), str(W), str(H)]
+    subprocess.run(cmd, check=True, timeout=240)
+    got = np.load(tmp_path / "frame.npy")
+    want = oracle_ffi.Oracle(S.config2(W, H, n_strands=1500)).render(W, H, 6, 5, threads=16)
+    assert_parity(got, want, exact=True)
+
+
+def test_bench_launches_its_own_ranks():
+    if _n_gpus() < 2:
+        pytest.skip(f"needs 2 GPUs, this box has {_n_gpus()}")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "1", "--steps",
+                          "4", "--warmup", "2", "--sync-check-steps", "1", "--no-cpu-baseline"], check=True,
+                         timeout=300, capture_output=True, text=True).stdout
+    line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
