@@ -199,6 +199,125 @@ KHD double k_j0(double x) {
 
 KHD float k_hypotf(float x, float y) { return sqrtf(x * x + y * y); }
 
+// ---- double log / exp / pow (the output stage's libm calls: Tonemapping.cpp) ----
+// Plain IEEE double arithmetic (no FMA contraction), identical on host, device
+// and in oracle/ (ko_log_d / ko_exp_d / ko_pow_d), within ~1 ulp of the
+// correctly rounded value (tests/test_kmath.py).
+KHD double d_from_bits(uint64_t u) {
+    union { uint64_t u; double d; } c;
+    c.u = u;
+    return c.d;
+}
+KHD uint64_t bits_from_d(double d) {
+    union { double d; uint64_t u; } c;
+    c.d = d;
+    return c.u;
+}
+constexpr double LN2_HI_D = 6.93147180369123816490e-01;  // ln 2, high part (trailing zeros: k*LN2_HI exact)
+constexpr double LN2_LO_D = 1.90821492927058770002e-10;
+constexpr double INV_LN2_D = 1.44269504088896338700e+00;
+
+// log x: x = m 2^e, m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s), s = (m-1)/(m+1).
+KHD double k_log_d(double x) {
+    if (!(x > 0.0)) return x == 0.0 ? -d_from_bits(0x7ff0000000000000ull) : d_from_bits(0x7ff8000000000000ull);
+    if (x == d_from_bits(0x7ff0000000000000ull)) return x;
+    int e = 0;
+    if (x < 2.2250738585072014e-308) {  // subnormal
+        x = x * 18014398509481984.0;    // 2^54
+        e = -54;
+    }
+    uint64_t b = bits_from_d(x);
+    e += (int)((b >> 52) & 0x7ffu) - 1023;
+    double m = d_from_bits((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+    if (m > 1.41421356237309504880) {
+        m = m * 0.5;
+        e += 1;
+    }
+    const double f = m - 1.0, s = f / (m + 1.0), z = s * s;
+    double p = 1.0 / 25.0;
+    p = p * z + 1.0 / 23.0;
+    p = p * z + 1.0 / 21.0;
+    p = p * z + 1.0 / 19.0;
+    p = p * z + 1.0 / 17.0;
+    p = p * z + 1.0 / 15.0;
+    p = p * z + 1.0 / 13.0;
+    p = p * z + 1.0 / 11.0;
+    p = p * z + 1.0 / 9.0;
+    p = p * z + 1.0 / 7.0;
+    p = p * z + 1.0 / 5.0;
+    p = p * z + 1.0 / 3.0;
+    const double lm = 2.0 * s + (2.0 * s) * (z * p);
+    const double de = (double)e;
+    return de * LN2_HI_D + (de * LN2_LO_D + lm);
+}
+
+// exp x: x = k ln2 + r, |r| <= ln2/2, Taylor series of e^r to r^14, times 2^k.
+KHD double k_exp_d(double x) {
+    if (x != x) return x;
+    if (x > 709.782712893384) return d_from_bits(0x7ff0000000000000ull);
+    if (x < -745.2) return 0.0;
+    const double kd = (double)(int64_t)((x * INV_LN2_D) + (x < 0.0 ? -0.5 : 0.5));
+    const int k = (int)kd;
+    const double r = (x - kd * LN2_HI_D) - kd * LN2_LO_D;
+    double p = 1.0 / 87178291200.0;          // 1/14!
+    p = p * r + 1.0 / 6227020800.0;          // 1/13!
+    p = p * r + 1.0 / 479001600.0;
+    p = p * r + 1.0 / 39916800.0;
+    p = p * r + 1.0 / 3628800.0;
+    p = p * r + 1.0 / 362880.0;
+    p = p * r + 1.0 / 40320.0;
+    p = p * r + 1.0 / 5040.0;
+    p = p * r + 1.0 / 720.0;
+    p = p * r + 1.0 / 120.0;
+    p = p * r + 1.0 / 24.0;
+    p = p * r + 1.0 / 6.0;
+    p = p * r + 0.5;
+    p = p * r + 1.0;
+    p = p * r + 1.0;
+    if (k < -1021) return (p * d_from_bits((uint64_t)(k + 1023 + 54) << 52)) * (1.0 / 18014398509481984.0);
+    if (k > 1023) return (p * 2.0) * d_from_bits((uint64_t)(k - 1 + 1023) << 52);
+    return p * d_from_bits((uint64_t)(k + 1023) << 52);
+}
+
+// pow with C99 Annex F special cases; finite positive x: exp(y log x).
+KHD bool k_is_int_d(double y) { return y == (double)(int64_t)y || (y > 9007199254740992.0 || y < -9007199254740992.0); }
+KHD bool k_is_odd_d(double y) {
+    if (y > 9007199254740992.0 || y < -9007199254740992.0) return false;
+    const int64_t i = (int64_t)y;
+    return (double)i == y && (i & 1);
+}
+KHD double k_pow_d(double x, double y) {
+    const double INF = d_from_bits(0x7ff0000000000000ull), NAN_ = d_from_bits(0x7ff8000000000000ull);
+    if (y == 0.0) return 1.0;
+    if (x == 1.0) return 1.0;
+    if (x != x || y != y) return NAN_;
+    const double ax = x < 0.0 ? -x : x;
+    if (y == INF || y == -INF) {
+        if (ax == 1.0) return 1.0;
+        return ((ax > 1.0) == (y > 0.0)) ? INF : 0.0;
+    }
+    const bool odd = k_is_odd_d(y);
+    if (x == 0.0) {
+        const bool neg = bits_from_d(x) >> 63;
+        if (y < 0.0) return (odd && neg) ? -INF : INF;
+        return (odd && neg) ? x : 0.0;
+    }
+    if (ax == INF) {
+        if (x > 0.0) return y < 0.0 ? 0.0 : INF;
+        if (y < 0.0) return odd ? -0.0 : 0.0;
+        return odd ? -INF : INF;
+    }
+    if (x < 0.0) {
+        if (!k_is_int_d(y)) return NAN_;
+        const double r = k_exp_d(y * k_log_d(ax));
+        return odd ? -r : r;
+    }
+    return k_exp_d(y * k_log_d(x));
+}
+// float overloads as the C++ <cmath> calls std::log(float) / std::pow(float, float)
+KHD float k_logf_d(float x) { return (float)k_log_d((double)x); }
+KHD float k_powf_d(float x, float y) { return (float)k_pow_d((double)x, (double)y); }
+
 // ---- counter RNG (DESIGN.md "RNG") ----------------------------------------
 KHD uint32_t lowbias32(uint32_t x) {
     x ^= x >> 16;

@@ -814,16 +814,17 @@ __global__ void k_rgba8(const float* fb, uint32_t n, uint8_t* out) {
     reinterpret_cast<uchar4*>(out)[i] = o;
 }
 
-// Tonemapper::RGB_to_Yxy (Tonemapping.cpp): per pixel Yxy, the max luminance
-// (glm::max, NaN-ignoring) and the log-luminance sum.  KIRK accumulates the
-// sum sequentially in float; this sums in double in parallel (stated tolerance
-// in tests/test_output.py).
+// Tonemapper::RGB_to_Yxy (Tonemapping.cpp:66-91): per pixel Yxy, the max
+// luminance (glm::max, NaN-ignoring: order-independent, reduced per block) and
+// the pixel's log-luminance term log(2.3e-5 + Y) (k_log_d, the documented
+// replacement of the CRT log).  KIRK's sum of those terms is a sequential
+// float running sum (`float sum; sum += log(...)`), which no reordering
+// reproduces, so the host adds the terms in pixel order.
 __device__ __forceinline__ float gdot3(float a0, float a1, float a2, float b0, float b1, float b2) {
     return (a0 * b0 + a1 * b1) + a2 * b2;  // glm::dot operand order
 }
-__global__ __launch_bounds__(256) void k_tm_yxy(const float* fb, uint32_t n, float* yxy, float* bmax, double* bsum) {
+__global__ __launch_bounds__(256) void k_tm_yxy(const float* fb, uint32_t n, float* yxy, float* bmax, double* lgv) {
     __shared__ float smax[256];
-    __shared__ double ssum[256];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     float Y = 0.0f, xx = 0.0f, yy = 0.0f, mx = 1e-06f;
     double lg = 0.0;
@@ -839,48 +840,38 @@ __global__ __launch_bounds__(256) void k_tm_yxy(const float* fb, uint32_t n, flo
             yy = Yv / W;
         }
         mx = (mx < Y) ? Y : mx;
-        lg = log(2.3e-5 + (double)Y);
+        lg = k_log_d(2.3e-5 + (double)Y);
+        lgv[i] = lg;
         yxy[3 * (size_t)i] = Y;
         yxy[3 * (size_t)i + 1] = xx;
         yxy[3 * (size_t)i + 2] = yy;
     }
+    (void)lg;
     smax[threadIdx.x] = mx;
-    ssum[threadIdx.x] = lg;
     __syncthreads();
     for (uint32_t w = 128; w > 0; w >>= 1) {
         if (threadIdx.x < w) {
             const float o = smax[threadIdx.x + w];
             smax[threadIdx.x] = (smax[threadIdx.x] < o) ? o : smax[threadIdx.x];
-            ssum[threadIdx.x] += ssum[threadIdx.x + w];
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        bmax[blockIdx.x] = smax[0];
-        bsum[blockIdx.x] = ssum[0];
-    }
+    if (threadIdx.x == 0) bmax[blockIdx.x] = smax[0];
 }
 
-// Tonemapper::luminance_from_center (Tonemapping.cpp:183-245): the log-sum of
-// the Gaussian-weighted window, with the reference's i1 = x*(y_start+ks)+y
-// indexing.  mask (ks*ks doubles) and `mean` are built on the host.
+// Tonemapper::luminance_from_center (Tonemapping.cpp:183-245): the log terms
+// of the Gaussian-weighted window, with the reference's i1 = x*(y_start+ks)+y
+// indexing, in KIRK's loop order (t = i * ks + j); the host adds them in that
+// order (a sequential double sum).  mask (ks*ks doubles) and `mean` are built
+// on the host.
 __global__ __launch_bounds__(256) void k_tm_center(const float* yxy, int ks, int xs, int ys, const double* mask,
-                                                   double mean, double* bsum) {
-    __shared__ double ssum[256];
+                                                   double mean, double* terms) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    double lg = 0.0;
     if (t < ks * ks) {
         const int i = t / ks, j = t % ks;
         const int i1 = (xs + i) * (ys + ks) + (ys + j);
-        lg = log(2.3e-5 + (double)yxy[3 * (size_t)i1] * mask[j * ks + i] * mean);
+        terms[t] = k_log_d(2.3e-5 + (double)yxy[3 * (size_t)i1] * mask[j * ks + i] * mean);
     }
-    ssum[threadIdx.x] = lg;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) ssum[threadIdx.x] += ssum[threadIdx.x + w];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) bsum[blockIdx.x] = ssum[0];
 }
 
 struct TmScalars {
@@ -895,12 +886,12 @@ __global__ __launch_bounds__(256) void k_tm_map(const float* yxy, uint32_t n, Tm
     if (i >= n) return;
     float v = yxy[3 * (size_t)i];
     const float xc = yxy[3 * (size_t)i + 1], yc = yxy[3 * (size_t)i + 2];
-    if (t.contrast_on) v = powf(v, t.contP);
+    if (t.contrast_on) v = k_powf_d(v, t.contP);
     v /= t.av_lum;
     v *= t.exposure;
-    const float bias = (float)pow((double)(v / t.Lmax), (double)t.biasP);
-    const float interpol = logf(2.0f + bias * 8.0f);
-    v = logf(v + 1.0f) / interpol / t.divider;
+    const float bias = (float)k_pow_d((double)(v / t.Lmax), (double)t.biasP);
+    const float interpol = k_logf_d(2.0f + bias * 8.0f);
+    v = k_logf_d(v + 1.0f) / interpol / t.divider;
     const float eps = 1e-06f;
     float X, Z;
     if (v > eps && xc > eps && yc > eps) {
@@ -914,8 +905,8 @@ __global__ __launch_bounds__(256) void k_tm_map(const float* yxy, uint32_t n, Tm
     for (int k = 0; k < 3; ++k) {
         float c = rgb[k];
         if (t.gamma_on) {
-            if (t.rec) c = c <= t.start ? c * t.slope : (float)(1.099 * (double)powf(c, t.inv_gamma) - 0.099);
-            else c = powf(c, t.inv_gamma);
+            if (t.rec) c = c <= t.start ? c * t.slope : (float)(1.099 * (double)k_powf_d(c, t.inv_gamma) - 0.099);
+            else c = k_powf_d(c, t.inv_gamma);
         }
         if (t.clamp_on) {
             c = (c < t.black) ? t.black : c;  // glm::clamp = min(max(x, lo), hi)
@@ -1075,6 +1066,7 @@ struct khp_ctx {
     DevMem fb, pix, stage, stage_pix, snap;   // snap: per-bounce Counters snapshots (stats renders)
     int cur_bounce = -1;
     std::vector<float> dump;   // prm.dump_bounce: SoA o.xyz, d.xyz of one bounce's extension queue
+    std::vector<float> dump_sh;  // prm.dump_bounce: that bounce's shadow rays, o.xyz d.xyz t_max each
     uint32_t fbW = 0, fbH = 0;
     std::vector<uint32_t> pix_host;
     uint32_t pix_key[5] = {0, 0, 0, 0, 0};
@@ -1854,14 +1846,18 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 Wb.sh = w.shb[cur].as<float4>();
                 Wb.vis = w.visb[cur].as<uint8_t>();
                 Wb.shq = w.shqb.as<ShadowQ>() + cur;
-                if (dump_b == (int)b && p0 == 0 && s0 == 0) {
-                    uint32_t nq = 0;
-                    HIPCHK(hipMemcpyAsync(&nq, &Wv.cnt->nq[cur], 4, hipMemcpyDeviceToHost, sA));
+                if (dump_b == (int)b && p0 == 0 && s0 == 0) {  // extension queue: front part, then back part
+                    uint32_t nq[2] = {0, 0};
+                    HIPCHK(hipMemcpyAsync(&nq[0], &Wv.cnt->nq[cur], 4, hipMemcpyDeviceToHost, sA));
+                    HIPCHK(hipMemcpyAsync(&nq[1], &Wv.cnt->nqb[cur], 4, hipMemcpyDeviceToHost, sA));
                     HIPCHK(hipStreamSynchronize(sA));
-                    c->dump.resize(6 * (size_t)nq);
-                    for (int q = 0; q < 3; ++q) {
-                        HIPCHK(hipMemcpy(c->dump.data() + (size_t)q * nq, Wv.qo[cur][q], 4 * (size_t)nq, hipMemcpyDeviceToHost));
-                        HIPCHK(hipMemcpy(c->dump.data() + (size_t)(3 + q) * nq, Wv.qd[cur][q], 4 * (size_t)nq, hipMemcpyDeviceToHost));
+                    const size_t m = (size_t)nq[0] + nq[1];
+                    c->dump.resize(6 * m);
+                    for (int q = 0; q < 6; ++q) {
+                        const float* col = q < 3 ? Wv.qo[cur][q] : Wv.qd[cur][q - 3];
+                        float* dst = c->dump.data() + (size_t)q * m;
+                        HIPCHK(hipMemcpy(dst, col, 4 * (size_t)nq[0], hipMemcpyDeviceToHost));
+                        HIPCHK(hipMemcpy(dst + nq[0], col + (Wv.cap - nq[1]), 4 * (size_t)nq[1], hipMemcpyDeviceToHost));
                     }
                 }
                 hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
@@ -1882,6 +1878,23 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     hipEvent_t shaded = slot_event(f.sync_pool, f.sync_next, true);
                     HIPCHK(hipEventRecord(shaded, sA));
                     HIPCHK(hipStreamWaitEvent(sB, shaded, 0));
+                }
+                if (dump_b == (int)b && p0 == 0 && s0 == 0) {  // this bounce's shadow rays: o, d, t_max
+                    HIPCHK(hipStreamSynchronize(sA));
+                    ShadowQ hq;
+                    HIPCHK(hipMemcpy(&hq, Wb.shq, sizeof(ShadowQ), hipMemcpyDeviceToHost));
+                    std::vector<float4> rec(6 * ((size_t)hq.nsh + hq.nshb));
+                    if (hq.nsh)
+                        HIPCHK(hipMemcpy(rec.data(), Wb.sh, 6 * sizeof(float4) * hq.nsh, hipMemcpyDeviceToHost));
+                    if (hq.nshb)
+                        HIPCHK(hipMemcpy(rec.data() + 6 * (size_t)hq.nsh, Wb.sh + 6 * (Wv.cap - hq.nshb),
+                                         6 * sizeof(float4) * hq.nshb, hipMemcpyDeviceToHost));
+                    c->dump_sh.resize(7 * ((size_t)hq.nsh + hq.nshb));
+                    for (size_t k = 0; k < (size_t)hq.nsh + hq.nshb; ++k) {
+                        const float4 a = rec[6 * k], d = rec[6 * k + 1];
+                        const float v[7] = {a.x, a.y, a.z, d.x, d.y, d.z, a.w};
+                        memcpy(c->dump_sh.data() + 7 * k, v, sizeof(v));
+                    }
                 }
                 timed(c, f, 2, true, sB);
                 if (stats)
@@ -2116,29 +2129,27 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
     HIPCHK(hipSetDevice(c->device));
     const uint32_t n = c->fbW * c->fbH;
     const uint32_t nb = (n + 255) / 256;
-    DevMem out, yxy, bmax, bsum;
+    DevMem out, yxy, bmax, lgv;
     HIPCHK(out.ensure(4 * (size_t)n));
     if (!tm) {
         hipLaunchKernelGGL(k_rgba8, dim3(nb), dim3(256), 0, c->stream, c->fb.as<float>(), n, out.as<uint8_t>());
     } else {
         HIPCHK(yxy.ensure(12 * (size_t)n));
         HIPCHK(bmax.ensure(4 * (size_t)nb));
-        HIPCHK(bsum.ensure(8 * (size_t)nb));
+        HIPCHK(lgv.ensure(8 * (size_t)n));
         hipLaunchKernelGGL(k_tm_yxy, dim3(nb), dim3(256), 0, c->stream, c->fb.as<float>(), n, yxy.as<float>(),
-                           bmax.as<float>(), bsum.as<double>());
+                           bmax.as<float>(), lgv.as<double>());
         std::vector<float> hm(nb);
-        std::vector<double> hs(nb);
+        std::vector<double> hl(n);
         HIPCHK(hipMemcpyAsync(hm.data(), bmax.p, 4 * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(hs.data(), bsum.p, 8 * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(hl.data(), lgv.p, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         float mx = 1e-06f;
-        double sum = 0.0;
-        for (uint32_t b = 0; b < nb; ++b) {
-            mx = (mx < hm[b]) ? hm[b] : mx;
-            sum += hs[b];
-        }
+        for (uint32_t b = 0; b < nb; ++b) mx = (mx < hm[b]) ? hm[b] : mx;
+        float sum = 0.0f;  // RGB_to_Yxy's float running sum, in pixel order
+        for (uint32_t k = 0; k < n; ++k) sum = (float)((double)sum + hl[k]);
         // Tonemapper::map / tonemapping scalars, in KIRK's float/double mix
-        float world_lum = (float)sum / (float)n;
+        float world_lum = sum / (float)n;
         if (tm->center_weight) {
             // window and mask on the host, as Tonemapping.cpp:186-236 builds them
             const int width = (int)c->fbW, height = (int)c->fbH;
@@ -2163,16 +2174,16 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
             for (double m : mask) acc += m;
             const double mean = (double)(ks * ks) / acc;
             const uint32_t nbc = (uint32_t)(ks * ks + 255) / 256;
-            DevMem dmask, csum;
+            DevMem dmask, cterm;
             HIPCHK(dmask.ensure(mask.size() * 8));
-            HIPCHK(csum.ensure(8 * (size_t)nbc));
+            HIPCHK(cterm.ensure(8 * (size_t)ks * ks));
             HIPCHK(hipMemcpyAsync(dmask.p, mask.data(), mask.size() * 8, hipMemcpyHostToDevice, c->stream));
             hipLaunchKernelGGL(k_tm_center, dim3(nbc), dim3(256), 0, c->stream, yxy.as<float>(), ks, xs, ys,
-                               dmask.as<double>(), mean, csum.as<double>());
-            std::vector<double> hc(nbc);
-            HIPCHK(hipMemcpyAsync(hc.data(), csum.p, 8 * (size_t)nbc, hipMemcpyDeviceToHost, c->stream));
+                               dmask.as<double>(), mean, cterm.as<double>());
+            std::vector<double> hc((size_t)ks * ks);
+            HIPCHK(hipMemcpyAsync(hc.data(), cterm.p, 8 * hc.size(), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
-            double cs = 0.0;
+            double cs = 0.0;  // luminance_from_center's double running sum, in its loop order
             for (double v : hc) cs += v;
             world_lum = (float)(cs / (ks * ks));
         }
@@ -2262,6 +2273,27 @@ extern "C" khp_status khp_read_layout(khp_ctx* c, uint32_t* n_records, uint32_t*
     if (prim_aux && c->n_slots)
         HIPCHK(hipMemcpyAsync(prim_aux, c->aux.p, sizeof(Aux) * (size_t)c->n_slots, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_debug_shadow_queue(khp_ctx* c, uint32_t* n, float* orig, float* dir, float* tmax) {
+    if (c) {  // complete asynchronous frames first
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+    }
+    if (!c || !n) return fail(KHP_EINVAL, "null argument");
+    const uint32_t m = (uint32_t)(c->dump_sh.size() / 7);
+    if (orig && dir && tmax) {
+        for (uint32_t i = 0; i < m && i < *n; ++i) {
+            const float* v = c->dump_sh.data() + 7 * (size_t)i;
+            for (int k = 0; k < 3; ++k) {
+                orig[3 * (size_t)i + k] = v[k];
+                dir[3 * (size_t)i + k] = v[3 + k];
+            }
+            tmax[i] = v[6];
+        }
+    }
+    *n = m;
     return KHP_OK;
 }
 

@@ -152,7 +152,7 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_read_rgba8", "khp_tonemap_defaults", "khp_read_bvh",
             "khp_read_layout", "khp_set_scene_device", "khp_gen_hairball_device", "khp_device_alloc",
             "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device",
-            "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params"]
+            "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params", "khp_debug_shadow_queue"]
 
 _lib = None
 
@@ -220,6 +220,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_gen_icosphere": (c_int, [c_uint32, P(c_float), c_float, P(c_float), P(c_float)]),
         "khp_gen_torus": (c_int, [c_uint32, c_uint32, P(c_float), c_float, c_float, P(c_float), P(c_float)]),
         "khp_debug_queue": (c_int, [c_void_p, P(c_uint32), P(c_float), P(c_float)]),
+        "khp_debug_shadow_queue": (c_int, [c_void_p, P(c_uint32), P(c_float), P(c_float), P(c_float)]),
         "khp_host_build": (c_int, [P(SceneDesc), P(c_uint32), P(c_uint32), P(c_float), P(c_int32), P(c_int32),
                                    P(c_int32), P(c_float), P(c_float)]),
     }

@@ -268,6 +268,21 @@ class HipContext:
                 "khp_trace_any")
         return hit.astype(bool)
 
+    def debug_queues(self):
+        """The extension rays and the shadow rays (o, d, t_max) of bounce
+        khp_ctx_params.dump_bounce of the last synchronous render."""
+        n = ctypes.c_uint32()
+        N.check(self.lib, self.lib.khp_debug_queue(self.ptr, ctypes.byref(n), None, None), "khp_debug_queue")
+        o, d = np.empty((n.value, 3), np.float32), np.empty((n.value, 3), np.float32)
+        N.check(self.lib, self.lib.khp_debug_queue(self.ptr, ctypes.byref(n), N.fptr(o), N.fptr(d)), "khp_debug_queue")
+        m = ctypes.c_uint32()
+        N.check(self.lib, self.lib.khp_debug_shadow_queue(self.ptr, ctypes.byref(m), None, None, None),
+                "khp_debug_shadow_queue")
+        so, sd, st = np.empty((m.value, 3), np.float32), np.empty((m.value, 3), np.float32), np.empty(m.value, np.float32)
+        N.check(self.lib, self.lib.khp_debug_shadow_queue(self.ptr, ctypes.byref(m), N.fptr(so), N.fptr(sd), N.fptr(st)),
+                "khp_debug_shadow_queue")
+        return (o, d), (so, sd, st)
+
     def stats(self) -> dict:
         s = N.Stats()
         N.check(self.lib, self.lib.khp_get_stats(self.ptr, ctypes.byref(s)), "khp_get_stats")

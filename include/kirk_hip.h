@@ -417,6 +417,9 @@ khp_status khp_host_build(const khp_scene* scene, uint32_t* n_nodes, uint32_t* d
  * khp_ctx_params.dump_bounce = b, the extension rays of bounce b (queue order) are
  * kept on the host.  Call with null arrays to get *n, then with [n][3] arrays. */
 khp_status khp_debug_queue(khp_ctx* ctx, uint32_t* n, float* orig, float* dir);
+/* The same render's shadow rays of bounce b as k_shadow traces them (after the
+ * zero-colour skip): origin, direction ([n][3]) and t_max ([n]). */
+khp_status khp_debug_shadow_queue(khp_ctx* ctx, uint32_t* n, float* orig, float* dir, float* tmax);
 
 /* ---- registries / host helpers --------------------------------------------- */
 /* BsdfFactory::getBsdf / ShaderFactory::getShader by KIRK name; -1 if unknown

@@ -93,6 +93,10 @@ int ko_bsdf_sample(ko_ctx* c, int hit_obj, const khp_material* mat, const float 
 /* Output stage (kirk_tonemap.c): Texture::setPixel byte conversion and
  * Tonemapper::map, sequential in KIRK's order. */
 void ko_tonemap_defaults(khp_tonemap* t);
+/* The output stage's log / exp / pow replacements (same algorithm as kmath.h k_*_d). */
+double ko_log_d(double x);
+double ko_exp_d(double x);
+double ko_pow_d(double x, double y);
 void ko_to_rgba8(uint32_t n_pixels, const float* rgb, uint8_t* out_rgba);
 int ko_tonemap(uint32_t W, uint32_t H, const float* rgb, const khp_tonemap* tm, float* out_rgb, float* max_lum,
                float* world_lum);

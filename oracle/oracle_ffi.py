@@ -64,6 +64,9 @@ def load():
         "ko_expf": (c_float, [c_float]),
         "ko_sinhf": (c_float, [c_float]),
         "ko_j0": (c_double, [c_double]),
+        "ko_log_d": (c_double, [c_double]),
+        "ko_exp_d": (c_double, [c_double]),
+        "ko_pow_d": (c_double, [c_double, c_double]),
         "ko_rand_u32": (c_uint32, [c_uint32, c_uint32, c_uint32, c_uint32]),
         "ko_bsdf_sample": (c_int, [c_void_p, c_int, c_void_p, P(c_float), P(c_float), P(c_float), P(c_float), c_int,
                                    P(c_float), P(c_float), P(c_float)]),

@@ -91,3 +91,41 @@ def test_rng_uniformity():
     u = np.array([L.ko_rand_u32(1, i, 0, 2) >> 8 for i in range(20000)], np.float64) / 2**24
     assert abs(u.mean() - 0.5) < 0.01
     assert abs(u.var() - 1 / 12) < 0.005
+
+
+def _ulp64(got, want):
+    if want == 0.0:
+        return 0.0 if got == 0.0 else np.inf
+    return abs(got - want) / np.spacing(abs(np.float64(want)))
+
+
+def test_log_exp_pow_double_ulp():
+    """The output stage's log / exp / pow (ko_*_d == kmath k_*_d) within 2 ulp of float64."""
+    rng = np.random.default_rng(4)
+    xs = np.concatenate([np.exp(rng.uniform(-700, 700, 3000)), rng.uniform(1e-6, 10, 3000), [2.3e-5, 1.0, 0.5, 2.0],
+                         [5e-324, 2.2250738585072014e-308 / 3]])
+    assert max(_ulp64(L.ko_log_d(float(x)), np.log(x)) for x in xs) <= 2.0
+    es = np.concatenate([rng.uniform(-740, 709, 3000), rng.uniform(-1, 1, 3000), [0.0, 1.0, -1.0]])
+    assert max(_ulp64(L.ko_exp_d(float(x)), np.exp(x)) for x in es if np.exp(x) > 2.2250738585072014e-308) <= 2.0
+    ps = [(float(a), float(b)) for a, b in zip(rng.uniform(1e-4, 50, 2000), rng.uniform(-4, 4, 2000))]
+    assert max(_ulp64(L.ko_pow_d(a, b), np.power(a, b)) for a, b in ps) <= 64.0   # |y log x| < 40: ~40 ulp worst
+    for a, b in ps[:500]:   # the float overload (powf) is the double result rounded: within 1 float ulp
+        assert ulp_err(np.float32(L.ko_pow_d(float(np.float32(a)), float(np.float32(b)))),
+                       np.power(np.float64(np.float32(a)), np.float64(np.float32(b)))) <= 1.0
+
+
+def test_pow_special_cases_c99():
+    inf, nan = float("inf"), float("nan")
+    cases = [((nan, 0.0), 1.0), ((1.0, nan), 1.0), ((0.0, -1.0), inf), ((-0.0, -1.0), -inf), ((-0.0, 3.0), -0.0),
+             ((0.0, 0.5), 0.0), ((-1.0, inf), 1.0), ((0.5, -inf), inf), ((2.0, -inf), 0.0), ((0.5, inf), 0.0),
+             ((-inf, -3.0), -0.0), ((-inf, 3.0), -inf), ((-inf, 2.0), inf), ((inf, -0.5), 0.0), ((-2.0, 3.0), -8.0),
+             ((-2.0, 2.0), 4.0), ((-8.0, 1.0 / 3.0), nan), ((2.0, 10.0), 1024.0)]
+    for (x, y), want in cases:
+        # exp(y log x) is within a few double ulp; the float overloads the output stage uses round it exactly
+        got = float(np.float32(L.ko_pow_d(x, y)))
+        if np.isnan(want):
+            assert np.isnan(got), (x, y)
+        else:
+            assert got == want and np.signbit(got) == np.signbit(want), (x, y, got)
+    assert L.ko_log_d(0.0) == -inf and np.isnan(L.ko_log_d(-1.0)) and L.ko_log_d(inf) == inf
+    assert L.ko_exp_d(1000.0) == inf and L.ko_exp_d(-1000.0) == 0.0 and L.ko_exp_d(0.0) == 1.0
