@@ -40,6 +40,7 @@ struct DevScene {
     uint32_t n_tris;
     int32_t textured;
     khp_env_map env_map;
+    const uint32_t* __restrict__ tri_slot;  // object-id order: the slot of each triangle (NaN-origin shadow rays)
 };
 
 // ---- textures (ABI 6) -------------------------------------------------------------------

@@ -730,9 +730,9 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, W
                 tmax = a.w;
                 trav_setup(tr, r);
                 lf.left = 0;
-                if (!STATS && tr.inv.x != tr.inv.x) {  // NaN x direction: occluded iff a triangle exists (ray_has_nan)
+                if (!STATS && x_slab_nan(tr)) {  // the whole-tree walk, answered exactly (any_hit_x_nan)
                     has = false;
-                    Wv.vis[idx] = S.n_tris > 0 ? 1 : 0;
+                    Wv.vis[idx] = any_hit_x_nan(S, r) ? 1 : 0;
                 } else {
                     has = trav2_begin<STATS>(S, tr, tmax, stk, mode, c, lf, st);
                     if (!has) Wv.vis[idx] = 0;
@@ -955,6 +955,14 @@ __global__ __launch_bounds__(256) void k_trace_any(DevScene S, uint32_t n, const
     hit_out[i] = trace_any<false>(S, r, tmax[i], stk, st) ? 1 : 0;
 }
 
+// The slot of every triangle (object-id order) for any_hit_x_nan.  Pad slots are zero records.
+__global__ void k_tri_slots(const float4* prims, const Aux* aux, uint32_t n_slots, uint32_t n_tris, uint32_t* out) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_slots || !is_tri(prims[4 * (size_t)s])) return;
+    const uint32_t o = aux[s].obj;
+    if (o < n_tris) out[o] = s;
+}
+
 // ---- multi-GPU: pack owned pixels / scatter a rank's pixels ------------------------------
 __global__ void k_pack(const float* fb, const uint32_t* pix, uint32_t P, float* out) {
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1042,7 +1050,7 @@ struct khp_ctx {
     int n_cu = 256;
     HostScene hs;
     bool scene_set = false, built = false;
-    DevMem prims, aux, trinrm, trifrm, nodes, mats, lights;
+    DevMem prims, aux, trinrm, trifrm, nodes, mats, lights, trislot;
     DevMem triuv, coneh, texd, texels, mtex;   // ABI 6 textures
     DevScene S{};
     khp_ctx_params prm{};
@@ -1373,9 +1381,15 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         HIPCHK(upload(c->texels, hs.texels.data(), hs.texels.size(), c->stream));
         HIPCHK(upload(c->mtex, hs.mtex.data(), hs.mtex.size(), c->stream));
     }
+    HIPCHK(c->trislot.ensure(4 * (size_t)std::max(hs.n_tris, 1u)));
+    if (hs.n_tris > 0 && n_slots > 0)
+        hipLaunchKernelGGL(k_tri_slots, dim3((n_slots + 255) / 256), dim3(256), 0, c->stream, c->prims.as<float4>(),
+                           c->aux.as<Aux>(), n_slots, hs.n_tris, c->trislot.as<uint32_t>());
+    HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     c->st.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     DevScene& S = c->S;
+    S.tri_slot = c->trislot.as<uint32_t>();
     S.prims = c->prims.as<float4>();
     S.aux = c->aux.as<Aux>();
     S.tri_nrm = host_build ? c->trinrm.as<float>() : c->obj.tri_nrm.as<float>();

@@ -60,6 +60,30 @@ __device__ __forceinline__ bool ray_has_nan(const Ray& r) {
            r.d.z != r.d.z;
 }
 
+// Any hit for rays whose x slab is NaN: a NaN origin x or a NaN inverse
+// direction x (shadow rays from a hit whose normal is NaN get a NaN origin and
+// a finite direction).  The x entry/exit of every box is then NaN and stays
+// NaN through BoundingVolume::intersects' comparisons, so every box passes
+// and nothing is pruned: KIRK visits every node and tests every candidate
+// until one passes.  Cones never pass (their quadratic is NaN).  A triangle
+// passes iff its determinant passes the |det| < eps rejection: u, v and t
+// are NaN (NaN origin) and no rejecting comparison holds; with a NaN direction
+// the determinant itself is NaN.  The answer does not depend on the visit
+// order, so it is "some triangle has !(|det| < eps)", found here in object
+// order (usually at the first triangle) instead of KIRK's walk of the whole
+// tree, which took ~10 s for one such ray at config 3.
+__device__ __forceinline__ bool x_slab_nan(const TravRay& tr) { return tr.inv.x != tr.inv.x || tr.r.o.x != tr.r.o.x; }
+__device__ __forceinline__ bool any_hit_x_nan(const DevScene& S, const Ray& r) {
+    for (uint32_t k = 0; k < S.n_tris; ++k) {
+        const float4* p = S.prims + 4 * (size_t)S.tri_slot[k];
+        const float4 ab = p[1], ac = p[2];  // tri_test's det: dot(cross(d, ac), ab)
+        const v3 dv = cross(r.d, mk(ac.x, ac.y, ac.z));
+        const float det = dot(dv, mk(ab.x, ab.y, ab.z));
+        if (!(fabsf(det) < TRI_EPS_D)) return true;
+    }
+    return false;
+}
+
 __device__ __forceinline__ bool ref_leaf(uint32_t r) { return (r & LEAF_BIT) != 0u; }
 
 struct PrivStack {

@@ -476,6 +476,9 @@ def test_production_traversal_kernels_ray_by_ray(hip_ctx, mode, name, kw):
     d[60:80, 1] = np.nan
     orig[80:100, 2] = np.nan
     orig[100:120] = np.nan
+    orig[120:140, 0] = np.nan   # the any-hit x-slab class (any_hit_x_nan): NaN origin x, finite direction
+    orig[140:150, 1] = np.nan
+    tmax[150:170] = np.nan
     t0, obj0, uv0, nodes, prims = o.trace_closest(orig, d)
     any0 = o.trace_any(orig, d, tmax)
     old = hip_ctx.set_params(trace_kernels=int(mode))
