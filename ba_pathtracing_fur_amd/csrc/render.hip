@@ -88,6 +88,10 @@ struct Wave {
     uint8_t* heavy;       // per queue slot: the ray's traversal took more than heavy_T iterations
     uint32_t cap;         // queue / path capacity of this set
     uint32_t heavy_T;
+    // shade_order 1 (hit sorting): k_shade takes queue slot perm[iv] instead of q_phys(iv)
+    uint32_t* perm;       // null: queue order
+    uint8_t* hkey;        // shading class of queue entry iv (k_hit_class -> k_hit_scatter)
+    uint32_t* hcls;       // [0,16): entries per class, [16,32): scatter cursors per class
 };
 
 // Longest-first queues.  A persistent traversal launch ends when its slowest
@@ -355,6 +359,55 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_extend(DevScene S, W
                     &Wv.cnt->lanes_busy, &Wv.cnt->spills);
 }
 
+// ---- hit sorting (khp_ctx_params.shade_order = 1) ----------------------------------------
+// The extension hits are grouped by shading class before k_shade, so a shade
+// wave runs one BSDF's code instead of the union of several: class 0 = no
+// surface hit (environment, or a light), class 1 + k = a surface whose
+// material has BSDF kind k.  A counting sort over the queue: k_hit_class
+// counts the classes, k_hit_scatter writes each entry's queue slot into the
+// range of its class (perm).  Paths are independent and each path's state is
+// updated by its own lane, so the order changes no result; the next bounce's
+// queues come out grouped the same way.
+constexpr uint32_t NCLS = 1 + KHP_BSDF_COUNT;
+static_assert(NCLS <= 16, "hit classes");
+__device__ __forceinline__ uint32_t hit_class(const DevScene& S, int32_t slot) {
+    return slot < 0 ? 0u : 1u + (uint32_t)S.mats[S.aux[slot].mat].bsdf;
+}
+__global__ __launch_bounds__(256) void k_hit_class(DevScene S, Wave Wv, int cur) {
+    __shared__ uint32_t h[16];
+    const uint32_t nf = Wv.cnt->nq[cur], n = nf + Wv.cnt->nqb[cur];
+    if (threadIdx.x < 16) h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t iv = blockIdx.x * blockDim.x + threadIdx.x; iv < n; iv += gridDim.x * blockDim.x) {
+        const uint32_t k = hit_class(S, Wv.hslot[q_phys(iv, nf, Wv.cap)]);
+        Wv.hkey[iv] = (uint8_t)k;
+        atomicAdd(&h[k], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < NCLS && h[threadIdx.x]) atomicAdd(&Wv.hcls[threadIdx.x], h[threadIdx.x]);
+}
+__global__ __launch_bounds__(256) void k_hit_scatter(Wave Wv, int cur) {
+    __shared__ uint32_t base[16], cnt[16], off[16];
+    const uint32_t nf = Wv.cnt->nq[cur], n = nf + Wv.cnt->nqb[cur];
+    if (threadIdx.x < 16) {
+        uint32_t b = 0;
+        for (uint32_t k = 0; k < threadIdx.x && k < NCLS; ++k) b += Wv.hcls[k];
+        base[threadIdx.x] = b;
+    }
+    for (uint32_t t0 = blockIdx.x * blockDim.x; t0 < n; t0 += gridDim.x * blockDim.x) {
+        const uint32_t iv = t0 + threadIdx.x;
+        if (threadIdx.x < 16) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        const uint32_t k = iv < n ? Wv.hkey[iv] : 0u;
+        const uint32_t local = iv < n ? atomicAdd(&cnt[k], 1u) : 0u;
+        __syncthreads();
+        if (threadIdx.x < NCLS && cnt[threadIdx.x]) off[threadIdx.x] = atomicAdd(&Wv.hcls[16 + threadIdx.x], cnt[threadIdx.x]);
+        __syncthreads();
+        if (iv < n) Wv.perm[base[k] + off[k] + local] = q_phys(iv, nf, Wv.cap);
+        __syncthreads();
+    }
+}
+
 // Hit texcoord (Cylinder::calcTcoord, Cylinder.cpp:239-260; Triangle::calcTcoord,
 // Triangle.cpp:250-254) and the material with its textured parameters resolved.
 // m holds the material's values on entry (resolve_material overwrites the textured ones).
@@ -458,7 +511,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {
         const uint32_t iv = base + threadIdx.x;
         bool active = iv < n;
-        const uint32_t i = active ? q_phys(iv, nf, Wv.cap) : 0u;
+        const uint32_t i = !active ? 0u : Wv.perm ? Wv.perm[iv] : q_phys(iv, nf, Wv.cap);
         const bool heavy = active && Wv.heavy[i] != 0;
         bool emit_ray = false, emit_sh = false;
         Ray nr;
@@ -1005,11 +1058,12 @@ struct PathSet {
     size_t cap = 0;
     DevMem qbuf[2][7], ht, hslot, hu, hv, TFb, CKb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
     DevMem heavyb;
+    DevMem permb, hkeyb, hclsb;   // shade_order 1
     hipStream_t sA = nullptr, sB = nullptr;
 };
 // Device bytes per path of a PathSet (ensure_wave): 2 x 7 queue columns, hit
 // t/slot/u/v, TF + CK records, heavy flag, 2 x (occlusion flag + 96-B shadow record).
-constexpr size_t PATH_BYTES = 2 * 7 * 4 + 4 * 4 + 2 * 16 + 1 + 2 * (1 + 6 * 16);
+constexpr size_t PATH_BYTES = 2 * 7 * 4 + 4 * 4 + 2 * 16 + 1 + 2 * (1 + 6 * 16) + 4 + 1;
 
 #ifndef KHP_MAX_INFLIGHT
 #define KHP_MAX_INFLIGHT 3
@@ -1124,6 +1178,7 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->heavy_iters = 160;
     out->dump_bounce = -1;
     out->trace_kernels = 0;
+    out->shade_order = 0;       // hit sorting measured, off
 }
 
 extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {
@@ -1140,6 +1195,7 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     if (prm->chunk_paths != 0 && prm->chunk_paths < 4096) return fail(KHP_EINVAL, "chunk_paths must be 0 or >= 4096");
     if (prm->chunk_paths > ((uint64_t)1 << 31)) return fail(KHP_EINVAL, "chunk_paths must be <= 2^31");
     if (prm->trace_kernels > 2) return fail(KHP_EINVAL, "trace_kernels must be 0, 1 or 2");
+    if (prm->shade_order > 1) return fail(KHP_EINVAL, "shade_order must be 0 or 1");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
     if (dr != KHP_OK) return dr;
@@ -1448,6 +1504,9 @@ static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap) {
     HIPCHK(w.TFb.ensure(cap * sizeof(float4)));
     HIPCHK(w.CKb.ensure(cap * sizeof(float4)));
     HIPCHK(w.heavyb.ensure(cap));
+    HIPCHK(w.permb.ensure(cap * 4));
+    HIPCHK(w.hkeyb.ensure(cap));
+    HIPCHK(w.hclsb.ensure(32 * 4));
     for (int q = 0; q < 2; ++q) {
         HIPCHK(w.visb[q].ensure(cap));
         HIPCHK(w.shb[q].ensure(cap * 6 * sizeof(float4)));
@@ -1489,6 +1548,9 @@ static Wave wave_view(const khp_ctx* c, PathSet& w) {
     Wv.heavy = w.heavyb.as<uint8_t>();
     Wv.cap = (uint32_t)w.cap;
     Wv.heavy_T = c->prm.heavy_iters;
+    Wv.perm = c->prm.shade_order ? w.permb.as<uint32_t>() : nullptr;
+    Wv.hkey = w.hkeyb.as<uint8_t>();
+    Wv.hcls = w.hclsb.as<uint32_t>();
     return Wv;
 }
 
@@ -1883,6 +1945,11 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 timed(c, f, 0, false, sA);
                 if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
                 timed(c, f, 1, true, sA);
+                if (Wb.perm) {  // hit sorting (shade_order 1): part of the shade time
+                    HIPCHK(hipMemsetAsync(Wb.hcls, 0, 32 * sizeof(uint32_t), sA));
+                    hipLaunchKernelGGL(k_hit_class, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur);
+                    hipLaunchKernelGGL(k_hit_scatter, dim3(c->grid_shade), dim3(256), 0, sA, Wb, cur);
+                }
                 if (c->S.textured)
                     hipLaunchKernelGGL(k_shade<true>, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
                 else

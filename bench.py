@@ -83,6 +83,7 @@ def parse():
     ap.add_argument("--fuse", type=int, default=None, help="khp_ctx_params.fuse_frames (default: the library's)")
     ap.add_argument("--chunk-paths", type=int, default=None, help="khp_ctx_params.chunk_paths")
     ap.add_argument("--frames-in-flight", type=int, default=None, help="khp_ctx_params.frames_in_flight")
+    ap.add_argument("--shade-order", type=int, default=None, help="khp_ctx_params.shade_order (1: hits sorted by shading class)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-scene", action="store_true",
@@ -260,7 +261,8 @@ def main():
             f"({setup}), depth {st0['bvh_depth']}, nodes {st0['n_nodes']}, HBM {st0['device_bytes'] / 1e9:.2f} GB")
     frame = ShardedFrame(ctx, rank, world, dist, tile=args.tile)
     knobs = {k: v for k, v in (("fuse_frames", args.fuse), ("chunk_paths", args.chunk_paths),
-                               ("frames_in_flight", args.frames_in_flight)) if v is not None}
+                               ("frames_in_flight", args.frames_in_flight), ("shade_order", args.shade_order))
+             if v is not None}
     if knobs:
         ctx.set_params(**knobs)
     params = ctx.params()

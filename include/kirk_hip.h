@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 6
+#define KHP_ABI_VERSION 7
 
 typedef struct khp_ctx khp_ctx;
 
@@ -282,6 +282,10 @@ typedef struct {
     uint32_t trace_kernels;      /* khp_trace_closest / khp_trace_any run on 0: one-ray-per-thread
                                     kernels (default), 1: the instrumented persistent kernels (KIRK's
                                     visit counts), 2: the production persistent kernels             */
+    uint32_t shade_order;        /* ABI 7: 0 (default): k_shade takes the hits in queue order; 1: hits are
+                                    first grouped by shading class (no hit / BSDF kind), a counting
+                                    sort per bounce -- KIRK's GLSL template only compacts its hits
+                                    (pt_sortHits.compute:17-38); measured in DESIGN.md §4            */
 } khp_ctx_params;
 
 /* ---- context --------------------------------------------------------------- */

@@ -159,11 +159,33 @@ def test_chunked_and_instrumented_frames(hip_ctx, chunk):
 
 def test_params_are_validated(hip_ctx):
     for bad in (dict(fuse_frames=0), dict(fuse_frames=33), dict(frames_in_flight=4), dict(chunk_paths=100),
-                dict(trace_kernels=3)):
+                dict(trace_kernels=3), dict(shade_order=2)):
         with pytest.raises(N.KhpError) as e:
             hip_ctx.set_params(**bad)
         assert e.value.status == N.KHP_EINVAL
     assert hip_ctx.params()["fuse_frames"] == 32
+
+
+@pytest.mark.parametrize("name,kw,w,h,spp,depth", [CASES[4], CASES[5], CASES[8]], ids=["config5", "zoo", "textured"])
+def test_hit_sorting(hip_ctx, name, kw, w, h, spp, depth):
+    """shade_order 1 (hits grouped by shading class before k_shade) changes only
+    the order k_shade takes the paths in: synchronous, instrumented and fused
+    asynchronous frames stay the oracle's, bit for bit."""
+    sd = S.build_config(name, width=w, height=h, **kw)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    want = oracle_ffi.Oracle(sd).render(w, h, spp, depth, threads=16)
+    old = hip_ctx.set_params(shade_order=1, chunk_paths=4096)
+    try:
+        assert_parity(hip_ctx.render(w, h, spp, depth), want, exact=True)
+        assert_parity(hip_ctx.render(w, h, spp, depth, stats=True), want, exact=True)
+        hip_ctx.set_params(chunk_paths=0)
+        for k in range(spp):
+            hip_ctx.render(w, h, 1, depth, first_sample=k, async_=True)
+        hip_ctx.sync()
+        assert_parity(hip_ctx.read_framebuffer(w, h), want, exact=True)
+    finally:
+        hip_ctx.set_params(**old)
 
 
 @pytest.mark.parametrize("fif", ["1", "2", "3"])
