@@ -24,6 +24,7 @@
 
 #include "device.h"
 #include "device_build.h"
+#include "lightpath.h"
 
 using namespace khp;
 
@@ -92,7 +93,10 @@ struct Wave {
     uint32_t* perm;       // null: queue order
     uint8_t* hkey;        // shading class of queue entry iv (k_hit_class -> k_hit_scatter)
     uint32_t* hcls;       // [0,16): entries per class, [16,32): scatter cursors per class
+    BdptDev bd;           // light-path variant (ABI 7); bd.on = 0: next-event estimate
 };
+
+
 
 // Longest-first queues.  A persistent traversal launch ends when its slowest
 // ray does; if long rays are claimed last, each launch ends one long-ray
@@ -116,6 +120,25 @@ __device__ __forceinline__ uint32_t wave_alloc(bool pred, uint32_t* counter) {
     uint32_t base = 0;
     if (lane == 0 && mask) base = atomicAdd(counter, (uint32_t)__popcll(mask));
     base = __shfl(base, 0);
+    return base + prefix;
+}
+
+// Wave-level allocation of cnt (< 32) consecutive entries per lane, callable
+// from divergent code: the prefix sum is built from one ballot per bit of
+// cnt, so lanes that do not execute the call count nothing.
+__device__ __forceinline__ uint32_t wave_alloc_n(uint32_t cnt, uint32_t* counter) {
+    const uint32_t lane = lane_id();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    uint32_t prefix = 0, total = 0;
+    for (int bit = 0; bit < 5; ++bit) {
+        const unsigned long long m = __ballot((cnt >> bit) & 1u);
+        prefix += (uint32_t)__popcll(m & lt) << bit;
+        total += (uint32_t)__popcll(m) << bit;
+    }
+    const uint32_t leader = (uint32_t)__ffsll((long long)__ballot(1)) - 1u;
+    uint32_t base = 0;
+    if (lane == leader && total) base = atomicAdd(counter, total);
+    base = __shfl(base, (int)leader);
     return base + prefix;
 }
 
@@ -359,6 +382,127 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_extend(DevScene S, W
                     &Wv.cnt->lanes_busy, &Wv.cnt->spills);
 }
 
+// ---- light-path variant (khp_bdpt_params, ABI 7; lightpath.h) ----------------------------
+// The surface at a closest hit: normal, hair frame and material (k_shade's
+// calcNormal / calcTcoord code; Cylinder.cpp:230-260, Triangle.cpp:244-254).
+__device__ __forceinline__ void textured_material(const DevScene& S, const Aux& ax, const float4* pr, v3 loc,
+                                               const ShadeCtx& s, float bu, float bv, khp_material& out);
+__device__ __forceinline__ v3 surface_at(const DevScene& S, const Ray& r, const Hit& h, ShadeCtx& s,
+                                         khp_material& mres) {
+    const Aux ax = S.aux[h.slot];
+    const float4* pr = S.prims + 4 * (size_t)h.slot;
+    s.m = &S.mats[ax.mat];
+    v3 nrm;
+    if (ax.flags & 1u) {
+        const float4 c0 = pr[0], c1 = pr[1], c2 = pr[2], c3 = pr[3];
+        s.U = mk(c1.x, c1.y, c1.z);
+        s.V = mk(c2.x, c2.y, c2.z);
+        s.W = mk(c3.x, c3.y, c3.z);
+        const v3 Q = follow(r, h.t);
+        const float tt = dot(Q, s.V) - ax.base_d;
+        const v3 q1 = Q - s.V * tt;
+        const v3 nn = normalize(q1 - mk(c0.x, c0.y, c0.z));
+        nrm = normalize(nn + s.V * c1.w);
+    } else {
+        const float* tn = S.tri_nrm + 9 * (size_t)ax.obj;
+        const float bx = (1.0f - h.u) - h.v;
+        nrm = normalize((ld3(tn) * bx + ld3(tn + 3) * h.u) + ld3(tn + 6) * h.v);
+        const float* tf = S.tri_frame + 9 * (size_t)ax.obj;
+        s.U = ld3(tf);
+        s.V = ld3(tf + 3);
+        s.W = ld3(tf + 6);
+    }
+    s.n = nrm;
+    if (S.textured) {
+        mres = S.mats[ax.mat];
+        textured_material(S, ax, pr, follow(r, h.t), s, h.u, h.v, mres);
+        s.m = &mres;
+    }
+    return nrm;
+}
+
+// One light subpath per thread (lbb_construction.compute:195-403; the
+// oracle's light_subpath): thread t = (sample slot q, subpath s, light) writes
+// vertices [t*J, t*J + J) of bd.lv.  Sample slot q = frame * n_samples + sample.
+__global__ __launch_bounds__(64) void k_light_paths(DevScene S, Wave Wv) {
+    const BdptDev& bd = Wv.bd;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nq = Wv.n_frames * Wv.n_samples;
+    if (t >= nq * bd.Ns * bd.L) return;
+    const uint32_t li = t % bd.L, sub = (t / bd.L) % bd.Ns, q = t / (bd.L * bd.Ns);
+    const uint32_t fr = q / Wv.n_samples, k = Wv.fsample0[fr] + (q - fr * Wv.n_samples);
+    float4* out = const_cast<float4*>(bd.lv) + 3 * (size_t)t * bd.J;
+    for (uint32_t j = 0; j < bd.J; ++j) out[3 * j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const DevLight& L = S.lights[li];
+    const uint32_t key = path_key(Wv.seed ^ LPATH_SEED, sub * bd.L + li, k);
+    Ray r = gl_light_ray(L, draw_u01(key, dim_of(0, P_LIGHT_0)), draw_u01(key, dim_of(0, P_LIGHT_1)),
+                         draw_u01(key, dim_of(0, P_BSDF_0)), draw_u01(key, dim_of(0, P_BSDF_1)));
+    v3 ppos = r.o, phc = mk(GL_ONE_OVER_PI, GL_ONE_OVER_PI, GL_ONE_OVER_PI);
+    out[0] = make_float4(ppos.x, ppos.y, ppos.z, 1.0f);
+    out[1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    out[2] = make_float4(phc.x, phc.y, phc.z, 0.0f);
+    const bool carries = L.kind == KHP_LIGHT_POINT || L.kind == KHP_LIGHT_QUAD;
+    const float al = carries ? L.l : 0.0f, aq = carries ? L.q : 0.0f;
+    float dist = 0.0f;
+    for (uint32_t j = 1; j < bd.J; ++j) {
+        if (ray_has_nan(r)) return;  // no closest hit (ray_has_nan)
+        Hit h;
+        PrivStack stk;
+        TravStats st{0, 0, 0};
+        trace_closest<false>(S, r, h, stk, st);
+        if (h.slot < 0) return;  // traceLightRays: no hit ends the subpath
+        ShadeCtx sc;
+        khp_material mres;
+        const v3 n = surface_at(S, r, h, sc, mres), pos = follow(r, h.t);
+        dist = dist + length(pos - r.o);
+        const float att = 1.0f / ((1.0f + dist * al) + (dist * dist) * aq);
+        const v3 in = -r.d;
+        v3 od = mk(0.0f, 0.0f, 0.0f), f = mk(0.0f, 0.0f, 0.0f);
+        float pdf = 0.0f;
+        int fl = 0;
+        if (!(dot(in, n) == 0.0f)) {  // reflectance (BSDF/header.compute:48-56)
+            float smp[2] = {draw_u01(key, dim_of(j, P_BSDF_0)), draw_u01(key, dim_of(j, P_BSDF_1))};
+            bool valid;
+            f = bsdf_sample(sc, in, n, smp, draw_u01(key, dim_of(j, P_HAIR_ALPHA)),
+                            draw_u01(key, dim_of(j, P_HAIR_BETA)), od, pdf, fl, valid);
+        }
+        v3 hc = phc * f;
+        const v3 w = pos - ppos;  // convertDensity (:280-299), previous vertex = its position
+        const float ww = dot(w, w);
+        if (ww == 0.0f) pdf = 0.0f;
+        else pdf = pdf * fabsf(dot(n, w * sqrtf(1.0f / ww)));
+        hc = hc * gclamp(fabsf(dot(od, n)) * pdf, 0.0f, 1.0f);
+        if ((fl & F_EMISSIVE) == F_EMISSIVE) return;
+        if (is_zero(hc) || pdf <= bd.min_pdf || att <= 0.0001f) return;
+        out[3 * j] = make_float4(pos.x, pos.y, pos.z, 1.0f);
+        out[3 * j + 1] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
+        out[3 * j + 2] = make_float4(hc.x, hc.y, hc.z, 0.0f);
+        ppos = pos;
+        phc = hc;
+        r = make_ray(pos + od * bd.bounce_bias, od);
+    }
+}
+
+// One connection of a camera hit to vertex j of its chosen subpath
+// (pt_shade.compute:150-199; the oracle's bdpt_connect): the connection ray
+// and the contribution it adds when unoccluded.  Returns false for an invalid vertex.
+__device__ __forceinline__ bool bd_connection(const DevScene& S, const BdptDev& bd, const float4* v, uint32_t j,
+                                              const DevLight& L, const ShadeCtx& s, v3 loc, v3 rd, uint32_t b,
+                                              Ray& sh, float& tmax, v3& cj) {
+    const float4 a = v[3 * j];
+    if (a.w == 0.0f) return false;
+    const float4 din = v[3 * j + 1], hc = v[3 * j + 2];
+    const v3 lp = mk(a.x, a.y, a.z) - mk(din.x, din.y, din.z) * bd.bounce_bias;
+    v3 lc = j == 0 ? ld3(L.color) * gl_ang_att(L, lp - loc) : ld3(L.color);
+    sh.o = loc + s.n * bd.bias;
+    sh.d = normalize(lp - loc);
+    tmax = length(lp - sh.o);
+    lc = lc * fabsf(dot(sh.d, s.n));
+    lc = lc * bsdf_eval(s, -rd, sh.d);
+    cj = (mk(hc.x, hc.y, hc.z) * lc) / (float)(j + 1 + b);
+    return true;
+}
+
 // ---- hit sorting (khp_ctx_params.shade_order = 1) ----------------------------------------
 // The extension hits are grouped by shading class before k_shade, so a shade
 // wave runs one BSDF's code instead of the union of several: class 0 = no
@@ -501,7 +645,7 @@ __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3,
 
 // TEX: the scene has textured materials or an environment map (a separate
 // instantiation, so untextured scenes keep k_shade's registers).
-template <bool TEX>
+template <bool TEX, bool BD>
 __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
     const uint32_t nf = Wv.cnt->nq[cur], n = nf + Wv.cnt->nqb[cur];
     const int nxt = cur ^ 1;
@@ -523,6 +667,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
         float sh_tmax = 0.0f;
         v3 lc = mk(0, 0, 0), Told = mk(0, 0, 0), AT = mk(0, 0, 0), ET = mk(0, 0, 0);
         bool has_emit = false;
+        bool deferred = false;  // BD: the colour add is left to the connection group's finish
         if (active) {
             pid = Wv.qpid[cur][i];
             Ray r;
@@ -599,7 +744,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                 // NEE setup: SimpleShader::calcDirectLight (SimpleShader.h:101-152) and
                 // MarschnerHairShader::calcDirectLight (MarschnerHairShader.h:87-138)
                 bool need_shadow = false;
-                if (S.n_lights > 0) {
+                if (!BD && S.n_lights > 0) {
                     int li = (int)((double)draw_u01(key, dim_of(bounce, P_LIGHT_SEL)) * (double)S.n_lights);
                     const DevLight& L = S.lights[li];
                     float att;
@@ -661,7 +806,59 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                         nr = make_ray(loc + off, out);
                     }
                 }
-                if (add_now) {
+                if (add_now && BD) {
+                    // pt_shade.compute:146-201: connect to every valid vertex of one subpath.
+                    // Contributions that are +-0 in every channel cannot change the sum
+                    // (it starts at +0), so they get no connection ray.
+                    uint32_t nv = 0, sp = 0, li = 0;
+                    const float4* lv = nullptr;
+                    if (S.n_lights > 0) {
+                        const BdptDev& bd = Wv.bd;
+                        sp = (uint32_t)((float)bd.Ns * draw_u01(key, dim_of(bounce, P_LIGHT_0)));
+                        li = (uint32_t)((float)bd.L * draw_u01(key, dim_of(bounce, P_LIGHT_SEL)));
+                        sp = sp < bd.Ns ? sp : bd.Ns - 1u;
+                        li = li < bd.L ? li : bd.L - 1u;
+                        const uint32_t per_frame = Wv.P * Wv.n_samples, fr = pid / per_frame;
+                        const uint32_t q = fr * Wv.n_samples + (pid - fr * per_frame) % Wv.n_samples;
+                        lv = bd.lv + 3 * ((((size_t)q * bd.Ns + sp) * bd.L + li) * bd.J);
+                        for (uint32_t j = 0; j < bd.J; ++j) {
+                            Ray sh;
+                            float tm;
+                            v3 cj;
+                            if (bd_connection(S, bd, lv, j, S.lights[li], s, loc, r.d, bounce, sh, tm, cj) &&
+                                !(cj.x == 0.0f && cj.y == 0.0f && cj.z == 0.0f))
+                                ++nv;
+                        }
+                    }
+                    if (nv == 0) {
+                        v3 acc = (mk(0, 0, 0) + mk(0, 0, 0) * Told) + AT;
+                        if (has_emit) acc = acc + ET;
+                        C = C + acc;
+                    } else {
+                        deferred = true;
+                        const BdptDev& bd = Wv.bd;
+                        uint32_t o = wave_alloc_n(nv, &Wv.shq->nsh);
+                        bool head = true;
+                        for (uint32_t j = 0; j < bd.J; ++j) {
+                            Ray sh;
+                            float tm;
+                            v3 cj;
+                            if (!bd_connection(S, bd, lv, j, S.lights[li], s, loc, r.d, bounce, sh, tm, cj) ||
+                                (cj.x == 0.0f && cj.y == 0.0f && cj.z == 0.0f))
+                                continue;
+                            float4* rec = Wv.sh + 6 * (size_t)o++;
+                            rec[0] = make_float4(sh.o.x, sh.o.y, sh.o.z, tm);
+                            rec[1] = make_float4(sh.d.x, sh.d.y, sh.d.z, f_from_bits(pid));
+                            rec[2] = make_float4(cj.x, cj.y, cj.z, has_emit ? 1.0f : 0.0f);
+                            rec[3] = make_float4(Told.x, Told.y, Told.z, head ? (float)nv : 0.0f);
+                            if (head) {
+                                rec[4] = make_float4(AT.x, AT.y, AT.z, 0.0f);
+                                if (has_emit) rec[5] = make_float4(ET.x, ET.y, ET.z, 0.0f);
+                            }
+                            head = false;
+                        }
+                    }
+                } else if (add_now) {
                     if (need_shadow && !(lc.x == 0.0f && lc.y == 0.0f && lc.z == 0.0f)) {
                         emit_sh = true;  // colour is added by k_shadow
                     } else if (need_shadow) {
@@ -681,7 +878,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                 }
             }
             Wv.TF[pid] = make_float4(T.x, T.y, T.z, f_from_bits((uint32_t)flags));
-            if (!emit_sh) Wv.CK[pid] = make_float4(C.x, C.y, C.z, ck.w);
+            if (!emit_sh && !deferred) Wv.CK[pid] = make_float4(C.x, C.y, C.z, ck.w);
             emit_ray = !last && !is_zero(T) && !is_zero(nr.d);
         }
         uint32_t qi, si;
@@ -741,12 +938,52 @@ __device__ __forceinline__ void shadow_finish_one(const DevScene& S, const Wave&
     }
 }
 
+// BD: the records of a light-path connection group (one path, one bounce) are
+// consecutive in the front part; the head (rec[3].w = group size) adds the
+// unoccluded contributions in vertex order (the oracle's bdpt_connect).
+__device__ __forceinline__ void connection_group_finish(const DevScene& S, const Wave& Wv, uint32_t i) {
+    const float4* rec = Wv.sh + 6 * (size_t)i;
+    const float4 d = rec[3];
+    if (d.w == 0.0f) return;  // not a group head
+    const uint32_t nv = (uint32_t)d.w;
+    const uint32_t pid = bits_from_f(rec[1].w);
+    v3 dl = mk(0, 0, 0);
+    for (uint32_t m = 0; m < nv; ++m) {
+        const float4* q = rec + 6 * (size_t)m;
+        const float4 a = q[0], b = q[1], c = q[2];
+        bool occ = Wv.vis[i + m] != 0;
+        if (!occ) {
+            Ray r;
+            r.o = mk(a.x, a.y, a.z);
+            r.d = mk(b.x, b.y, b.z);
+            for (int li = 0; li < S.n_lights; ++li) {
+                float t;
+                if (light_isect(S.lights[li], r, t) && (t < a.w)) {
+                    occ = true;
+                    break;
+                }
+            }
+        }
+        if (!occ) dl = dl + mk(c.x, c.y, c.z);
+    }
+    const float4 e = rec[4];
+    v3 acc = (mk(0, 0, 0) + dl * mk(d.x, d.y, d.z)) + mk(e.x, e.y, e.z);
+    if (rec[2].w != 0.0f) {
+        const float4 f = rec[5];
+        acc = acc + mk(f.x, f.y, f.z);
+    }
+    const float4 ck = Wv.CK[pid];
+    Wv.CK[pid] = make_float4(ck.x + acc.x, ck.y + acc.y, ck.z + acc.z, ck.w);
+}
+
+template <bool BD>
 __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
     const uint32_t nf = Wv.shq->nsh, n = nf + Wv.shq->nshb;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Wv.cnt->sh_rays, (unsigned long long)n);
     for (uint32_t iv = blockIdx.x * blockDim.x + threadIdx.x; iv < n; iv += gridDim.x * blockDim.x) {
         const uint32_t i = q_phys(iv, nf, Wv.cap);
-        shadow_finish_one(S, Wv, i, Wv.vis[i] != 0);
+        if (BD) connection_group_finish(S, Wv, i);
+        else shadow_finish_one(S, Wv, i, Wv.vis[i] != 0);
     }
 }
 
@@ -1059,6 +1296,8 @@ struct PathSet {
     DevMem qbuf[2][7], ht, hslot, hu, hv, TFb, CKb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
     DevMem heavyb;
     DevMem permb, hkeyb, hclsb;   // shade_order 1
+    DevMem lvb;                   // light-path variant: subpath vertices of a chunk's sample slots
+    size_t sh_cap = 0;            // shadow-record capacity per parity (cap x connections per path)
     hipStream_t sA = nullptr, sB = nullptr;
 };
 // Device bytes per path of a PathSet (ensure_wave): 2 x 7 queue columns, hit
@@ -1108,6 +1347,7 @@ struct khp_ctx {
     DevMem triuv, coneh, texd, texels, mtex;   // ABI 6 textures
     DevScene S{};
     khp_ctx_params prm{};
+    khp_bdpt_params bd{};   // light-path variant (ABI 7), off by default
     size_t auto_chunk = 0;         // chunk_paths() when prm.chunk_paths == 0
     // wavefront: one path set per frame slot (ps[0] also serves the batch query API)
     PathSet ps[KHP_MAX_INFLIGHT];
@@ -1204,6 +1444,35 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     return KHP_OK;
 }
 
+extern "C" void khp_bdpt_params_defaults(khp_bdpt_params* out) {
+    if (!out) return;
+    *out = khp_bdpt_params{};
+    out->enabled = 0;
+    out->light_paths = 256;
+    out->vertices = 4;
+    out->bias = 1e-4f;         // the GLSL's 1e-4 bounce bias (pt_shade.compute:269)
+    out->bounce_bias = 1e-4f;
+    out->min_pdf = 1e-4f;      // SimpleShader's pdf <= 1E-4 cut (SimpleShader.h)
+}
+
+extern "C" khp_status khp_get_bdpt(khp_ctx* c, khp_bdpt_params* out) {
+    if (!c || !out) return fail(KHP_EINVAL, "null argument");
+    *out = c->bd;
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_set_bdpt(khp_ctx* c, const khp_bdpt_params* p) {
+    if (!c || !p) return fail(KHP_EINVAL, "null argument");
+    if (p->enabled && (p->light_paths < 1 || p->light_paths > 65536))
+        return fail(KHP_EINVAL, "light_paths must be 1..65536");
+    if (p->enabled && (p->vertices < 1 || p->vertices > 16)) return fail(KHP_EINVAL, "vertices must be 1..16");
+    HIPCHK(hipSetDevice(c->device));
+    khp_status dr = drain(c);  // frames in flight finish with the estimator they started with
+    if (dr != KHP_OK) return dr;
+    c->bd = *p;
+    return KHP_OK;
+}
+
 extern "C" khp_status khp_create(khp_ctx** out, int device, uint32_t flags) {
     if (!out) return fail(KHP_EINVAL, "out is null");
     *out = nullptr;
@@ -1215,6 +1484,7 @@ extern "C" khp_status khp_create(khp_ctx** out, int device, uint32_t flags) {
     c->device = device;
     c->flags = flags;
     khp_ctx_params_defaults(&c->prm);
+    khp_bdpt_params_defaults(&c->bd);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1486,15 +1756,17 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, TRAV_BLOCK, LDS_BYTES));
     c->grid_sh = std::max(1, nb) * c->n_cu;
     nb = 0;
-    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade<true>, 256, 0));
-    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade<false>, 256, 0));
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<true, false>), 256, 0));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false>), 256, 0));
     c->grid_shade = std::max(1, nb) * c->n_cu;
     c->built = true;
     return KHP_OK;
 }
 
-static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap) {
-    if (cap <= w.cap) return KHP_OK;
+static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap, size_t sh_per_path = 1) {
+    if (cap <= w.cap && cap * sh_per_path <= w.sh_cap) return KHP_OK;
+    cap = std::max(cap, w.cap);
+    const size_t shc = std::max(cap * sh_per_path, w.sh_cap);
     for (int q = 0; q < 2; ++q)
         for (int k = 0; k < 7; ++k) HIPCHK(w.qbuf[q][k].ensure(cap * 4));
     HIPCHK(w.ht.ensure(cap * 4));
@@ -1508,9 +1780,10 @@ static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap) {
     HIPCHK(w.hkeyb.ensure(cap));
     HIPCHK(w.hclsb.ensure(32 * 4));
     for (int q = 0; q < 2; ++q) {
-        HIPCHK(w.visb[q].ensure(cap));
-        HIPCHK(w.shb[q].ensure(cap * 6 * sizeof(float4)));
+        HIPCHK(w.visb[q].ensure(shc));
+        HIPCHK(w.shb[q].ensure(shc * 6 * sizeof(float4)));
     }
+    w.sh_cap = shc;
     HIPCHK(w.shqb.ensure(2 * sizeof(ShadowQ)));
     HIPCHK(w.cnt.ensure(sizeof(Counters)));
     // traversal-stack spill columns: one per resident lane, STACK_MAX entries deep
@@ -1835,7 +2108,11 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     // Chunks: the owned pixels x samples (x fused frames) are cut into chunks
     // of at most chunk_paths() paths, pixel-major; a fused chunk carries all
     // samples of all frames of its pixels.
-    const size_t cap_paths = chunk_paths(c);
+    // light-path variant: up to `vertices` connection records per path and bounce,
+    // so a chunk carries 1/vertices of the paths (the same shadow-record memory)
+    const bool bdm = c->bd.enabled != 0 && c->S.n_lights > 0;
+    const uint32_t sh_per_path = bdm ? c->bd.vertices : 1u;
+    const size_t cap_paths = std::max<size_t>(4096 / sh_per_path, chunk_paths(c) / sh_per_path);
     uint32_t P_chunk, S_chunk;
     if (nf > 1) {
         P_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(std::max<uint32_t>(1, P_all),
@@ -1853,8 +2130,10 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         want = std::max(want, std::min<size_t>(cap_paths, (size_t)P_chunk * S_chunk * fuse));
     }
     PathSet& w = c->ps[slot];
-    s = ensure_wave(c, w, want);
+    s = ensure_wave(c, w, want, sh_per_path);
     if (s != KHP_OK) return s;
+    const size_t lv_bytes = bdm ? (size_t)nf * S_chunk * c->bd.light_paths * c->S.n_lights * c->bd.vertices * 48 : 0;
+    if (bdm) HIPCHK(w.lvb.ensure(lv_bytes));
     const int dump_b = (!async && !ops) ? c->prm.dump_bounce : -1;
     if (stats) {
         const size_t chunks = (size_t)((P_all + P_chunk - 1) / P_chunk) * ((p->spp + S_chunk - 1) / S_chunk);
@@ -1898,6 +2177,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     Wv.H = p->height;
     Wv.seed = p->seed;
     Wv.depth = p->depth;
+    Wv.bd = BdptDev{bdm ? 1u : 0u, c->bd.light_paths, (uint32_t)c->S.n_lights, c->bd.vertices, c->bd.bias,
+                    c->bd.bounce_bias, c->bd.min_pdf, bdm ? w.lvb.as<float4>() : nullptr};
     SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
     SpillArea sp_sh{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
     for (uint32_t p0 = 0; p0 < P_all; p0 += P_chunk) {
@@ -1913,6 +2194,10 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
             const uint32_t npaths = P * ns * nf;
             timed(c, f, 3, true, sA);
             hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wv);
+            if (bdm) {  // the light subpaths of this chunk's sample slots (frames x samples)
+                const uint32_t nsub = nf * ns * c->bd.light_paths * (uint32_t)c->S.n_lights;
+                hipLaunchKernelGGL(k_light_paths, dim3((nsub + 63) / 64), dim3(64), 0, sA, c->S, Wv);
+            }
             timed(c, f, 3, false, sA);
             hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
             for (uint32_t b = 0; b < p->depth; ++b) {
@@ -1950,10 +2235,14 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     hipLaunchKernelGGL(k_hit_class, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur);
                     hipLaunchKernelGGL(k_hit_scatter, dim3(c->grid_shade), dim3(256), 0, sA, Wb, cur);
                 }
-                if (c->S.textured)
-                    hipLaunchKernelGGL(k_shade<true>, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                if (c->S.textured && bdm)
+                    hipLaunchKernelGGL((k_shade<true, true>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                else if (c->S.textured)
+                    hipLaunchKernelGGL((k_shade<true, false>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                else if (bdm)
+                    hipLaunchKernelGGL((k_shade<false, true>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
                 else
-                    hipLaunchKernelGGL(k_shade<false>, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                    hipLaunchKernelGGL((k_shade<false, false>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
                 timed(c, f, 1, false, sA);
                 if (sB != sA) {
                     hipEvent_t shaded = slot_event(f.sync_pool, f.sync_next, true);
@@ -1984,7 +2273,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     hipLaunchKernelGGL(k_shadow<false>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sB, c->S, Wb, sp_sh);
                 timed(c, f, 2, false, sB);
                 timed(c, f, 4, true, sB);   // shadow stage = any-hit traversal + finish
-                hipLaunchKernelGGL(k_shadow_finish, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
+                if (bdm) hipLaunchKernelGGL(k_shadow_finish<true>, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
+                else hipLaunchKernelGGL(k_shadow_finish<false>, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
                 timed(c, f, 4, false, sB);
                 if (sB != sA) {
                     done_b = slot_event(f.sync_pool, f.sync_next, true);

@@ -127,6 +127,15 @@ class CtxParams(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class BdptParams(ctypes.Structure):
+    """khp_bdpt_params (ABI 7): the light-path (bidirectional) variant, SURVEY §8(f)4."""
+    _fields_ = [("enabled", c_uint32), ("light_paths", c_uint32), ("vertices", c_uint32), ("bias", c_float),
+                ("bounce_bias", c_float), ("min_pdf", c_float)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class Tonemap(ctypes.Structure):
     """khp_tonemap: KIRK::Tonemapper's parameters (Utils/Tonemapping.h:22-33)."""
     _fields_ = [("exposure", c_float), ("bias", c_float), ("gamma", c_float), ("contrast", c_float),
@@ -153,7 +162,8 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_read_rgba8", "khp_tonemap_defaults", "khp_read_bvh",
             "khp_read_layout", "khp_set_scene_device", "khp_gen_hairball_device", "khp_device_alloc",
             "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device",
-            "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params", "khp_debug_shadow_queue"]
+            "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params", "khp_debug_shadow_queue",
+            "khp_bdpt_params_defaults", "khp_set_bdpt", "khp_get_bdpt"]
 
 _lib = None
 
@@ -188,6 +198,9 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_ctx_params_defaults": (None, [P(CtxParams)]),
         "khp_set_params": (c_int, [c_void_p, P(CtxParams)]),
         "khp_get_params": (c_int, [c_void_p, P(CtxParams)]),
+        "khp_bdpt_params_defaults": (None, [P(BdptParams)]),
+        "khp_set_bdpt": (c_int, [c_void_p, P(BdptParams)]),
+        "khp_get_bdpt": (c_int, [c_void_p, P(BdptParams)]),
         "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
         "khp_read_rgba8": (c_int, [c_void_p, P(Tonemap), P(c_uint8)]),
         "khp_tonemap_defaults": (None, [P(Tonemap)]),

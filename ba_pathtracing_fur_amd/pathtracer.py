@@ -181,6 +181,19 @@ class HipContext:
         N.check(self.lib, self.lib.khp_set_params(self.ptr, ctypes.byref(prm)), "khp_set_params")
         return old
 
+    def set_bdpt(self, **kw) -> dict:
+        """khp_set_bdpt with the given khp_bdpt_params fields changed (enabled,
+        light_paths, vertices, bias, bounce_bias, min_pdf); returns the previous values."""
+        prm = N.BdptParams()
+        N.check(self.lib, self.lib.khp_get_bdpt(self.ptr, ctypes.byref(prm)), "khp_get_bdpt")
+        old = prm.as_dict()
+        for k, v in kw.items():
+            if k not in old:
+                raise AttributeError(f"khp_bdpt_params has no field {k}")
+            setattr(prm, k, v)
+        N.check(self.lib, self.lib.khp_set_bdpt(self.ptr, ctypes.byref(prm)), "khp_set_bdpt")
+        return old
+
     def render(self, width, height, spp, depth, seed=0x4B49524B, first_sample=0, tile_size=64, tile_rank=0,
                tile_nranks=1, out: np.ndarray | None = None, readback=True, stats=False,
                async_: bool = False) -> np.ndarray | None:

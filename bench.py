@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--chunk-paths", type=int, default=None, help="khp_ctx_params.chunk_paths")
     ap.add_argument("--frames-in-flight", type=int, default=None, help="khp_ctx_params.frames_in_flight")
     ap.add_argument("--shade-order", type=int, default=None, help="khp_ctx_params.shade_order (1: hits sorted by shading class)")
+    ap.add_argument("--bdpt", default=None, metavar="PATHS,VERTICES",
+                    help="light-path variant (khp_bdpt_params, SURVEY §8(f)4): not the metric's estimator")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-scene", action="store_true",
@@ -266,6 +268,10 @@ def main():
     if knobs:
         ctx.set_params(**knobs)
     params = ctx.params()
+    if args.bdpt:
+        ns, nv = (int(x) for x in args.bdpt.split(","))
+        ctx.set_bdpt(enabled=1, light_paths=ns, vertices=nv)
+        params["bdpt"] = {"light_paths": ns, "vertices": nv}
     k = 0  # progressive pass counter: pass k renders samples [k*spp, (k+1)*spp)
 
     def step(stats=False, async_=True):
@@ -344,7 +350,8 @@ def main():
         "data": "synthetic: seeded hairball (khp_gen_hairball[_device], seed 0x4B49524B), scene built in-process; "
                 "step k = progressive pass k (samples k*spp .. (k+1)*spp-1)",
         "config": {
-            "workload": f"{cfg['what']} ({n_objects} objects), {W}x{H}, {spp} spp, depth {depth}, progressive passes",
+            "workload": f"{cfg['what']} ({n_objects} objects), {W}x{H}, {spp} spp, depth {depth}, progressive passes"
+                        + (f", light-path variant {args.bdpt}" if args.bdpt else ""),
             "config": args.config, "width": W, "height": H, "spp": spp, "depth": depth, "strands": args.strands,
             "objects": n_objects, "parallelism": f"tile-sharded {args.tile}px tiles x{world}, RCCL gather",
         },

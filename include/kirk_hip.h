@@ -311,6 +311,29 @@ khp_status khp_build_accel(khp_ctx* ctx);
  * Pixels of tiles not owned by this rank are left untouched. */
 khp_status khp_render(khp_ctx* ctx, const khp_render_params* p, float* out_rgb);
 
+/* ABI 7: the light-path (bidirectional) variant of KIRK's GLSL path tracer,
+ * lbb_construction.compute:195-403 builds light subpaths
+ * (generatePrimaryLightRays / traceLightRays / shadeLightRays) and
+ * pt_shade.compute:146-201 connects every camera hit to the vertices of one
+ * randomly chosen subpath (sampling.is_bidirectional) instead of KIRK's
+ * next-event estimate.  Per sample index k of a render, `light_paths`
+ * subpaths per light are traced, each with up to `vertices` vertices (the
+ * first on the light).  The exact rules, with the points where the GLSL is
+ * undefined and this restatement decides, are in DESIGN.md §10.  KIRK's GLSL
+ * marks the feature "experimental"; its estimator is not KIRK's CPU one, so
+ * frames differ from khp_render without it (not a parity mode). */
+typedef struct {
+    uint32_t enabled;       /* 0: KIRK's next-event estimate (default)                          */
+    uint32_t light_paths;   /* samples_per_light: subpaths per light and sample index, 1..65536  */
+    uint32_t vertices;      /* bounces_per_path: vertices per subpath incl. the light's, 1..16   */
+    float bias;             /* debug.bias: connection-ray origin offset along the normal         */
+    float bounce_bias;      /* debug.bounce_bias: light-ray origin offset and vertex pull-back   */
+    float min_pdf;          /* debug.min_pdf: a light vertex with pdf <= min_pdf ends its subpath */
+} khp_bdpt_params;
+void khp_bdpt_params_defaults(khp_bdpt_params* out);   /* off; 256 paths, 4 vertices, 1e-4 x 3 */
+khp_status khp_set_bdpt(khp_ctx* ctx, const khp_bdpt_params* params);
+khp_status khp_get_bdpt(khp_ctx* ctx, khp_bdpt_params* out);
+
 /* Completes every frame enqueued with KHP_RENDER_ASYNC (ABI 5).  A progressive
  * caller (KIRK's PathTracer::render loop) enqueues its passes and syncs before
  * reading the texture; passes accumulate in call order.  Any synchronous call

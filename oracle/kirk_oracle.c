@@ -626,6 +626,11 @@ struct ko_ctx {
     khp_camera cam;
     node_t* nodes; uint32_t n_nodes, cap_nodes, depth;
     uint32_t* ids;
+    /* light-path variant (ABI 7): parameters and the subpaths of
+     * the sample indices of the current render call */
+    khp_bdpt_params bd;
+    struct lvert* lv; size_t lv_cap;
+    uint32_t lv_k0, lv_nk;
 };
 
 typedef struct { float cbmin, k; } axis_const_t;
@@ -1427,6 +1432,202 @@ static v3 direct_light(const struct ko_ctx* c, const shade_ctx_t* s, v3 loc, con
 
 static int max3_lt(v3 T, float th) { return gmax(T.x, gmax(T.y, T.z)) < th; }
 
+/* ======================================================================= */
+/*  light-path (bidirectional) variant: KIRK's GLSL lbb_construction.compute */
+/*  :195-403 and pt_shade.compute:146-201    */
+/* ======================================================================= */
+#define GL_PI 3.14159265359f          /* inc_random.compute:11, a GLSL float */
+#define GL_ONE_OVER_PI 0.31830988618f /* inc_random.compute:12 */
+#define GL_DEG2RAD 0.01745329251994329577f
+struct lvert {
+    int valid;
+    v3 pos;   /* vertex position (the light sample point for vertex 0) */
+    v3 din;   /* direction of the ray that reached it (0 for vertex 0, lbb_construction.compute:235) */
+    v3 hc;    /* hit_color */
+};
+typedef struct lvert lvert_t;
+/* light-path RNG: the path key of subpath (s, light) at sample index k */
+static uint32_t lpath_key(uint32_t seed, uint32_t sub, uint32_t k) { return path_key(seed ^ 0x4C504154u, sub, k); }
+
+static v3 gl_cos_hemi(float u, float v) {   /* cosineHemisphereSample, inc_random.compute:50-65 */
+    float r = sqrtf(u), th = 2.0f * GL_PI * v;
+    float x = r * ko_cosf(th), y = r * ko_sinf(th);
+    return V(x, y, sqrtf(gmax(0.0f, (1.0f - x * x) - y * y)));
+}
+static v3 gl_uniform_sphere(float u, float v) {   /* uniformSphereSample, inc_random.compute:75-81 */
+    float phi = v * 2.0f * GL_PI, ct = 2.0f * u - 1.0f;
+    float st = sqrtf(gmax(0.0f, 1.0f - ct * ct));
+    return V(st * ko_cosf(phi), st * ko_sinf(phi), ct);
+}
+static v3 gl_sample_angle(float u, float v, float max_angle) {   /* sampleAngle, inc_random.compute:67-73 */
+    float phi = v * 2.0f * GL_PI, ct = 1.0f - u * (1.0f - ko_cosf(max_angle));
+    float st = sqrtf(1.0f - ct * ct);
+    return V(ko_cosf(phi) * st, ko_sinf(phi) * st, ct);
+}
+/* the (s, t, n) frame of lbb_construction.compute:42-45, and localToWorld (BSDF/header.compute:23-26) */
+static v3 gl_to_world(v3 v, v3 n) {
+    v3 s = normalize(n.y * n.y > n.x * n.x ? V(0.0f, n.z, -n.y) : V(-n.z, 0.0f, n.x));
+    v3 t = normalize(cross(n, s));
+    return vadd(vadd(vscale(s, v.x), vscale(t, v.y)), vscale(n, v.z));
+}
+/* calcLightBounce{Point,Sun,Spot,Quad} (lbb_construction.compute:35-141): the ray leaving the light */
+static ray_t gl_light_ray(const light_t* L, float a0, float a1, float b0, float b1) {
+    ray_t r;
+    if (L->kind == KHP_LIGHT_POINT) {
+        v3 n = gl_uniform_sphere(a0, a1);
+        r.o = vadd(L->position, vscale(n, L->radius));
+        r.d = gl_to_world(gl_cos_hemi(b0, b1), n);
+    } else if (L->kind == KHP_LIGHT_SUN) {
+        v3 pos = vadd(vneg(L->direction), vscale(gl_uniform_sphere(a0, a1), L->radius));
+        v3 dn = normalize(pos);
+        r.o = vadd(pos, vscale(dn, 1e16f));
+        r.d = L->direction;
+    } else if (L->kind == KHP_LIGHT_SPOT) {
+        v3 pr = gl_cos_hemi(a0, a1);
+        pr.z = 0.0f;
+        pr = vscale(pr, L->radius);
+        v3 dr = gl_sample_angle(b0, b1, L->outer * GL_DEG2RAD);
+        r.o = vadd(L->position, gl_to_world(pr, L->direction));
+        r.d = gl_to_world(dr, L->direction);
+    } else {
+        v3 x1 = vadd(L->vert[0], vscale(vsub(L->vert[1], L->vert[0]), a0));
+        v3 x2 = vadd(L->vert[3], vscale(vsub(L->vert[2], L->vert[3]), a0));
+        r.o = vadd(x1, vscale(vsub(x2, x1), a1));
+        r.d = gl_to_world(gl_cos_hemi(b0, b1), L->direction);
+    }
+    r.d = normalize(r.d);
+    return r;
+}
+/* the light's attenuation_linear / _quadratic as the GLSL light bounce carries them (0 for spot and sun) */
+static void gl_light_att(const light_t* L, float* al, float* aq) {
+    int carries = L->kind == KHP_LIGHT_POINT || L->kind == KHP_LIGHT_QUAD;
+    *al = carries ? L->l : 0.0f;
+    *aq = carries ? L->q : 0.0f;
+}
+/* angularAttenuation (inc_light.compute:207-237) */
+static float gl_ang_att(const light_t* L, v3 d) {
+    if (L->kind == KHP_LIGHT_SPOT) {
+        float ang = ko_acosf(dot(normalize(vneg(d)), L->direction)) * K_RAD2DEG;
+        return 1.0f - gclamp((ang - L->inner) / (L->outer - L->inner), 0.0f, 1.0f);
+    }
+    if (L->kind == KHP_LIGHT_QUAD) return dot(normalize(vneg(d)), L->direction);
+    return 1.0f;
+}
+
+/* One light subpath (generatePrimaryLightRays + traceLightRays + shadeLightRays,
+ * lbb_construction.compute:195-403): J vertices, the first on the light. */
+static void light_subpath(const struct ko_ctx* c, uint32_t seed, uint32_t k, uint32_t s, uint32_t li, lvert_t* out) {
+    const khp_bdpt_params* bd = &c->bd;
+    const uint32_t J = bd->vertices, L = c->n_lights;
+    const light_t* Lt = &c->lights[li];
+    const uint32_t key = lpath_key(seed, s * L + li, k);
+    memset(out, 0, sizeof(lvert_t) * J);   /* invalid vertices are all-zero records */
+    ray_t r = gl_light_ray(Lt, draw_u01(key, DIM(0, P_LIGHT_0)), draw_u01(key, DIM(0, P_LIGHT_1)),
+                           draw_u01(key, DIM(0, P_BSDF_0)), draw_u01(key, DIM(0, P_BSDF_1)));
+    out[0].valid = 1;
+    out[0].pos = r.o;
+    out[0].din = V(0.0f, 0.0f, 0.0f);
+    out[0].hc = V(GL_ONE_OVER_PI, GL_ONE_OVER_PI, GL_ONE_OVER_PI);
+    float al, aq, dist = 0.0f;
+    gl_light_att(Lt, &al, &aq);
+    for (uint32_t j = 1; j < J; ++j) {
+        hit_t h;
+        if (!bvh_closest(c, &r, &h, NULL)) return;   /* traceLightRays: no hit ends the subpath */
+        const obj_t* o = &c->obj[h.obj];
+        v3 n = obj_normal(o, &r, &h), pos = follow(&r, h.lambda);
+        const khp_material* m = &c->mats[o->mat];
+        khp_material mtx;
+        if (c->textured) {
+            float tu, tv;
+            obj_tcoord(o, &h, pos, &tu, &tv);
+            material_at(c, o->mat, tu, tv, &mtx);
+            m = &mtx;
+        }
+        shade_ctx_t sc; sc.obj = o; sc.m = m; sc.n = n;
+        dist = dist + length(vsub(pos, r.o));
+        float att = 1.0f / ((1.0f + dist * al) + (dist * dist) * aq);
+        v3 in = vneg(r.d), out_d = V(0.0f, 0.0f, 0.0f), f = V(0.0f, 0.0f, 0.0f);
+        float pdf = 0.0f;
+        int fl = 0;
+        if (!(dot(in, n) == 0.0f)) {   /* reflectance (BSDF/header.compute:48-56) */
+            float smp[2] = {draw_u01(key, DIM(j, P_BSDF_0)), draw_u01(key, DIM(j, P_BSDF_1))};
+            float hu[2] = {draw_u01(key, DIM(j, P_HAIR_ALPHA)), draw_u01(key, DIM(j, P_HAIR_BETA))};
+            int valid;
+            f = bsdf_sample(&sc, in, n, smp, hu, &out_d, &pdf, &fl, &valid);
+        }
+        v3 hc = vmul(out[j - 1].hc, f);
+        v3 w = vsub(pos, out[j - 1].pos);   /* convertDensity (:280-299), previous vertex = its position */
+        float ww = dot(w, w);
+        if (ww == 0.0f) pdf = 0.0f;
+        else pdf = pdf * fabsf(dot(n, vscale(w, sqrtf(1.0f / ww))));
+        hc = vscale(hc, gclamp(fabsf(dot(out_d, n)) * pdf, 0.0f, 1.0f));
+        if ((fl & F_EMISSIVE) == F_EMISSIVE) return;
+        if (is_zero(hc) || pdf <= bd->min_pdf || att <= 0.0001f) return;
+        out[j].valid = 1;
+        out[j].pos = pos;
+        out[j].din = r.d;
+        out[j].hc = hc;
+        r = make_ray(vadd(pos, vscale(out_d, bd->bounce_bias)), out_d);
+    }
+}
+
+/* The subpaths of sample indices [k0, k0+nk) (before the render's worker threads start). */
+static int build_light_paths(struct ko_ctx* c, uint32_t seed, uint32_t k0, uint32_t nk) {
+    const uint32_t Ns = c->bd.light_paths, L = c->n_lights, J = c->bd.vertices;
+    size_t n = (size_t)nk * Ns * L * J;
+    if (n > c->lv_cap) {
+        free(c->lv);
+        c->lv = (lvert_t*)malloc(sizeof(lvert_t) * (n ? n : 1));
+        if (!c->lv) { c->lv_cap = 0; return KHP_ENOMEM; }
+        c->lv_cap = n;
+    }
+    for (uint32_t q = 0; q < nk; ++q)
+        for (uint32_t s = 0; s < Ns; ++s)
+            for (uint32_t li = 0; li < L; ++li)
+                light_subpath(c, seed, k0 + q, s, li, c->lv + (((size_t)q * Ns + s) * L + li) * J);
+    c->lv_k0 = k0;
+    c->lv_nk = nk;
+    return KHP_OK;
+}
+
+/* pt_shade.compute:146-201: connect the hit to every valid vertex of one subpath
+ * (subpath and light chosen with the path's light-select draws).  Returns the
+ * sum of the unoccluded contributions hit_color * light colour * |cos| * f / (j + 1 + b). */
+static v3 bdpt_connect(const struct ko_ctx* c, const shade_ctx_t* s, v3 loc, const ray_t* ray, uint32_t key, uint32_t b,
+                       uint32_t k) {
+    v3 dl = V(0.0f, 0.0f, 0.0f);
+    const khp_bdpt_params* bd = &c->bd;
+    const uint32_t Ns = bd->light_paths, L = c->n_lights, J = bd->vertices;
+    if (L == 0) return dl;
+    uint32_t sp = (uint32_t)((float)Ns * draw_u01(key, DIM(b, P_LIGHT_0)));
+    uint32_t li = (uint32_t)((float)L * draw_u01(key, DIM(b, P_LIGHT_SEL)));
+    if (sp >= Ns) sp = Ns - 1;
+    if (li >= L) li = L - 1;
+    const light_t* Lt = &c->lights[li];
+    const lvert_t* v = c->lv + (((size_t)(k - c->lv_k0) * Ns + sp) * L + li) * J;
+    for (uint32_t j = 0; j < J; ++j) {
+        if (!v[j].valid) continue;
+        v3 lp = vsub(v[j].pos, vscale(v[j].din, bd->bounce_bias));
+        v3 lc = j == 0 ? vscale(Lt->color, gl_ang_att(Lt, vsub(lp, loc))) : Lt->color;
+        ray_t sh;
+        sh.o = vadd(loc, vscale(s->n, bd->bias));
+        sh.d = normalize(vsub(lp, loc));
+        float t_max = length(vsub(lp, sh.o));
+        lc = vscale(lc, fabsf(dot(sh.d, s->n)));
+        lc = vmul(lc, bsdf_eval(s, vneg(ray->d), sh.d));
+        v3 cj = vdivs(vmul(v[j].hc, lc), (float)(j + 1 + b));
+        int occ = bvh_any(c, &sh, t_max, NULL);
+        if (!occ) {   /* intersectsAnyWithLights (inc_light.compute:508-535); the sun is never hit */
+            for (uint32_t i = 0; i < c->n_lights; ++i) {
+                float t;
+                if (light_isect(&c->lights[i], &sh, &t) && (t < t_max)) { occ = 1; break; }
+            }
+        }
+        if (!occ) dl = vadd(dl, cj);
+    }
+    return dl;
+}
+
 /* One sample of one pixel: generatePrimaryRays + traceRays + traceRay + shaders
  * (CPU_PathTracer.cpp:118-209; SimpleShader.h:31-98; MarschnerHairShader.h:31-84;
  *  LightShader.h:20-25; EnvironmentShader.h:20-26). */
@@ -1502,7 +1703,8 @@ static v3 trace_sample(const struct ko_ctx* c, const khp_render_params* p, uint3
             if ((P.flags & F_CYL_T) || (P.flags & F_CYL_TR)) continue;
             v3 ev = bsdf_eval(&s, n, n);
             v3 amb = vmul(ld3(c->env.ambient), vscale(ev, K_ONE_OVER_PI));
-            v3 dl = direct_light(c, &s, loc, &ray_in, key, b);
+            v3 dl = c->bd.enabled ? bdpt_connect(c, &s, loc, &ray_in, key, b, sample)
+                                  : direct_light(c, &s, loc, &ray_in, key, b);
             v3 acc = vadd(vadd(V(0.0f, 0.0f, 0.0f), vmul(dl, P.T)), vmul(amb, P.T));
             if (is_zero(refl) || pdf <= 1E-4f || max3_lt(P.T, 0.01f)) P.T = V(0.0f, 0.0f, 0.0f);
             else {
@@ -1515,7 +1717,8 @@ static v3 trace_sample(const struct ko_ctx* c, const khp_render_params* p, uint3
             v3 emitted = ld3(m->emission);
             v3 ev = bsdf_eval(&s, n, n);
             v3 amb = vmul(ld3(c->env.ambient), vscale(ev, K_ONE_OVER_PI));
-            v3 dl = direct_light(c, &s, loc, &P.ray, key, b);
+            v3 dl = c->bd.enabled ? bdpt_connect(c, &s, loc, &P.ray, key, b, sample)
+                                  : direct_light(c, &s, loc, &P.ray, key, b);
             v3 acc = vadd(vadd(V(0.0f, 0.0f, 0.0f), vmul(dl, P.T)), vmul(amb, P.T));
             v3 out; float pdf = 0.0f; int fl = 0, valid;
             v3 refl = bsdf_sample(&s, counter, n, sample2, hu, &out, &pdf, &fl, &valid);
@@ -1628,7 +1831,7 @@ int ko_create(ko_ctx** out, const khp_scene* s) {
 
 void ko_destroy(ko_ctx* c) {
     if (!c) return;
-    free(c->obj); free(c->mats); free(c->lights); free(c->nodes); free(c->ids);
+    free(c->obj); free(c->mats); free(c->lights); free(c->nodes); free(c->ids); free(c->lv);
     for (uint32_t i = 0; i < c->n_tex; ++i) free(c->tex[i].data);
     free(c->tex); free(c->mtex);
     free(c);
@@ -1682,6 +1885,10 @@ int ko_render_rows_step(ko_ctx* c, const khp_render_params* p, int n_threads, ui
                         uint32_t ystep, float* out_rgb) {
     if (!c || !p || !out_rgb || p->width == 0 || p->height == 0 || ystep == 0) return KHP_EINVAL;
     if (y1 > p->height) y1 = p->height;
+    if (c->bd.enabled) {
+        int e = build_light_paths(c, p->seed, p->first_sample, p->spp);
+        if (e != KHP_OK) return e;
+    }
     if (n_threads < 1) n_threads = 1;
     if (n_threads > 256) n_threads = 256;
     pthread_t th[256];
@@ -1725,6 +1932,29 @@ int ko_trace_any(ko_ctx* c, uint32_t n, const float* orig, const float* dir, con
 }
 
 uint32_t ko_n_objects(ko_ctx* c) { return c->n_obj; }
+
+int ko_set_bdpt(ko_ctx* c, const khp_bdpt_params* p) {
+    if (!c || !p) return KHP_EINVAL;
+    if (p->enabled && (p->light_paths < 1 || p->light_paths > 65536 || p->vertices < 1 || p->vertices > 16))
+        return KHP_EINVAL;
+    c->bd = *p;
+    return KHP_OK;
+}
+
+/* The light subpaths of sample index k (test hook): [light_paths][n_lights][vertices]
+ * records of 10 floats: valid, pos.xyz, din.xyz, hit_color.xyz. */
+int ko_light_paths(ko_ctx* c, uint32_t seed, uint32_t k, float* out10) {
+    if (!c || !c->bd.enabled) return KHP_EINVAL;
+    int e = build_light_paths(c, seed, k, 1);
+    if (e != KHP_OK) return e;
+    size_t n = (size_t)c->bd.light_paths * c->n_lights * c->bd.vertices;
+    for (size_t i = 0; i < n; ++i) {
+        const lvert_t* v = &c->lv[i];
+        float r[10] = {(float)v->valid, v->pos.x, v->pos.y, v->pos.z, v->din.x, v->din.y, v->din.z, v->hc.x, v->hc.y, v->hc.z};
+        memcpy(out10 + 10 * i, r, sizeof(r));
+    }
+    return KHP_OK;
+}
 
 void ko_object_bounds(ko_ctx* c, float* o9) {
     for (uint32_t i = 0; i < c->n_obj; ++i) {

@@ -52,6 +52,11 @@ int ko_trace_any(ko_ctx* c, uint32_t n, const float* orig, const float* dir, con
 
 /* Structural views for parity of the flatten + build stages. */
 uint32_t ko_n_objects(ko_ctx* c);
+/* ABI 7 light-path variant (include/kirk_hip.h khp_bdpt_params); ko_light_paths:
+ * the subpaths of sample index k, [light_paths][n_lights][vertices] x
+ * (valid, pos.xyz, din.xyz, hit_color.xyz). */
+int ko_set_bdpt(ko_ctx* c, const khp_bdpt_params* p);
+int ko_light_paths(ko_ctx* c, uint32_t seed, uint32_t k, float* out10);
 /* per object: bmin.xyz, bmax.xyz, centroid.xyz (9 floats) */
 void ko_object_bounds(ko_ctx* c, float* out9);
 /* per cone: base.xyz r0 | u.xyz slope | v.xyz min_d | w.xyz max_d | base_d height (18 floats) */

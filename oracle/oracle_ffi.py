@@ -49,6 +49,8 @@ def load():
                                      P(c_float), P(c_uint64), P(c_uint64)]),
         "ko_trace_any": (c_int, [c_void_p, c_uint32, P(c_float), P(c_float), P(c_float), P(c_uint8)]),
         "ko_n_objects": (c_uint32, [c_void_p]),
+        "ko_set_bdpt": (c_int, [c_void_p, c_void_p]),
+        "ko_light_paths": (c_int, [c_void_p, c_uint32, c_uint32, P(c_float)]),
         "ko_env_color": (None, [c_void_p, P(c_float), P(c_float)]),
         "ko_tex_color": (None, [c_void_p, c_uint32, c_float, c_float, P(c_float)]),
         "ko_object_bounds": (None, [c_void_p, P(c_float)]),
@@ -118,6 +120,23 @@ class Oracle:
         if rc != 0:
             raise ValueError(f"ko_render failed ({rc})")
         return out
+
+    def set_bdpt(self, enabled=1, light_paths=256, vertices=4, bias=1e-4, bounce_bias=1e-4, min_pdf=1e-4):
+        """The light-path variant (khp_bdpt_params, ABI 7) for the following renders."""
+        from ba_pathtracing_fur_amd import native as N
+        self._bd = N.BdptParams(enabled, light_paths, vertices, bias, bounce_bias, min_pdf)
+        rc = self.lib.ko_set_bdpt(self.ptr, ctypes.addressof(self._bd))
+        if rc != 0:
+            raise ValueError(f"ko_set_bdpt failed ({rc})")
+
+    def light_paths(self, k, seed=0x4B49524B):
+        """Subpaths of sample index k: [light_paths, n_lights, vertices, 10] (valid, pos, din, hit_color)."""
+        n = self._bd.light_paths * len(self.scene.lights) * self._bd.vertices
+        out = np.zeros((n, 10), np.float32)
+        rc = self.lib.ko_light_paths(self.ptr, seed, k, _fp(out))
+        if rc != 0:
+            raise ValueError(f"ko_light_paths failed ({rc})")
+        return out.reshape(self._bd.light_paths, len(self.scene.lights), self._bd.vertices, 10)
 
     def trace_closest(self, orig, direction):
         o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
