@@ -1419,6 +1419,7 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->dump_bounce = -1;
     out->trace_kernels = 0;
     out->shade_order = 0;       // hit sorting measured, off
+    out->serial_stages = 0;
 }
 
 extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {
@@ -1436,6 +1437,7 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     if (prm->chunk_paths > ((uint64_t)1 << 31)) return fail(KHP_EINVAL, "chunk_paths must be <= 2^31");
     if (prm->trace_kernels > 2) return fail(KHP_EINVAL, "trace_kernels must be 0, 1 or 2");
     if (prm->shade_order > 1) return fail(KHP_EINVAL, "shade_order must be 0 or 1");
+    if (prm->serial_stages > 1) return fail(KHP_EINVAL, "serial_stages must be 0 or 1");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
     if (dr != KHP_OK) return dr;
@@ -2147,7 +2149,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     // of bounce b+2 reuses parity b's buffers only after shade(b+1), which
     // already waited for B(b).  Instrumented renders run everything on the
     // context stream so the per-bounce snapshots are exact.
-    const bool overlap = !stats;
+    const bool overlap = !stats && !c->prm.serial_stages;
     hipStream_t sA = overlap ? w.sA : c->stream;
     hipStream_t sB = overlap ? w.sB : c->stream;
     c->cur_bounce = -1;

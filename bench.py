@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--fuse", type=int, default=None, help="khp_ctx_params.fuse_frames (default: the library's)")
     ap.add_argument("--chunk-paths", type=int, default=None, help="khp_ctx_params.chunk_paths")
     ap.add_argument("--frames-in-flight", type=int, default=None, help="khp_ctx_params.frames_in_flight")
+    ap.add_argument("--iso-steps", type=int, default=8,
+                    help="fused passes re-run with serial_stages=1 for the isolated per-kernel rooflines (0: skip)")
     ap.add_argument("--shade-order", type=int, default=None, help="khp_ctx_params.shade_order (1: hits sorted by shading class)")
     ap.add_argument("--bdpt", default=None, metavar="PATHS,VERTICES",
                     help="light-path variant (khp_bdpt_params, SURVEY §8(f)4): not the metric's estimator")
@@ -314,6 +316,19 @@ def main():
                      "ms_per_step": round(sync_el / args.sync_check_steps * 1e3, 3), "steps": args.sync_check_steps,
                      "def": "one synchronous khp_render per pass (+ gather), no frame fusion"}
 
+    # the same fused passes with the shadow stage on the extend stream (serial_stages):
+    # no two kernels overlap, so each kernel's HIP-event time is its own -- the
+    # isolated per-kernel rooflines (k_shadow's overlapped launch time above also
+    # counts the co-running k_extend's share of the chip)
+    iso_st = None
+    if args.iso_steps > 0:
+        old_prm = ctx.set_params(serial_stages=1)
+        for _ in range(args.iso_steps):
+            step()
+        frame.sync()
+        iso_st = ctx.stats()
+        ctx.set_params(**old_prm)
+
     # roofline of the extend kernel (this rank's launches)
     rays = cnt["extend_rays"]
     alg_bytes_frame = 44 * rays + 32 * (cnt["node_visits"] + cnt["prim_tests"])
@@ -334,6 +349,28 @@ def main():
     sh_bytes_per_launch = sh_bytes_frame * nfr / sh_launches
     sh_avg_ms = sh_ms / sh_launches
     sh_achieved = sh_bytes_per_launch / (sh_avg_ms * 1e-3) / 1e9 if sh_avg_ms > 0 else 0.0
+    isolated = None
+    if iso_st is not None:
+        nfi = max(1, iso_st["frames"])
+        e_ms, s_ms = iso_st["extend_ms"], iso_st["shadow_ms"] - iso_st["shadow_finish_ms"]
+
+        def _rl(bytes_frame, ms, launches):
+            a = bytes_frame * nfi / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+            return {"ms_per_frame": round(ms / nfi, 3), "launches": launches, "achieved": round(a, 1),
+                    "frac": round(a / HBM_PEAK_GBPS, 4)}
+        isolated = {
+            "frames": nfi, "def": "the same fused progressive passes with khp_ctx_params.serial_stages = 1 "
+                                  "(one stream: no kernel overlaps another); algorithmic bytes / kernel time",
+            "device_ms_per_frame": round(iso_st["render_ms"] / nfi, 3),
+            "k_extend": _rl(alg_bytes_frame, e_ms, iso_st["extend_launches"]),
+            "k_shadow": _rl(sh_bytes_frame, s_ms, iso_st["shadow_launches"]),
+            "k_shade_ms_per_frame": round(iso_st["shade_ms"] / nfi, 3),
+            "k_shadow_finish_ms_per_frame": round(iso_st["shadow_finish_ms"] / nfi, 3),
+        }
+        isolated["k_shadow"]["records_per_s"] = round(
+            (cnt["shadow_node_visits"] + cnt["shadow_prim_tests"]) * nfi / max(1e-9, s_ms * 1e-3), 1)
+        isolated["k_extend"]["records_per_s"] = round(
+            (cnt["node_visits"] + cnt["prim_tests"]) * nfi / max(1e-9, e_ms * 1e-3), 1)
     cfg = CONFIGS[args.config]
     out = {
         "metric": METRIC if args.config == "metric" else f"Msamples/s, {cfg['what']}, {W}x{H} {spp}spp",
@@ -356,6 +393,7 @@ def main():
             "objects": n_objects, "parallelism": f"tile-sharded {args.tile}px tiles x{world}, RCCL gather",
         },
         "sync_steps": sync_line,
+        "isolated": isolated,
         "roofline": {
             "bound": "hbm",
             "kernel": "k_extend (closest-hit BVH2 traversal)",

@@ -286,6 +286,10 @@ typedef struct {
                                     first grouped by shading class (no hit / BSDF kind), a counting
                                     sort per bounce -- KIRK's GLSL template only compacts its hits
                                     (pt_sortHits.compute:17-38); measured in DESIGN.md §4            */
+    uint32_t serial_stages;      /* ABI 7: 1 = the shadow stage runs on the extend stream, so no two
+                                    kernels of a frame overlap and each kernel's timing is its own
+                                    (bench.py's isolated per-kernel rooflines); 0 (default) = two
+                                    streams, shadow stage b beside extend b+1                         */
 } khp_ctx_params;
 
 /* ---- context --------------------------------------------------------------- */

@@ -159,7 +159,7 @@ def test_chunked_and_instrumented_frames(hip_ctx, chunk):
 
 def test_params_are_validated(hip_ctx):
     for bad in (dict(fuse_frames=0), dict(fuse_frames=33), dict(frames_in_flight=4), dict(chunk_paths=100),
-                dict(trace_kernels=3), dict(shade_order=2)):
+                dict(trace_kernels=3), dict(shade_order=2), dict(serial_stages=2)):
         with pytest.raises(N.KhpError) as e:
             hip_ctx.set_params(**bad)
         assert e.value.status == N.KHP_EINVAL
@@ -184,6 +184,24 @@ def test_hit_sorting(hip_ctx, name, kw, w, h, spp, depth):
             hip_ctx.render(w, h, 1, depth, first_sample=k, async_=True)
         hip_ctx.sync()
         assert_parity(hip_ctx.read_framebuffer(w, h), want, exact=True)
+    finally:
+        hip_ctx.set_params(**old)
+
+
+def test_serial_stages(hip_ctx):
+    """serial_stages 1 (shadow stage on the extend stream; bench.py's isolated
+    timings) changes only the stream the kernels run on."""
+    sd = S.config2(64, 48, n_strands=1500)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    want = oracle_ffi.Oracle(sd).render(64, 48, 4, 5, threads=16)
+    old = hip_ctx.set_params(serial_stages=1)
+    try:
+        assert_parity(hip_ctx.render(64, 48, 4, 5), want, exact=True)
+        for k in range(4):
+            hip_ctx.render(64, 48, 1, 5, first_sample=k, async_=True)
+        hip_ctx.sync()
+        assert_parity(hip_ctx.read_framebuffer(64, 48), want, exact=True)
     finally:
         hip_ctx.set_params(**old)
 
