@@ -162,6 +162,13 @@ class Context {
         return p;
     }
     void set_params(const khp_ctx_params& p) { check(khp_set_params(c_, &p), "khp_set_params"); }
+    // ABI 7: the light-path variant (KIRK's GLSL lbb_construction / pt_shade bidirectional mode)
+    khp_bdpt_params bdpt() {
+        khp_bdpt_params p{};
+        check(khp_get_bdpt(c_, &p), "khp_get_bdpt");
+        return p;
+    }
+    void set_bdpt(const khp_bdpt_params& p) { check(khp_set_bdpt(c_, &p), "khp_set_bdpt"); }
     void render(const khp_render_params& p, float* out_rgb = nullptr) {
         check(khp_render(c_, &p, out_rgb), "khp_render");
     }
