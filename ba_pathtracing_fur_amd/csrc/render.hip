@@ -70,8 +70,9 @@ struct Wave {
     // Per-path state, one 16-B record per array so that k_shade and
     // k_shadow_finish, which reach paths in queue order (scattered pids after
     // bounce 0), touch one line per array instead of one per component:
-    float4* TF;          // throughput T.xyz, BSDF flags (bits) in w
-    float4* CK;          // colour C.xyz, RNG key (bits) in w
+    float4* TFq[2];      // per queue slot (moves with the path's ray): throughput T.xyz, BSDF flags (bits) in w
+    float4* CKq[2];      // per queue slot: colour C.xyz, RNG key (bits) in w
+    float4* CK;          // per path: the final colour, written when the path ends (k_accumulate reads it)
     uint8_t* vis;        // shadow-ray occlusion flag per shadow record (this parity)
     ShadowQ* shq;        // shadow queue of this parity
     float4* sh;          // 6 float4 per shadow record
@@ -174,8 +175,9 @@ __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
     Wv.qo[0][0][pid] = r.o.x; Wv.qo[0][1][pid] = r.o.y; Wv.qo[0][2][pid] = r.o.z;
     Wv.qd[0][0][pid] = r.d.x; Wv.qd[0][1][pid] = r.d.y; Wv.qd[0][2][pid] = r.d.z;
     Wv.qpid[0][pid] = pid;
-    Wv.TF[pid] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));
-    Wv.CK[pid] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));
+    Wv.TFq[0][pid] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));  // queue slot = path at bounce 0
+    Wv.CKq[0][pid] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));
+    if (Wv.depth == 0) Wv.CK[pid] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));  // no bounce writes it
 }
 
 __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
@@ -667,7 +669,8 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
         float sh_tmax = 0.0f;
         v3 lc = mk(0, 0, 0), Told = mk(0, 0, 0), AT = mk(0, 0, 0), ET = mk(0, 0, 0);
         bool has_emit = false;
-        bool deferred = false;  // BD: the colour add is left to the connection group's finish
+        uint32_t bd_head = 0xFFFFFFFFu;  // BD: the group's head record (its rec[4] is written with the destination)
+        float4 tfo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cko = tfo;  // the path state after this bounce
         if (active) {
             pid = Wv.qpid[cur][i];
             Ray r;
@@ -675,7 +678,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
             r.d = mk(Wv.qd[cur][0][i], Wv.qd[cur][1][i], Wv.qd[cur][2][i]);
             float lambda = Wv.ht[i];
             int32_t slot = Wv.hslot[i];
-            const float4 tf = Wv.TF[pid], ck = Wv.CK[pid];
+            const float4 tf = Wv.TFq[cur][i], ck = Wv.CKq[cur][i];
             v3 T = mk(tf.x, tf.y, tf.z);
             v3 C = mk(ck.x, ck.y, ck.z);
             int flags = (int)bits_from_f(tf.w);
@@ -834,8 +837,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                         v3 acc = (mk(0, 0, 0) + mk(0, 0, 0) * Told) + AT;
                         if (has_emit) acc = acc + ET;
                         C = C + acc;
-                    } else {
-                        deferred = true;
+                    } else {  // the colour add is left to the group's finish
                         const BdptDev& bd = Wv.bd;
                         uint32_t o = wave_alloc_n(nv, &Wv.shq->nsh);
                         bool head = true;
@@ -852,7 +854,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                             rec[2] = make_float4(cj.x, cj.y, cj.z, has_emit ? 1.0f : 0.0f);
                             rec[3] = make_float4(Told.x, Told.y, Told.z, head ? (float)nv : 0.0f);
                             if (head) {
-                                rec[4] = make_float4(AT.x, AT.y, AT.z, 0.0f);
+                                bd_head = o - 1u;
                                 if (has_emit) rec[5] = make_float4(ET.x, ET.y, ET.z, 0.0f);
                             }
                             head = false;
@@ -877,8 +879,10 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                     }
                 }
             }
-            Wv.TF[pid] = make_float4(T.x, T.y, T.z, f_from_bits((uint32_t)flags));
-            if (!emit_sh && !deferred) Wv.CK[pid] = make_float4(C.x, C.y, C.z, ck.w);
+            // (with a deferred add -- emit_sh or a BD group -- C is unchanged here and the
+            // shadow finish adds this bounce's term to wherever the state goes)
+            tfo = make_float4(T.x, T.y, T.z, f_from_bits((uint32_t)flags));
+            cko = make_float4(C.x, C.y, C.z, ck.w);
             emit_ray = !last && !is_zero(T) && !is_zero(nr.d);
         }
         uint32_t qi, si;
@@ -886,10 +890,18 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                      &Wv.cnt->nq[nxt], &Wv.cnt->nqb[nxt], &Wv.shq->nsh, &Wv.shq->nshb, balloc, qi, si);
         qi = heavy ? qi : Wv.cap - 1u - qi;
         si = heavy ? si : Wv.cap - 1u - si;
+        // The path state moves with the ray: to the next queue slot (coalesced
+        // with the ray's own columns), or, when the path ends, to its final
+        // colour CK[pid].  A deferred colour add is told where the state went.
+        const uint32_t dest = emit_ray ? qi : (0x80000000u | pid);
         if (emit_ray) {
             Wv.qo[nxt][0][qi] = nr.o.x; Wv.qo[nxt][1][qi] = nr.o.y; Wv.qo[nxt][2][qi] = nr.o.z;
             Wv.qd[nxt][0][qi] = nr.d.x; Wv.qd[nxt][1][qi] = nr.d.y; Wv.qd[nxt][2][qi] = nr.d.z;
             Wv.qpid[nxt][qi] = pid;
+            Wv.TFq[nxt][qi] = tfo;
+            Wv.CKq[nxt][qi] = cko;
+        } else if (active) {
+            Wv.CK[pid] = cko;
         }
         if (emit_sh) {
             float4* rec = Wv.sh + 6 * (size_t)si;
@@ -897,9 +909,10 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
             rec[1] = make_float4(shr.d.x, shr.d.y, shr.d.z, f_from_bits(pid));
             rec[2] = make_float4(lc.x, lc.y, lc.z, has_emit ? 1.0f : 0.0f);
             rec[3] = make_float4(Told.x, Told.y, Told.z, 0.0f);
-            rec[4] = make_float4(AT.x, AT.y, AT.z, 0.0f);
+            rec[4] = make_float4(AT.x, AT.y, AT.z, f_from_bits(dest));
             if (has_emit) rec[5] = make_float4(ET.x, ET.y, ET.z, 0.0f);
         }
+        if (BD && bd_head != 0xFFFFFFFFu) Wv.sh[6 * (size_t)bd_head + 4] = make_float4(AT.x, AT.y, AT.z, f_from_bits(dest));
     }
 }
 
@@ -908,7 +921,12 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
 // k_shadow_finish: one shadow record per lane, streaming; kept out of the
 // traversal kernel so k_shadow's registers go to traversal only.
 // The light occlusion loop and colour add of one shadow record (SimpleShader.h:131-148).
-__device__ __forceinline__ void shadow_finish_one(const DevScene& S, const Wave& Wv, uint32_t i, bool occ) {
+// Where shade left a path's state: the next queue slot (parity nxt), or, high bit set, the final colour of path i.
+__device__ __forceinline__ float4* state_dest(const Wave& Wv, int nxt, uint32_t dest) {
+    return (dest & 0x80000000u) ? Wv.CK + (dest & 0x7FFFFFFFu) : Wv.CKq[nxt] + dest;
+}
+
+__device__ __forceinline__ void shadow_finish_one(const DevScene& S, const Wave& Wv, int nxt, uint32_t i, bool occ) {
     {
         const float4* rec = Wv.sh + 6 * (size_t)i;
         float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3], e = rec[4];
@@ -933,15 +951,17 @@ __device__ __forceinline__ void shadow_finish_one(const DevScene& S, const Wave&
             float4 f = rec[5];
             acc = acc + mk(f.x, f.y, f.z);
         }
-        const float4 ck = Wv.CK[pid];
-        Wv.CK[pid] = make_float4(ck.x + acc.x, ck.y + acc.y, ck.z + acc.z, ck.w);
+        (void)pid;
+        float4* dst = state_dest(Wv, nxt, bits_from_f(e.w));
+        const float4 ck = *dst;
+        *dst = make_float4(ck.x + acc.x, ck.y + acc.y, ck.z + acc.z, ck.w);
     }
 }
 
 // BD: the records of a light-path connection group (one path, one bounce) are
 // consecutive in the front part; the head (rec[3].w = group size) adds the
 // unoccluded contributions in vertex order (the oracle's bdpt_connect).
-__device__ __forceinline__ void connection_group_finish(const DevScene& S, const Wave& Wv, uint32_t i) {
+__device__ __forceinline__ void connection_group_finish(const DevScene& S, const Wave& Wv, int nxt, uint32_t i) {
     const float4* rec = Wv.sh + 6 * (size_t)i;
     const float4 d = rec[3];
     if (d.w == 0.0f) return;  // not a group head
@@ -972,18 +992,20 @@ __device__ __forceinline__ void connection_group_finish(const DevScene& S, const
         const float4 f = rec[5];
         acc = acc + mk(f.x, f.y, f.z);
     }
-    const float4 ck = Wv.CK[pid];
-    Wv.CK[pid] = make_float4(ck.x + acc.x, ck.y + acc.y, ck.z + acc.z, ck.w);
+    (void)pid;
+    float4* dst = state_dest(Wv, nxt, bits_from_f(e.w));
+    const float4 ck = *dst;
+    *dst = make_float4(ck.x + acc.x, ck.y + acc.y, ck.z + acc.z, ck.w);
 }
 
 template <bool BD>
-__global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv) {
+__global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv, int nxt) {
     const uint32_t nf = Wv.shq->nsh, n = nf + Wv.shq->nshb;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&Wv.cnt->sh_rays, (unsigned long long)n);
     for (uint32_t iv = blockIdx.x * blockDim.x + threadIdx.x; iv < n; iv += gridDim.x * blockDim.x) {
         const uint32_t i = q_phys(iv, nf, Wv.cap);
-        if (BD) connection_group_finish(S, Wv, i);
-        else shadow_finish_one(S, Wv, i, Wv.vis[i] != 0);
+        if (BD) connection_group_finish(S, Wv, nxt, i);
+        else shadow_finish_one(S, Wv, nxt, i, Wv.vis[i] != 0);
     }
 }
 
@@ -1293,7 +1315,7 @@ struct TimedLaunch {
 // extend / shade / accumulate; B: the shadow stage).
 struct PathSet {
     size_t cap = 0;
-    DevMem qbuf[2][7], ht, hslot, hu, hv, TFb, CKb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
+    DevMem qbuf[2][7], ht, hslot, hu, hv, TFq[2], CKq[2], CKb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
     DevMem heavyb;
     DevMem permb, hkeyb, hclsb;   // shade_order 1
     DevMem lvb;                   // light-path variant: subpath vertices of a chunk's sample slots
@@ -1302,7 +1324,7 @@ struct PathSet {
 };
 // Device bytes per path of a PathSet (ensure_wave): 2 x 7 queue columns, hit
 // t/slot/u/v, TF + CK records, heavy flag, 2 x (occlusion flag + 96-B shadow record).
-constexpr size_t PATH_BYTES = 2 * 7 * 4 + 4 * 4 + 2 * 16 + 1 + 2 * (1 + 6 * 16) + 4 + 1;
+constexpr size_t PATH_BYTES = 2 * 7 * 4 + 4 * 4 + 5 * 16 + 1 + 2 * (1 + 6 * 16) + 4 + 1;
 
 #ifndef KHP_MAX_INFLIGHT
 #define KHP_MAX_INFLIGHT 3
@@ -1775,7 +1797,10 @@ static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap, size_t sh_per_
     HIPCHK(w.hslot.ensure(cap * 4));
     HIPCHK(w.hu.ensure(cap * 4));
     HIPCHK(w.hv.ensure(cap * 4));
-    HIPCHK(w.TFb.ensure(cap * sizeof(float4)));
+    for (int q = 0; q < 2; ++q) {
+        HIPCHK(w.TFq[q].ensure(cap * sizeof(float4)));
+        HIPCHK(w.CKq[q].ensure(cap * sizeof(float4)));
+    }
     HIPCHK(w.CKb.ensure(cap * sizeof(float4)));
     HIPCHK(w.heavyb.ensure(cap));
     HIPCHK(w.permb.ensure(cap * 4));
@@ -1814,7 +1839,10 @@ static Wave wave_view(const khp_ctx* c, PathSet& w) {
     Wv.hslot = w.hslot.as<int32_t>();
     Wv.hu = w.hu.as<float>();
     Wv.hv = w.hv.as<float>();
-    Wv.TF = w.TFb.as<float4>();
+    for (int q = 0; q < 2; ++q) {
+        Wv.TFq[q] = w.TFq[q].as<float4>();
+        Wv.CKq[q] = w.CKq[q].as<float4>();
+    }
     Wv.CK = w.CKb.as<float4>();
     Wv.vis = w.visb[0].as<uint8_t>();
     Wv.sh = w.shb[0].as<float4>();
@@ -2275,8 +2303,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     hipLaunchKernelGGL(k_shadow<false>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sB, c->S, Wb, sp_sh);
                 timed(c, f, 2, false, sB);
                 timed(c, f, 4, true, sB);   // shadow stage = any-hit traversal + finish
-                if (bdm) hipLaunchKernelGGL(k_shadow_finish<true>, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
-                else hipLaunchKernelGGL(k_shadow_finish<false>, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb);
+                if (bdm) hipLaunchKernelGGL(k_shadow_finish<true>, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb, cur ^ 1);
+                else hipLaunchKernelGGL(k_shadow_finish<false>, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb, cur ^ 1);
                 timed(c, f, 4, false, sB);
                 if (sB != sA) {
                     done_b = slot_event(f.sync_pool, f.sync_next, true);

@@ -16,5 +16,5 @@ t = sys.argv[1]
 for k in ("A1", "B1", "A2", "B2"):
     d = json.loads(open(f"gpurun_out/ab_{t}_{k}.json").read().strip().splitlines()[-1])
     f = d["frame"]
-    print(k, d["value"], "sync", d.get("sync_steps", {}).get("value"), "shade_ms", f["shade_ms"], "ext", f["extend_ms"], "dev", f["device_ms"])
+    print(k, d["value"], "sync", (d.get("sync_steps") or {}).get("value"), "shade_ms", f["shade_ms"], "ext", f["extend_ms"], "dev", f["device_ms"])
 PY
