@@ -142,6 +142,28 @@ def test_bdpt_frame_parity(hip_ctx, name, kw, w, h, spp, depth, ns, nv):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_bdpt_tile_shards(hip_ctx, nranks):
+    """Each rank's tiles of a variant frame equal the full frame's pixels (subpaths
+    are keyed by sample index, not by rank)."""
+    from ba_pathtracing_fur_amd import sharding
+    sd = S.config2(64, 40, n_strands=800)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    o = oracle_ffi.Oracle(sd)
+    o.set_bdpt(light_paths=16, vertices=4)
+    full = o.render(64, 40, 2, 5, threads=16)
+    old = hip_ctx.set_bdpt(enabled=1, light_paths=16, vertices=4)
+    try:
+        for r in range(nranks):
+            got = hip_ctx.render(64, 40, 2, 5, tile_size=16, tile_rank=r, tile_nranks=nranks)
+            m = sharding.owned_mask(64, 40, r, nranks, 16)
+            assert_parity(got[m][None], full[m][None], exact=True)
+    finally:
+        hip_ctx.set_bdpt(**old)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("path", FIXTURES, ids=IDS)
 def test_product_reproduces_bdpt_fixture(path, hip_ctx):
     sd, a = _load(path)
