@@ -340,7 +340,7 @@ def main():
     per_launch = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     achieved = (bytes_per_launch * ext_launches) / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
     frames_per_launch = nfr * launches_frame / max(1, ext_launches)
-    traffic = pmc_traffic(frames_per_launch, args.config)
+    traffic = None if args.bdpt else pmc_traffic(frames_per_launch, args.config)  # profiles are of the default estimator
     # the any-hit kernel (k_shadow alone; the finish is a separate streaming kernel)
     sh_rays = cnt["shadow_rays"]
     sh_bytes_frame = 32 * sh_rays + 32 * (cnt["shadow_node_visits"] + cnt["shadow_prim_tests"])
