@@ -595,14 +595,10 @@ __device__ __forceinline__ v3 hair_r(const ShadeCtx& s, v3 in, v3 n, float sampl
 
 // BSDF::sample (Bsdf.cpp:179-184) + localSample dispatch; valid=false on the
 // `dot(ray_in, normal) == 0` early exit.
-#ifndef KHP_BSDF_INLINE
-#define KHP_BSDF_INLINE 0
-#endif
-#if KHP_BSDF_INLINE
+// Inlined into k_shade: measured 2.02 -> 1.66 ms per frame against a real call
+// (whose frame spilled 41 SGPRs and 112 B of scratch), +0.7% at the metric row
+// (profiles/r02p_bsdf_inline.json).
 __device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
 v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float h1, v3& out,
                                        float& pdf, int& flags, bool& valid) {
     v3 zero = mk(0.0f, 0.0f, 0.0f);
