@@ -47,12 +47,15 @@ def main():
         for r in ranks:
             kw = dict(seed=0x4B49524B, tile_size=a.tile, tile_rank=r, tile_nranks=n, readback=False,
                       async_=not a.sync_steps)
-            ctx.render(W, H, spp, depth, **kw)  # warmup
-            ctx.render(W, H, spp, depth, **kw)
+            k = 0  # progressive passes, as bench.py: pass k renders samples [k*spp, (k+1)*spp)
+            for _ in range(a.steps):  # warmup (allocations, a full fused batch)
+                ctx.render(W, H, spp, depth, first_sample=k * spp, **kw)
+                k += 1
             ctx.sync()
             t0 = time.perf_counter()
             for _ in range(a.steps):
-                ctx.render(W, H, spp, depth, **kw)
+                ctx.render(W, H, spp, depth, first_sample=k * spp, **kw)
+                k += 1
             ctx.sync()
             per[r] = (time.perf_counter() - t0) / a.steps * 1e3
             print(f"N={n} rank {r}: {per[r]:.3f} ms/frame", file=sys.stderr, flush=True)
