@@ -20,9 +20,12 @@ constexpr float GL_ONE_OVER_PI = 0.31830988618f;  // inc_random.compute:12
 constexpr float GL_DEG2RAD = 0.01745329251994329577f;
 constexpr uint32_t LPATH_SEED = 0x4C504154u;      // light-path RNG: path_key(seed ^ LPATH_SEED, s * L + light, k)
 
+constexpr uint32_t IMG_BOUNCE = 4095u;            // draw dims of the image-plane pass: bounce slot 4095
+
 struct BdptDev {
     uint32_t on, Ns, L, J;
     float bias, bounce_bias, min_pdf;
+    uint32_t img;      // shadeBDPTImagePlane pass on
     const float4* lv;  // [sample slot][Ns][L][J] x 3 float4: (pos, valid) (din, 0) (hit colour, 0)
 };
 

@@ -485,6 +485,73 @@ __global__ __launch_bounds__(64) void k_light_paths(DevScene S, Wave Wv) {
     }
 }
 
+// shadeBDPTImagePlane (pt_shade.compute:17-97; the oracle's bdpt_image_plane):
+// every path connects the vertices of one subpath to its own point on the
+// sensor before bounce 0.  The connections are a group of shadow records like
+// k_shade's (Told = 1, no ambient: the finish adds exactly their sum) whose
+// destination is the path's state at bounce 0 (queue slot = path).  Runs on
+// the shadow buffers of parity 1, which bounce 0 does not use.
+__global__ __launch_bounds__(256) void k_img_connect(DevScene S, Wave Wv) {
+    const BdptDev& bd = Wv.bd;
+    const uint32_t per_frame = Wv.P * Wv.n_samples;
+    const uint32_t pid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pid >= per_frame * Wv.n_frames) return;
+    const uint32_t fr = pid / per_frame, pf = pid - fr * per_frame;
+    const uint32_t p_local = pf / Wv.n_samples, s_local = pf - p_local * Wv.n_samples;
+    const uint32_t pixel = Wv.pix[Wv.p_off + p_local];
+    const uint32_t x = pixel % Wv.W, y = pixel / Wv.W;
+    const uint32_t key = path_key(Wv.seed, pixel, Wv.fsample0[fr] + s_local);
+    const khp_camera& cam = S.cam;
+    const float u1 = draw_u01(key, dim_of(0, P_CAM_X)), u2 = draw_u01(key, dim_of(0, P_CAM_Y));
+    const float s1 = ((float)x + u1) * cam.pixel_size, s2 = ((float)y + u2) * cam.pixel_size;
+    const v3 sensor = (ld3(cam.bottom_left) + ld3(cam.axis_x) * s1) + ld3(cam.axis_y) * s2;
+    uint32_t sp = (uint32_t)((float)bd.Ns * draw_u01(key, dim_of(IMG_BOUNCE, P_LIGHT_0)));
+    uint32_t li = (uint32_t)((float)bd.L * draw_u01(key, dim_of(IMG_BOUNCE, P_LIGHT_SEL)));
+    sp = sp < bd.Ns ? sp : bd.Ns - 1u;
+    li = li < bd.L ? li : bd.L - 1u;
+    const v3 axs = ld3(cam.axis_x) * cam.pixel_size, ays = ld3(cam.axis_y) * cam.pixel_size;
+    const float a = length(cross(ays * (float)Wv.H, axs * (float)Wv.W));
+    const v3 cn = normalize(cross(ays, axs));
+    const uint32_t q = fr * Wv.n_samples + s_local;
+    const float4* lv = bd.lv + 3 * ((((size_t)q * bd.Ns + sp) * bd.L + li) * bd.J);
+    // two passes over the vertices: count the non-zero terms, then write the group
+    uint32_t nv = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        uint32_t o = 0;
+        if (pass == 1) {
+            if (nv == 0) return;
+            o = wave_alloc_n(nv, &Wv.shq->nsh);
+        }
+        bool head = true;
+        for (uint32_t j = 0; j < bd.J; ++j) {
+            const float4 pv = lv[3 * j];
+            if (pv.w == 0.0f) continue;
+            const float4 din = lv[3 * j + 1], hc = lv[3 * j + 2];
+            const v3 lp = mk(pv.x, pv.y, pv.z) - mk(din.x, din.y, din.z) * bd.bounce_bias;
+            const v3 d = lp - sensor;
+            const float t = length(d);
+            const v3 dir = normalize(d);
+            const float ct = dot(cn, dir);
+            float we = 1.0f / ((((a * ct) * ct) * ct) * ct);
+            const float npdf = (t * t) / fabsf(dot(cn, dir));
+            if (ct <= 0.0f) we = 0.0f;
+            const v3 cj = ((mk(hc.x, hc.y, hc.z) * we) / npdf) / (float)(j + 1);
+            if (cj.x == 0.0f && cj.y == 0.0f && cj.z == 0.0f) continue;  // cannot change the sum
+            if (pass == 0) {
+                ++nv;
+                continue;
+            }
+            float4* rec = Wv.sh + 6 * (size_t)o++;
+            rec[0] = make_float4(sensor.x, sensor.y, sensor.z, t);
+            rec[1] = make_float4(dir.x, dir.y, dir.z, f_from_bits(pid));
+            rec[2] = make_float4(cj.x, cj.y, cj.z, 0.0f);
+            rec[3] = make_float4(1.0f, 1.0f, 1.0f, head ? (float)nv : 0.0f);
+            if (head) rec[4] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(pid));  // destination: queue slot pid, parity 0
+            head = false;
+        }
+    }
+}
+
 // One connection of a camera hit to vertex j of its chosen subpath
 // (pt_shade.compute:150-199; the oracle's bdpt_connect): the connection ray
 // and the contribution it adds when unoccluded.  Returns false for an invalid vertex.
@@ -1477,6 +1544,7 @@ extern "C" void khp_bdpt_params_defaults(khp_bdpt_params* out) {
     out->bias = 1e-4f;         // the GLSL's 1e-4 bounce bias (pt_shade.compute:269)
     out->bounce_bias = 1e-4f;
     out->min_pdf = 1e-4f;      // SimpleShader's pdf <= 1E-4 cut (SimpleShader.h)
+    out->image_plane = 1;      // both GLSL passes: shadeBDPTImagePlane and the hit connections
 }
 
 extern "C" khp_status khp_get_bdpt(khp_ctx* c, khp_bdpt_params* out) {
@@ -2208,7 +2276,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     Wv.seed = p->seed;
     Wv.depth = p->depth;
     Wv.bd = BdptDev{bdm ? 1u : 0u, c->bd.light_paths, (uint32_t)c->S.n_lights, c->bd.vertices, c->bd.bias,
-                    c->bd.bounce_bias, c->bd.min_pdf, bdm ? w.lvb.as<float4>() : nullptr};
+                    c->bd.bounce_bias, c->bd.min_pdf, c->bd.image_plane ? 1u : 0u,
+                    bdm ? w.lvb.as<float4>() : nullptr};
     SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
     SpillArea sp_sh{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
     for (uint32_t p0 = 0; p0 < P_all; p0 += P_chunk) {
@@ -2229,6 +2298,23 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 hipLaunchKernelGGL(k_light_paths, dim3((nsub + 63) / 64), dim3(64), 0, sA, c->S, Wv);
             }
             timed(c, f, 3, false, sA);
+            if (bdm && c->bd.image_plane) {
+                // shadeBDPTImagePlane before bounce 0, all on stream A: connection groups
+                // on the parity-1 shadow buffers, traced, and added to the bounce-0 state
+                Wave Wi = Wv;
+                Wi.sh = w.shb[1].as<float4>();
+                Wi.vis = w.visb[1].as<uint8_t>();
+                Wi.shq = w.shqb.as<ShadowQ>() + 1;
+                HIPCHK(hipMemsetAsync(Wi.shq, 0, sizeof(ShadowQ), sA));
+                hipLaunchKernelGGL(k_img_connect, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wi);
+                timed(c, f, 2, true, sA);
+                if (stats)
+                    hipLaunchKernelGGL(k_shadow<true>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wi, sp_sh);
+                else
+                    hipLaunchKernelGGL(k_shadow<false>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wi, sp_sh);
+                timed(c, f, 2, false, sA);
+                hipLaunchKernelGGL(k_shadow_finish<true>, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wi, 0);
+            }
             hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
             for (uint32_t b = 0; b < p->depth; ++b) {
                 const int cur = b & 1;

@@ -130,7 +130,7 @@ class CtxParams(ctypes.Structure):
 class BdptParams(ctypes.Structure):
     """khp_bdpt_params (ABI 7): the light-path (bidirectional) variant, SURVEY §8(f)4."""
     _fields_ = [("enabled", c_uint32), ("light_paths", c_uint32), ("vertices", c_uint32), ("bias", c_float),
-                ("bounce_bias", c_float), ("min_pdf", c_float)]
+                ("bounce_bias", c_float), ("min_pdf", c_float), ("image_plane", c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

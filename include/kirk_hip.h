@@ -333,8 +333,10 @@ typedef struct {
     float bias;             /* debug.bias: connection-ray origin offset along the normal         */
     float bounce_bias;      /* debug.bounce_bias: light-ray origin offset and vertex pull-back   */
     float min_pdf;          /* debug.min_pdf: a light vertex with pdf <= min_pdf ends its subpath */
+    uint32_t image_plane;   /* 1: also connect each sample's light vertices to its point on the
+                               sensor (shadeBDPTImagePlane, pt_shade.compute:17-97)           */
 } khp_bdpt_params;
-void khp_bdpt_params_defaults(khp_bdpt_params* out);   /* off; 256 paths, 4 vertices, 1e-4 x 3 */
+void khp_bdpt_params_defaults(khp_bdpt_params* out);   /* off; 256 paths, 4 vertices, 1e-4 x 3, image plane on */
 khp_status khp_set_bdpt(khp_ctx* ctx, const khp_bdpt_params* params);
 khp_status khp_get_bdpt(khp_ctx* ctx, khp_bdpt_params* out);
 

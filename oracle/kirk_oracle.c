@@ -1590,6 +1590,50 @@ static int build_light_paths(struct ko_ctx* c, uint32_t seed, uint32_t k0, uint3
     return KHP_OK;
 }
 
+/* shadeBDPTImagePlane (pt_shade.compute:17-97): connect every valid vertex of one
+ * subpath (chosen with the sample's own draws at dims IMG_DIM) to the sample's
+ * point on the sensor; the unoccluded importance-weighted terms, summed in
+ * vertex order, are the path's first colour add. */
+#define IMG_BOUNCE 4095u
+static v3 bdpt_image_plane(const struct ko_ctx* c, uint32_t W, uint32_t H, v3 sensor, uint32_t key, uint32_t k) {
+    v3 dl = V(0.0f, 0.0f, 0.0f);
+    const khp_bdpt_params* bd = &c->bd;
+    const uint32_t Ns = bd->light_paths, L = c->n_lights, J = bd->vertices;
+    uint32_t sp = (uint32_t)((float)Ns * draw_u01(key, DIM(IMG_BOUNCE, P_LIGHT_0)));
+    uint32_t li = (uint32_t)((float)L * draw_u01(key, DIM(IMG_BOUNCE, P_LIGHT_SEL)));
+    if (sp >= Ns) sp = Ns - 1;
+    if (li >= L) li = L - 1;
+    const khp_camera* cam = &c->cam;
+    v3 axs = vscale(ld3(cam->axis_x), cam->pixel_size), ays = vscale(ld3(cam->axis_y), cam->pixel_size);
+    float a = length(cross(vscale(ays, (float)H), vscale(axs, (float)W)));   /* sensor area */
+    v3 cn = normalize(cross(ays, axs));                                        /* camera normal */
+    const lvert_t* v = c->lv + (((size_t)(k - c->lv_k0) * Ns + sp) * L + li) * J;
+    for (uint32_t j = 0; j < J; ++j) {
+        if (!v[j].valid) continue;
+        v3 lp = vsub(v[j].pos, vscale(v[j].din, bd->bounce_bias));
+        v3 d = vsub(lp, sensor);
+        float t = length(d);
+        ray_t vis;
+        vis.o = sensor;
+        vis.d = normalize(d);
+        float ct = dot(cn, vis.d);
+        float we = 1.0f / ((((a * ct) * ct) * ct) * ct);
+        float npdf = (t * t) / fabsf(dot(cn, vis.d));
+        if (ct <= 0.0f) we = 0.0f;
+        v3 cj = vdivs(vdivs(vscale(v[j].hc, we), npdf), (float)(j + 1));
+        int occ = bvh_any(c, &vis, t, NULL);
+        if (!occ) {
+            for (uint32_t i = 0; i < c->n_lights; ++i) {
+                float tl;
+                if (light_isect(&c->lights[i], &vis, &tl) && (tl < t)) { occ = 1; break; }
+            }
+        }
+        if (!occ) dl = vadd(dl, cj);
+    }
+    /* added like a connection group's term: (0 + dl * 1) + 0 */
+    return vadd(vadd(V(0.0f, 0.0f, 0.0f), vmul(dl, V(1.0f, 1.0f, 1.0f))), V(0.0f, 0.0f, 0.0f));
+}
+
 /* pt_shade.compute:146-201: connect the hit to every valid vertex of one subpath
  * (subpath and light chosen with the path's light-select draws).  Returns the
  * sum of the unoccluded contributions hit_color * light colour * |cos| * f / (j + 1 + b). */
@@ -1644,6 +1688,10 @@ static v3 trace_sample(const struct ko_ctx* c, const khp_render_params* p, uint3
     P.T = V(1.0f, 1.0f, 1.0f);
     P.color = V(0.0f, 0.0f, 0.0f);
     P.flags = 0;
+    if (c->bd.enabled && c->bd.image_plane && c->n_lights > 0) {
+        v3 sensor = vadd(vadd(ld3(cam->bottom_left), vscale(ld3(cam->axis_x), s1)), vscale(ld3(cam->axis_y), s2));
+        P.color = vadd(P.color, bdpt_image_plane(c, p->width, p->height, sensor, key, sample));
+    }
     for (uint32_t b = 0; b < p->depth; ++b) {
         if (is_zero(P.T)) break;
         if (is_zero(P.ray.d)) break;   /* traceRay lambda=-1 guard (CPU_PathTracer.cpp:172-174); unreachable */

@@ -121,10 +121,11 @@ class Oracle:
             raise ValueError(f"ko_render failed ({rc})")
         return out
 
-    def set_bdpt(self, enabled=1, light_paths=256, vertices=4, bias=1e-4, bounce_bias=1e-4, min_pdf=1e-4):
+    def set_bdpt(self, enabled=1, light_paths=256, vertices=4, bias=1e-4, bounce_bias=1e-4, min_pdf=1e-4,
+                 image_plane=1):
         """The light-path variant (khp_bdpt_params, ABI 7) for the following renders."""
         from ba_pathtracing_fur_amd import native as N
-        self._bd = N.BdptParams(enabled, light_paths, vertices, bias, bounce_bias, min_pdf)
+        self._bd = N.BdptParams(enabled, light_paths, vertices, bias, bounce_bias, min_pdf, image_plane)
         rc = self.lib.ko_set_bdpt(self.ptr, ctypes.addressof(self._bd))
         if rc != 0:
             raise ValueError(f"ko_set_bdpt failed ({rc})")

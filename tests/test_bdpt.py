@@ -1,6 +1,6 @@
 """The light-path (bidirectional) variant, khp_bdpt_params (ABI 7).
 
-KIRK's GLSL lbb_construction.compute:195-403 / pt_shade.compute:146-201 is
+KIRK's GLSL lbb_construction.compute:195-403 / pt_shade.compute:17-97, 146-201 is
 never run by KIRK (dead GPU path) and ships no outputs: parity is
 unpinned by the reference.  The oracle's restatement (oracle/kirk_oracle.c
 light_subpath / bdpt_connect) is pinned by the invariants below and frozen by
@@ -92,7 +92,7 @@ def test_bdpt_params_struct():
     lib = N.load_library()
     p = N.BdptParams()
     lib.khp_bdpt_params_defaults(p)
-    assert p.as_dict()["enabled"] == 0 and p.light_paths == 256 and p.vertices == 4
+    assert p.as_dict()["enabled"] == 0 and p.light_paths == 256 and p.vertices == 4 and p.image_plane == 1
     assert abs(p.bias - 1e-4) < 1e-9 and abs(p.bounce_bias - 1e-4) < 1e-9 and abs(p.min_pdf - 1e-4) < 1e-9
 
 
@@ -139,6 +139,35 @@ def test_bdpt_frame_parity(hip_ctx, name, kw, w, h, spp, depth, ns, nv):
     # off again: KIRK's next-event estimate
     assert_parity(hip_ctx.render(w, h, spp, depth), oracle_ffi.Oracle(sd).render(w, h, spp, depth, threads=16),
                   exact=True)
+
+
+@pytest.mark.gpu
+def test_bdpt_without_image_plane(hip_ctx):
+    """image_plane = 0: only the hit connections (pt_shade.compute:146-201)."""
+    sd = S.build_config("zoo", width=40, height=30, n_strands=300)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    o = oracle_ffi.Oracle(sd)
+    o.set_bdpt(light_paths=16, vertices=4, image_plane=0)
+    want = o.render(40, 30, 2, 6, threads=16)
+    old = hip_ctx.set_bdpt(enabled=1, light_paths=16, vertices=4, image_plane=0)
+    try:
+        assert_parity(hip_ctx.render(40, 30, 2, 6), want, exact=True)
+    finally:
+        hip_ctx.set_bdpt(**old)
+
+
+def test_image_plane_term_is_separate():
+    """The image-plane pass only adds to a frame: with it on, frames differ from
+    image_plane = 0 exactly where an unoccluded light vertex faces the sensor."""
+    sd = S.config1(32, 24)
+    o = oracle_ffi.Oracle(sd)
+    o.set_bdpt(light_paths=32, vertices=3, image_plane=0)
+    a = o.render(32, 24, 2, 5, threads=4)
+    o.set_bdpt(light_paths=32, vertices=3, image_plane=1)
+    b = o.render(32, 24, 2, 5, threads=4)
+    fin = np.isfinite(a) & np.isfinite(b)
+    assert (b[fin] >= a[fin] - 1e-6 * np.abs(a[fin])).all() and (b[fin] > a[fin]).any()
 
 
 @pytest.mark.gpu
