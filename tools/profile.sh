@@ -24,6 +24,7 @@ for p in $PASSES; do
     tcpa)  timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TCP_TOTAL_CACHE_ACCESSES_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tcpa -o run -- $B --steps 16 --warmup 16 > $OUT/tcpa_bench.json 2> $OUT/tcpa_bench.log ;;
     mix)   timeout -k 10 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/mix -o run -- $B --steps 16 --warmup 16 > $OUT/mix_bench.json 2> $OUT/mix_bench.log ;;
     mix2)  timeout -k 10 240 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU_TRANS_F32 SQ_BUSY_CYCLES --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/mix2 -o run -- $B --steps 16 --warmup 16 > $OUT/mix2_bench.json 2> $OUT/mix2_bench.log ;;
+    l1)    timeout -k 10 240 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/l1 -o run -- $B --steps 16 --warmup 16 > $OUT/l1_bench.json 2> $OUT/l1_bench.log ;;
     tcc)   timeout -k 10 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tcc -o run -- $B --steps 16 --warmup 16 > $OUT/tcc_bench.json 2> $OUT/tcc_bench.log ;;
   esac
 done

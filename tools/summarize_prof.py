@@ -21,7 +21,7 @@ if os.path.exists(stats):
                      f"{float(r['AverageNs'])/1e6:.3f} | {float(r['Percentage']):.1f} |")
     lines.append("")
 pmc = collections.defaultdict(dict)
-for p in ["fetch", "write", "sq", "tcc", "lat", "ea"]:
+for p in ["fetch", "write", "sq", "tcc", "lat", "ea", "l1"]:
     f = os.path.join(src, p, "run_counter_collection.csv")
     if not os.path.exists(f):
         continue
@@ -59,8 +59,8 @@ if pmc:
 # derived per-launch metrics of the uninstrumented traversal kernels
 if pmc:
     lines += ["", "## derived (uninstrumented traversal kernels, averages over the frame's launches)", "",
-              "| kernel | launches | lines read/launch | L2 hit | VMEM latency (cyc) | VALU wave-instr/launch | VMEM wave-instr/launch |",
-              "|---|---|---|---|---|---|---|"]
+              "| kernel | launches | lines read/launch | L2 hit | L1 hit | VMEM latency (cyc) | VALU wave-instr/launch | VMEM wave-instr/launch |",
+              "|---|---|---|---|---|---|---|---|"]
     for kname in ("k_extend<false>", "k_shadow<false>"):
         def col(pas, cn):
             return [v[cn] for (k, p, d), v in pmc.items() if k == kname and p == pas and cn in v]
@@ -70,7 +70,9 @@ if pmc:
         valu, vmem = col("sq", "SQ_INSTS_VALU"), col("sq", "SQ_INSTS_VMEM_RD")
         mean = lambda v: sum(v) / len(v) if v else float("nan")
         l2 = sum(hit) / (sum(hit) + sum(miss)) if hit and miss else float("nan")
-        lines.append(f"| {kname} | {max(len(rd), len(lat), 1)} | {mean(rd):.4g} | {l2:.2f} | {mean(lat):.0f} | "
+        acc, l1miss = col("l1", "TCP_TOTAL_CACHE_ACCESSES_sum"), col("l1", "TCP_TCC_READ_REQ_sum")
+        l1 = 1.0 - sum(l1miss) / sum(acc) if acc and l1miss and sum(acc) > 0 else float("nan")
+        lines.append(f"| {kname} | {max(len(rd), len(lat), 1)} | {mean(rd):.4g} | {l2:.2f} | {l1:.2f} | {mean(lat):.0f} | "
                      f"{mean(valu):.4g} | {mean(vmem):.4g} |")
 
 calib = os.path.join(os.path.dirname(src.rstrip("/")), "calib")
