@@ -171,36 +171,7 @@ __device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx,
 
 __device__ __forceinline__ bool is_tri(float4 r0) { return bits_from_f(r0.w) == TRI_TAG; }
 
-#ifndef KHP_BRANCHLESS
-#define KHP_BRANCHLESS 0   // 1: select-based tests (exact; measured 3 % slower)
-#endif
-// KHP_BRANCHLESS: the primitive tests below evaluate every float operation of
-// KIRK's test unconditionally and combine the early-out conditions with
-// selects.  Results (hit flag, t, u, v) are identical -- the same IEEE
-// operations on the same inputs -- but a wave no longer pays exec-mask
-// bookkeeping (SALU) for each early return; most lanes of a traversal wave
-// would execute the masked arithmetic anyway.
-
 // Triangle::closestIntersection / isIntersection (Common/Triangle.cpp:152-184, 213-242)
-#if KHP_BRANCHLESS
-__device__ __forceinline__ bool tri_test(float4 r0, float4 r1, float4 r2, const Ray& r, float tMin, float tMax,
-                                         float& t, float& u, float& v) {
-    v3 A = mk(r0.x, r0.y, r0.z), ab = mk(r1.x, r1.y, r1.z), ac = mk(r2.x, r2.y, r2.z);
-    v3 dv = cross(r.d, ac);
-    float det = dot(dv, ab);
-    bool ok = !(fabsf(det) < TRI_EPS_D);
-    float inv = 1.0f / det;
-    v3 w = r.o - A;
-    u = dot(dv, w) * inv;
-    ok = ok && !(u < 0.0f || u > 1.0f);
-    v3 wu = cross(w, ab);
-    v = dot(wu, r.d) * inv;
-    ok = ok && !(v < 0.0f || u + v > 1.0f);
-    t = dot(wu, ac) * inv;
-    ok = ok && !((t < tMin) || (t > tMax));
-    return ok;
-}
-#else
 __device__ __forceinline__ bool tri_test(float4 r0, float4 r1, float4 r2, const Ray& r, float tMin, float tMax,
                                          float& t, float& u, float& v) {
     v3 A = mk(r0.x, r0.y, r0.z), ab = mk(r1.x, r1.y, r1.z), ac = mk(r2.x, r2.y, r2.z);
@@ -218,36 +189,8 @@ __device__ __forceinline__ bool tri_test(float4 r0, float4 r1, float4 r2, const 
     if ((t < tMin) || (t > tMax)) return false;
     return true;
 }
-#endif
 
 // Cylinder::closestIntersection (Common/Cylinder.cpp:73-156), open cone frustum.
-#if KHP_BRANCHLESS
-__device__ __forceinline__ bool cone_closest(float4 c0, float4 c1, float4 c2, float4 c3, const Ray& r, float tMin,
-                                             float tMax, float& t) {
-    v3 base = mk(c0.x, c0.y, c0.z), U = mk(c1.x, c1.y, c1.z), Vv = mk(c2.x, c2.y, c2.z), W = mk(c3.x, c3.y, c3.z);
-    float r0 = c0.w, slope = c1.w, min_d = c2.w, max_d = c3.w;
-    v3 P = r.o - base;
-    P = mk(dot(P, U), dot(P, Vv), dot(P, W));
-    v3 D = mk(dot(r.d, U), dot(r.d, Vv), dot(r.d, W));
-    float a = 1.0f - D.y * D.y * (1.0f + slope * slope);
-    float b = P.x * D.x + P.z * D.z + r0 * slope * D.y - slope * slope * P.y * D.y;
-    float c = r0 - slope * P.y;
-    c = P.x * P.x + P.z * P.z - c * c;
-    float disc = b * b - a * c;
-    const bool real = !(disc < 0.0f);
-    disc = sqrtf(disc);
-    float t1 = (-b - disc) / a;
-    float t2 = (-b + disc) / a;
-    const bool span = real && !((t2 < tMin) || (t1 > tMax));
-    const float d1 = dot(Vv, follow(r, t1)), d2 = dot(Vv, follow(r, t2));
-    const bool in1 = d1 >= min_d && d1 <= max_d, in2 = d2 >= min_d && d2 <= max_d;
-    const bool behind = t1 < RAY_EPS_D;  // origin inside: only the second root counts
-    const bool ok_b = !((t2 > tMax) || (t2 < tMin)) && in2;
-    const bool ok_f = !((t1 < tMin) && (t2 > tMax)) && (in1 || in2);
-    t = (!behind && in1) ? t1 : t2;
-    return span && (behind ? ok_b : ok_f);
-}
-#else
 __device__ __forceinline__ bool cone_closest(float4 c0, float4 c1, float4 c2, float4 c3, const Ray& r, float tMin,
                                              float tMax, float& t) {
     v3 base = mk(c0.x, c0.y, c0.z), U = mk(c1.x, c1.y, c1.z), Vv = mk(c2.x, c2.y, c2.z), W = mk(c3.x, c3.y, c3.z);
@@ -278,34 +221,8 @@ __device__ __forceinline__ bool cone_closest(float4 c0, float4 c1, float4 c2, fl
     if (d >= min_d && d <= max_d) { t = t2; return true; }
     return false;
 }
-#endif
 
 // Cylinder::isIntersection (Common/Cylinder.cpp:158-228): note a = Dx^2+Dz^2-s^2 Dy^2.
-#if KHP_BRANCHLESS
-__device__ __forceinline__ bool cone_any(float4 c0, float4 c1, float4 c2, float4 c3, const Ray& r, float tMax) {
-    v3 base = mk(c0.x, c0.y, c0.z), U = mk(c1.x, c1.y, c1.z), Vv = mk(c2.x, c2.y, c2.z), W = mk(c3.x, c3.y, c3.z);
-    float r0 = c0.w, slope = c1.w, min_d = c2.w, max_d = c3.w;
-    v3 P = r.o - base;
-    P = mk(dot(P, U), dot(P, Vv), dot(P, W));
-    v3 D = mk(dot(r.d, U), dot(r.d, Vv), dot(r.d, W));
-    float a = D.x * D.x + D.z * D.z - slope * slope * D.y * D.y;
-    float b = P.x * D.x + P.z * D.z + r0 * slope * D.y - slope * slope * P.y * D.y;
-    float c = r0 - slope * P.y;
-    c = P.x * P.x + P.z * P.z - c * c;
-    float disc = b * b - a * c;
-    const bool real = !(disc < 0.0f);
-    disc = sqrtf(disc);
-    float t1 = (-b - disc) / a;
-    float t2 = (-b + disc) / a;
-    const bool span = real && !((t2 < 0.0f) || (t1 > tMax));
-    const float d1 = dot(Vv, follow(r, t1)), d2 = dot(Vv, follow(r, t2));
-    const bool in1 = d1 >= min_d && d1 <= max_d, in2 = d2 >= min_d && d2 <= max_d;
-    const bool behind = t1 < RAY_EPS_D;
-    const bool ok_b = !((t2 > tMax) || (t2 < 0.0f)) && in2;
-    const bool ok_f = !((t1 < 0.0f) && (t2 > tMax)) && (in1 || in2);
-    return span && (behind ? ok_b : ok_f);
-}
-#else
 __device__ __forceinline__ bool cone_any(float4 c0, float4 c1, float4 c2, float4 c3, const Ray& r, float tMax) {
     v3 base = mk(c0.x, c0.y, c0.z), U = mk(c1.x, c1.y, c1.z), Vv = mk(c2.x, c2.y, c2.z), W = mk(c3.x, c3.y, c3.z);
     float r0 = c0.w, slope = c1.w, min_d = c2.w, max_d = c3.w;
@@ -333,7 +250,6 @@ __device__ __forceinline__ bool cone_any(float4 c0, float4 c1, float4 c2, float4
     d = dot(Vv, follow(r, t2));
     return d >= min_d && d <= max_d;
 }
-#endif
 
 #include "traverse.h"
 

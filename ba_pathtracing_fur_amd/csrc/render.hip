@@ -1558,6 +1558,7 @@ extern "C" khp_status khp_set_bdpt(khp_ctx* c, const khp_bdpt_params* p) {
     if (p->enabled && (p->light_paths < 1 || p->light_paths > 65536))
         return fail(KHP_EINVAL, "light_paths must be 1..65536");
     if (p->enabled && (p->vertices < 1 || p->vertices > 16)) return fail(KHP_EINVAL, "vertices must be 1..16");
+    if (p->image_plane > 1) return fail(KHP_EINVAL, "image_plane must be 0 or 1");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the estimator they started with
     if (dr != KHP_OK) return dr;

@@ -209,7 +209,8 @@ def test_product_reproduces_bdpt_fixture(path, hip_ctx):
 
 @pytest.mark.gpu
 def test_bdpt_params_validated(hip_ctx):
-    for bad in (dict(enabled=1, light_paths=0), dict(enabled=1, vertices=0), dict(enabled=1, vertices=17)):
+    for bad in (dict(enabled=1, light_paths=0), dict(enabled=1, vertices=0), dict(enabled=1, vertices=17),
+                dict(enabled=1, image_plane=2)):
         with pytest.raises(N.KhpError) as e:
             hip_ctx.set_bdpt(**bad)
         assert e.value.status == N.KHP_EINVAL
