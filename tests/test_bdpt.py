@@ -193,6 +193,25 @@ def test_bdpt_tile_shards(hip_ctx, nranks):
 
 
 @pytest.mark.gpu
+def test_bdpt_metric_scene_sampled_rows(hip_ctx):
+    """The variant on the metric scene itself (1M strands, 1080p, 256 subpaths x 4
+    vertices) at 2 spp: every 45th row against the oracle."""
+    sd = S.config3(1920, 1080, n_strands=1_000_000)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    old = hip_ctx.set_bdpt(enabled=1, light_paths=256, vertices=4)
+    try:
+        got = hip_ctx.render(1920, 1080, 2, 5)
+    finally:
+        hip_ctx.set_bdpt(**old)
+    o = oracle_ffi.Oracle(sd)
+    o.set_bdpt(light_paths=256, vertices=4)
+    want = o.render(1920, 1080, 2, 5, threads=16, rows=(0, 1080, 45))
+    rows = list(range(0, 1080, 45))
+    assert_parity(got[rows], want[rows], exact=True)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("path", FIXTURES, ids=IDS)
 def test_product_reproduces_bdpt_fixture(path, hip_ctx):
     sd, a = _load(path)
