@@ -389,6 +389,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_extend(DevScene S, W
 // calcNormal / calcTcoord code; Cylinder.cpp:230-260, Triangle.cpp:244-254).
 __device__ __forceinline__ void textured_material(const DevScene& S, const Aux& ax, const float4* pr, v3 loc,
                                                const ShadeCtx& s, float bu, float bv, khp_material& out);
+template <bool TEX>
 __device__ __forceinline__ v3 surface_at(const DevScene& S, const Ray& r, const Hit& h, ShadeCtx& s,
                                          khp_material& mres) {
     const Aux ax = S.aux[h.slot];
@@ -415,7 +416,7 @@ __device__ __forceinline__ v3 surface_at(const DevScene& S, const Ray& r, const 
         s.W = ld3(tf + 6);
     }
     s.n = nrm;
-    if (S.textured) {
+    if (TEX) {  // calcTcoord (traceRay, CPU_PathTracer.cpp:178-179), then the textured parameters
         mres = S.mats[ax.mat];
         textured_material(S, ax, pr, follow(r, h.t), s, h.u, h.v, mres);
         s.m = &mres;
@@ -455,7 +456,8 @@ __global__ __launch_bounds__(64) void k_light_paths(DevScene S, Wave Wv) {
         if (h.slot < 0) return;  // traceLightRays: no hit ends the subpath
         ShadeCtx sc;
         khp_material mres;
-        const v3 n = surface_at(S, r, h, sc, mres), pos = follow(r, h.t);
+        const v3 n = S.textured ? surface_at<true>(S, r, h, sc, mres) : surface_at<false>(S, r, h, sc, mres);
+        const v3 pos = follow(r, h.t);
         dist = dist + length(pos - r.o);
         const float att = 1.0f / ((1.0f + dist * al) + (dist * dist) * aq);
         const v3 in = -r.d;
@@ -772,42 +774,12 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                 C = C + light_emit(S.lights[t_index], r.d) * T;
                 T = mk(0, 0, 0);
             } else {
-                Aux ax = S.aux[slot];
-                const float4* pr = S.prims + 4 * (size_t)slot;
+                // normal and hair frame (Cylinder::calcNormal / Triangle::calcNormal), material
                 ShadeCtx s;
-                s.m = &S.mats[ax.mat];
-                v3 nrm;
-                if (ax.flags & 1u) {  // Cylinder::calcNormal (Cylinder.cpp:230-237)
-                    float4 c0 = pr[0], c1 = pr[1], c2 = pr[2], c3 = pr[3];
-                    v3 base3 = mk(c0.x, c0.y, c0.z);
-                    s.U = mk(c1.x, c1.y, c1.z);
-                    s.V = mk(c2.x, c2.y, c2.z);
-                    s.W = mk(c3.x, c3.y, c3.z);
-                    v3 Q = follow(r, lambda);
-                    float tt = dot(Q, s.V) - ax.base_d;
-                    v3 q1 = Q - s.V * tt;
-                    v3 nn = normalize(q1 - base3);
-                    nrm = normalize(nn + s.V * c1.w);
-                } else {           // Triangle::calcNormal (Triangle.cpp:244-248)
-                    const float* tn = S.tri_nrm + 9 * (size_t)ax.obj;
-                    float bu = Wv.hu[i], bv = Wv.hv[i];
-                    float bx = (1.0f - bu) - bv;
-                    nrm = normalize((ld3(tn) * bx + ld3(tn + 3) * bu) + ld3(tn + 6) * bv);
-                    const float* tf = S.tri_frame + 9 * (size_t)ax.obj;  // fiberToTriangles frame (else 0)
-                    s.U = ld3(tf);
-                    s.V = ld3(tf + 3);
-                    s.W = ld3(tf + 6);
-                }
-                s.n = nrm;
-                v3 loc = follow(r, lambda);
-                // the material by value; textured scenes: calcTcoord (traceRay,
-                // CPU_PathTracer.cpp:178-179), then the textured parameters
                 khp_material mres;
-                if (TEX) {
-                    mres = S.mats[ax.mat];
-                    textured_material(S, ax, pr, loc, s, Wv.hu[i], Wv.hv[i], mres);
-                    s.m = &mres;
-                }
+                const Hit hh{lambda, slot, Wv.hu[i], Wv.hv[i]};
+                const v3 nrm = surface_at<TEX>(S, r, hh, s, mres);
+                const v3 loc = follow(r, lambda);
                 const khp_material* m = s.m;
                 float h0 = draw_u01(key, dim_of(bounce, P_HAIR_ALPHA)), h1 = draw_u01(key, dim_of(bounce, P_HAIR_BETA));
                 v3 counter = -normalize(r.d);
