@@ -414,6 +414,9 @@ def main():
                         "prims": round(cnt["prim_tests"] / max(1, rays), 2)},
             "shadow": {
                 "kernel": "k_shadow (any-hit BVH2 traversal)",
+                "achieved_def": "algorithmic bytes per launch / average launch duration of the overlapped "
+                                "launches, which share the chip with the next bounce's k_extend; the "
+                                "kernel's own rate is isolated.k_shadow",
                 "achieved": round(sh_achieved, 1), "frac": round(sh_achieved / HBM_PEAK_GBPS, 4),
                 "bytes_per_launch": int(sh_bytes_per_launch), "avg_launch_ms": round(sh_avg_ms, 4),
                 "alg_bytes_per_frame": int(sh_bytes_frame),
