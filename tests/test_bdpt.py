@@ -142,6 +142,30 @@ def test_bdpt_frame_parity(hip_ctx, name, kw, w, h, spp, depth, ns, nv):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prm", [dict(shade_order=1), dict(serial_stages=1), dict(frames_in_flight=2, fuse_frames=1),
+                                 dict(fuse_frames=3, chunk_paths=8192)],
+                         ids=["hit-sorting", "serial-stages", "2-in-flight", "fused-chunked"])
+def test_bdpt_with_schedules(hip_ctx, prm):
+    """The variant under every scheduling parameter: frames stay the oracle's."""
+    sd = S.build_config("zoo", width=48, height=36, n_strands=300)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    o = oracle_ffi.Oracle(sd)
+    o.set_bdpt(light_paths=16, vertices=4)
+    want = o.render(48, 36, 4, 6, threads=16)
+    old_bd = hip_ctx.set_bdpt(enabled=1, light_paths=16, vertices=4)
+    old = hip_ctx.set_params(**prm)
+    try:
+        for k in range(4):
+            hip_ctx.render(48, 36, 1, 6, first_sample=k, async_=True)
+        hip_ctx.sync()
+        assert_parity(hip_ctx.read_framebuffer(48, 36), want, exact=True)
+    finally:
+        hip_ctx.set_params(**old)
+        hip_ctx.set_bdpt(**old_bd)
+
+
+@pytest.mark.gpu
 def test_bdpt_without_image_plane(hip_ctx):
     """image_plane = 0: only the hit connections (pt_shade.compute:146-201)."""
     sd = S.build_config("zoo", width=40, height=30, n_strands=300)
