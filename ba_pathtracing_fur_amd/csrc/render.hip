@@ -177,7 +177,6 @@ __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
     Wv.qpid[0][pid] = pid;
     Wv.TFq[0][pid] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));  // queue slot = path at bounce 0
     Wv.CKq[0][pid] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));
-    if (Wv.depth == 0) Wv.CK[pid] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));  // no bounce writes it
 }
 
 __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
