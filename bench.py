@@ -32,7 +32,11 @@ The JSON line also carries:
                   pass) of all timed launches / the time during which at
                   least one of them was running (union of their HIP-event
                   intervals), against 8 TB/s HBM; roofline.shadow is the same
-                  for the any-hit kernel (28 B + 32 B per node/prim + 4 B);
+                  for the any-hit kernel (28 B + 32 B per node/prim + 4 B)
+                  over its overlapped launches;
+  isolated     -- both traversal kernels' own rates: the same fused passes
+                  re-run with khp_ctx_params.serial_stages = 1 (no kernel
+                  overlaps another), algorithmic bytes / kernel time;
   cpu_baseline -- the C restatement (oracle/) timed on the host cores this
                   process may use, on a bounded sample of the same frame.
 """
