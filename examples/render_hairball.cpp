@@ -8,6 +8,9 @@
 // C++ bench:
 //
 //   render_hairball [strands=1000000] [W=1920] [H=1080] [spp=8] [depth=5] [frames=3] [out.pfm]
+//                   [light_paths=0]
+// light_paths > 0 renders with the light-path (bidirectional) variant (ABI 7,
+// khp_set_bdpt): that many subpaths per light, 4 vertices, both connection passes.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -33,7 +36,8 @@ int main(int argc, char** argv) {
     const uint32_t W = argc > 2 ? (uint32_t)atoi(argv[2]) : 1920u, H = argc > 3 ? (uint32_t)atoi(argv[3]) : 1080u;
     const uint32_t spp = argc > 4 ? (uint32_t)atoi(argv[4]) : 8u, depth = argc > 5 ? (uint32_t)atoi(argv[5]) : 5u;
     const int frames = argc > 6 ? atoi(argv[6]) : 3;
-    const char* out = argc > 7 ? argv[7] : nullptr;
+    const char* out = argc > 7 && strcmp(argv[7], "-") != 0 ? argv[7] : nullptr;
+    const uint32_t light_paths = argc > 8 ? (uint32_t)atoi(argv[8]) : 0u;
     const uint32_t SEED = 0x4B49524Bu;
     try {
         khp::SceneBuilder sb;
@@ -68,6 +72,14 @@ int main(int argc, char** argv) {
         sb.set_camera(cam);
 
         khp::Context ctx(0);
+        if (light_paths > 0) {
+            khp_bdpt_params bd;
+            khp_bdpt_params_defaults(&bd);
+            bd.enabled = 1;
+            bd.light_paths = light_paths;
+            bd.vertices = 4;
+            ctx.set_bdpt(bd);
+        }
         auto t0 = std::chrono::steady_clock::now();
         ctx.set_scene(sb);
         ctx.build_accel();

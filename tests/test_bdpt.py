@@ -166,6 +166,27 @@ def test_bdpt_with_schedules(hip_ctx, prm):
 
 
 @pytest.mark.gpu
+def test_cpp_host_program_bdpt(hip_ctx, tmp_path):
+    """examples/render_hairball (C++ on the C-ABI) with the variant on renders the
+    frame the Python host renders."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "render_hairball")
+    out = tmp_path / "f.pfm"
+    subprocess.run([exe, "3000", "64", "40", "2", "5", "1", str(out), "32"], check=True, timeout=300)
+    raw = out.read_bytes()
+    img = np.frombuffer(raw[raw.index(b"-1.0\n") + 5:], np.float32).reshape(40, 64, 3)
+    sd = S.config3(64, 40, n_strands=3000)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    old = hip_ctx.set_bdpt(enabled=1, light_paths=32, vertices=4)
+    try:
+        want = hip_ctx.render(64, 40, 2, 5)
+    finally:
+        hip_ctx.set_bdpt(**old)
+    assert np.array_equal(img.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
 def test_bdpt_without_image_plane(hip_ctx):
     """image_plane = 0: only the hit connections (pt_shade.compute:146-201)."""
     sd = S.build_config("zoo", width=40, height=30, n_strands=300)
