@@ -177,7 +177,11 @@ def uptr(a: np.ndarray):
 
 
 def load_library(path: str | None = None) -> ctypes.CDLL:
-    """Load libkirk_hip.so; raises RuntimeError if it was not built."""
+    """Load libkirk_hip.so; raises RuntimeError if it was not built.
+
+    `path`, or the KHP_LIB environment variable, selects another build of the
+    same ABI (tools/build_variant.sh + tools/gpu_variants.sh A/B runs); the
+    library itself reads no environment."""
     global _lib
     if _lib is not None and path is None:
         return _lib
