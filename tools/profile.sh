@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 passes for bench.py (run on the GPU box via gpurun, from the repo root).
-# usage: tools/profile.sh <tag> [pass...]   passes: trace fetch write sq lat ea tcc ta tas tcp tcpa mix mix2 list
+# usage: [CFG=1|2|3|5] tools/profile.sh <tag> [pass...]   passes: trace fetch write sq lat ea tcc ta tas tcp tcpa mix mix2 l1 list
+# (per-config PMC files must be tagged ..._cfg<N>_... for bench.py to pick them up)
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}; shift || true
@@ -8,7 +9,7 @@ PASSES=${@:-trace fetch write sq}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/bench.py --no-cpu-baseline --sync-check-steps 0 --iso-steps 0"  # every k_extend launch of the run then carries the same fused frames
+B="python3 $R/bench.py --no-cpu-baseline --sync-check-steps 0 --iso-steps 0 --config ${CFG:-metric}"  # every k_extend launch of the run then carries the same fused frames
 for p in $PASSES; do
   case $p in
     list)  timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true ;;
