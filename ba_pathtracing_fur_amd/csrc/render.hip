@@ -318,7 +318,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_extend(DevScene S, W
     Hit h;
     Cur c{0u, 0.0f, 0.0f, false};
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
-    Prefetch pf{0.0f, 0.0f};
     bool has = false, exhausted = false;
     uint32_t idx = 0, mode = 0u;
     unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
@@ -365,7 +364,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_extend(DevScene S, W
             if (has) {
                 bool occ_unused;
                 ++it;
-                if (iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused, exhausted, pf)) {
+                if (iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused)) {
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = h.slot;
                     Wv.hu[idx] = h.u;
@@ -1057,7 +1056,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, W
     TravRay tr;
     Cur c{0u, 0.0f, 0.0f, false};
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
-    Prefetch pf{0.0f, 0.0f};
     unsigned long long wit = 0, wbusy = 0;  // STATS: wave iterations, busy lanes
     float tmax = 0.0f;
     uint32_t mode = 0u;
@@ -1103,7 +1101,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, W
             if (has) {
                 bool occ = false;
                 Hit hu_{0.0f, -1, 0.0f, 0.0f};
-                if (iter2<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ, exhausted, pf)) {
+                if (iter2<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ)) {
                     Wv.vis[idx] = occ ? 1 : 0;
                     has = false;
                 }

@@ -458,34 +458,12 @@ __device__ __forceinline__ bool trav2_begin(const DevScene& S, const TravRay& tr
     return true;
 }
 
-// Tail prefetch: once a launch's queue is drained, the few rays still running
-// decide its duration, and each of their iterations waits a full HBM round
-// trip for the record it fetches.  In that phase the memory system is idle,
-// so as soon as an interior record's child boxes are tested, the lines of the
-// children that will be visited (the near one next iteration, the pushed far
-// one later) are requested with plain dword loads whose results are
-// discarded (`tail_pf` set by the caller, wave-uniform).  The loaded
-// registers stay live until the next fetch has been waited for; vmcnt retires
-// loads in order, so they cannot be reused while in flight.  Exactness is
-// unaffected: nothing reads the prefetched values.
-struct Prefetch {
-    float d0, d1;
-};
-__device__ __forceinline__ const void* child_line(const DevScene& S, uint32_t ref) {
-    return ref_leaf(ref) ? (const void*)(S.prims + 4 * (size_t)(ref & 0x00FFFFFFu))
-                         : (const void*)(S.nodes + ref);
-}
-__device__ __forceinline__ void pf_line(const DevScene& S, uint32_t ref, float& d) {
-    asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(child_line(S, ref)) : "memory");
-}
-
 // One wave iteration of one lane (mode != M_IDLE).  ANY: any-hit with the
 // fixed limit tlimit = the ray's tMax; else closest hit, tlimit = h.t.
 // Returns true when the ray is finished; for ANY, `occluded` tells the result.
 template <bool ANY, bool STATS, class Stack>
 __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
-                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded,
-                                      bool tail_pf, Prefetch& pf) {
+                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
     const bool in_leaf = mode == M_LEAF;
     const bool fetch = in_leaf || mode == M_NODE;
     const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
@@ -497,7 +475,6 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
         q3 = p[3];
         pin(q0); pin(q1); pin(q2); pin(q3);
     }
-    asm volatile("" : "+v"(pf.d0), "+v"(pf.d1));  // prefetches issued last iteration are complete here
     bool need_pop = mode == M_POP;
     bool have = false;  // a new entry (ref, t0, t1) for take_entry
     uint32_t eref = 0u;
@@ -551,10 +528,6 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
         pref = nearl ? rref : lref;
         pt0 = nearl ? r0 : l0;
         pt1 = nearl ? r1 : l1;
-        if (tail_pf) {
-            if (have) pf_line(S, eref, pf.d0);
-            if (push) pf_line(S, pref, pf.d1);
-        }
     }
     if (push) stk.push(pref, pt0, pt1);
     if (need_pop) {
