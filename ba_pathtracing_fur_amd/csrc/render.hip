@@ -200,12 +200,23 @@ __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
 // Measured on the metric row: 8-entry LDS rings, refill at 24
 // idle lanes and 6 waves per SIMD (72 VGPRs, 6 x 24 KB of LDS rings per CU)
 // are the best of the variants tried.
-constexpr int RING = 8;        // LDS ring entries per lane (3 x 4 B each)
+#ifndef KHP_EXT_RING
+#define KHP_EXT_RING 8
+#endif
+#ifndef KHP_EXT_WAVES
+#define KHP_EXT_WAVES 6
+#endif
+constexpr int RING = 8;        // LDS ring entries per lane (3 x 4 B each), k_shadow
 constexpr int REFILL = 24;     // refill when >= REFILL lanes are idle
-constexpr int TRAV_WAVES = 6;  // __launch_bounds__ waves per SIMD
+constexpr int TRAV_WAVES = 6;  // __launch_bounds__ waves per SIMD, k_shadow
+constexpr int EXT_RING = KHP_EXT_RING;    // the same for k_extend
+constexpr int EXT_WAVES = KHP_EXT_WAVES;
 constexpr size_t LDS_BYTES = 3 * RING * TRAV_BLOCK * sizeof(uint32_t);
+constexpr size_t EXT_LDS_BYTES = 3 * EXT_RING * TRAV_BLOCK * sizeof(uint32_t);
 template <bool STATS>
 using TravStack = LdsStack<RING, STATS>;
+template <bool STATS>
+using ExtStack = LdsStack<EXT_RING, STATS>;
 
 struct SpillArea {
     int4* base;
@@ -308,10 +319,10 @@ __device__ __forceinline__ void flush_stats(const TravStats& st, const Stack& st
 
 // ---- extend: closest hit for every queued ray ------------------------------------------
 template <bool STATS>
-__global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
+__global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t nf = Wv.cnt->nq[cur], nb = Wv.cnt->nqb[cur];
-    TravStack<STATS> stk;
+    ExtStack<STATS> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0, 0};
     TravRay tr;
@@ -1810,9 +1821,9 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     // persistent grid sizes
     int nb = 0;
     if (c->flags & KHP_CTX_STATS)
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<true>, TRAV_BLOCK, LDS_BYTES));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<true>, TRAV_BLOCK, EXT_LDS_BYTES));
     else
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, TRAV_BLOCK, LDS_BYTES));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, TRAV_BLOCK, EXT_LDS_BYTES));
     c->grid_ext = std::max(1, nb) * c->n_cu;
     nb = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, TRAV_BLOCK, LDS_BYTES));
@@ -2310,9 +2321,9 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
                 timed(c, f, 0, true, sA);
                 if (stats)
-                    hipLaunchKernelGGL(k_extend<true>, dim3(grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                    hipLaunchKernelGGL(k_extend<true>, dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
                 else
-                    hipLaunchKernelGGL(k_extend<false>, dim3(grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                    hipLaunchKernelGGL(k_extend<false>, dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
                 timed(c, f, 0, false, sA);
                 if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
                 timed(c, f, 1, true, sA);
@@ -2850,8 +2861,8 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
         HIPCHK(hipMemcpyAsync(hit_out, Wv.vis, n, hipMemcpyDeviceToHost, c->stream));
     } else {
         SpillArea sp{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
-        if (prod) hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, c->stream, c->S, Wv, 0, sp);
-        else hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(TRAV_BLOCK), LDS_BYTES, c->stream, c->S, Wv, 0, sp);
+        if (prod) hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, c->stream, c->S, Wv, 0, sp);
+        else hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, c->stream, c->S, Wv, 0, sp);
         (void)hipEventRecord(e1, c->stream);
         HIPCHK(t.ensure(4 * (size_t)n));
         HIPCHK(ob.ensure(4 * (size_t)n));
