@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 passes for bench.py (run on the GPU box via gpurun, from the repo root).
-# usage: [CFG=1|2|3|5] tools/profile.sh <tag> [pass...]   passes: trace fetch write sq lat ea tcc ta tas tcp tcpa mix mix2 l1 list
+# usage: [CFG=1|2|3|5] tools/profile.sh <tag> [pass...]   passes: trace fetch write sq lat ea tcc ta tab tas tcp tcpa mix mix2 l1 list
 # (per-config PMC files must be tagged ..._cfg<N>_... for bench.py to pick them up)
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -22,6 +22,7 @@ for p in $PASSES; do
     ta)    timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_BUSY_avr --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/ta -o run -- $B --steps 16 --warmup 16 > $OUT/ta_bench.json 2> $OUT/ta_bench.log ;;
     tas)   timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_ADDR_STALLED_BY_TC_CYCLES_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tas -o run -- $B --steps 16 --warmup 16 > $OUT/tas_bench.json 2> $OUT/tas_bench.log ;;
     tcp)   timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TCP_PENDING_STALL_CYCLES_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tcp -o run -- $B --steps 16 --warmup 16 > $OUT/tcp_bench.json 2> $OUT/tcp_bench.log ;;
+    tab)   timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_BUSY_max --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tab -o run -- $B --steps 16 --warmup 16 > $OUT/tab_bench.json 2> $OUT/tab_bench.log ;;
     tcpa)  timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TCP_TOTAL_CACHE_ACCESSES_sum --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/tcpa -o run -- $B --steps 16 --warmup 16 > $OUT/tcpa_bench.json 2> $OUT/tcpa_bench.log ;;
     mix)   timeout -k 10 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/mix -o run -- $B --steps 16 --warmup 16 > $OUT/mix_bench.json 2> $OUT/mix_bench.log ;;
     mix2)  timeout -k 10 240 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU_TRANS_F32 SQ_BUSY_CYCLES --kernel-include-regex 'k_extend|k_shadow' --output-format csv -d $OUT/mix2 -o run -- $B --steps 16 --warmup 16 > $OUT/mix2_bench.json 2> $OUT/mix2_bench.log ;;
