@@ -372,18 +372,10 @@ __global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wa
                 ++wit;
                 wbusy += (uint32_t)__popcll(wm);
             }
-#ifdef KHP_COOP_FETCH
-            float4 q0, q1, q2, q3;
-            coop_fetch(S, fetch_key(has, mode, c, lf), q0, q1, q2, q3);
-#endif
             if (has) {
                 bool occ_unused;
                 ++it;
-#ifdef KHP_COOP_FETCH
-                if (iter2<false, STATS, true>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused, q0, q1, q2, q3)) {
-#else
                 if (iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused)) {
-#endif
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = h.slot;
                     Wv.hu[idx] = h.u;

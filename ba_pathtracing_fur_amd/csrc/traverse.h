@@ -458,108 +458,22 @@ __device__ __forceinline__ bool trav2_begin(const DevScene& S, const TravRay& tr
     return true;
 }
 
-// The record a lane's next iteration reads, as a fetch key for coop_fetch:
-// 0 when the lane fetches nothing, else bit 30 set, bit 31 = candidate
-// primitive (else interior node), bits 0-29 = slot or node index.
-__device__ __forceinline__ uint32_t fetch_key(bool active, uint32_t mode, const Cur& c, const LeafCur& lf) {
-    const bool in_leaf = mode == M_LEAF;
-    const bool fetch = active && (in_leaf || mode == M_NODE);
-    return fetch ? (0x40000000u | (in_leaf ? 0x80000000u | lf.slot : c.ref)) : 0u;
-}
-
-// Cooperative record fetch, called by the whole wave (all 64 lanes active).
-// A lane's 64-B record is four 16-B pieces.  Lane (16r + c) of load k reads
-// piece r of lane (16k + c)'s record, so each load instruction touches 16
-// records -- 64 contiguous bytes per 4 lanes -- instead of 64 scattered ones,
-// and the vector L1 looks up a quarter of the tags (the traversal loop is
-// bound by that path).  The keys are broadcast row-wise
-// and the pieces transposed back to their owners with the gfx950 row swaps
-// (v_permlane32_swap / v_permlane16_swap): rows are 16 lanes, and a 4x4
-// transpose of (load, row) blocks is one 32-swap and one 16-swap round.
-// Every address read is a valid record (a key of some lane, or node 0 for
-// lanes that fetch nothing), and a lane reads pieces only through loads
-// whose key is its own.
-__device__ __forceinline__ uint32_t swap32(uint32_t& a, uint32_t& b) {
-    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-    a = r[0];
-    b = r[1];
-    return 0u;
-}
-__device__ __forceinline__ uint32_t swap16(uint32_t& a, uint32_t& b) {
-    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
-    a = r[0];
-    b = r[1];
-    return 0u;
-}
-__device__ __forceinline__ void swap32(float4& a, float4& b) {
-    uint32_t ax = __float_as_uint(a.x), ay = __float_as_uint(a.y), az = __float_as_uint(a.z), aw = __float_as_uint(a.w);
-    uint32_t bx = __float_as_uint(b.x), by = __float_as_uint(b.y), bz = __float_as_uint(b.z), bw = __float_as_uint(b.w);
-    swap32(ax, bx); swap32(ay, by); swap32(az, bz); swap32(aw, bw);
-    a = make_float4(__uint_as_float(ax), __uint_as_float(ay), __uint_as_float(az), __uint_as_float(aw));
-    b = make_float4(__uint_as_float(bx), __uint_as_float(by), __uint_as_float(bz), __uint_as_float(bw));
-}
-__device__ __forceinline__ void swap16(float4& a, float4& b) {
-    uint32_t ax = __float_as_uint(a.x), ay = __float_as_uint(a.y), az = __float_as_uint(a.z), aw = __float_as_uint(a.w);
-    uint32_t bx = __float_as_uint(b.x), by = __float_as_uint(b.y), bz = __float_as_uint(b.z), bw = __float_as_uint(b.w);
-    swap16(ax, bx); swap16(ay, by); swap16(az, bz); swap16(aw, bw);
-    a = make_float4(__uint_as_float(ax), __uint_as_float(ay), __uint_as_float(az), __uint_as_float(aw));
-    b = make_float4(__uint_as_float(bx), __uint_as_float(by), __uint_as_float(bz), __uint_as_float(bw));
-}
-__device__ __forceinline__ float4 coop_piece(const DevScene& S, uint32_t key, uint32_t row) {
-    // unconditional (a branch per load would wait for each load in turn): key 0 reads node 0
-    const uint32_t i = key & 0x3FFFFFFFu;
-    const float4* p = (key & 0x80000000u) ? S.prims + 4 * (size_t)i : reinterpret_cast<const float4*>(S.nodes + i);
-    return p[row];
-}
-__device__ __forceinline__ void coop_fetch(const DevScene& S, uint32_t key, float4& q0, float4& q1, float4& q2,
-                                           float4& q3) {
-    // keys of rows 0..3, each broadcast to all rows
-    uint32_t k0 = key, k2 = key;
-    swap32(k0, k2);  // k0 = [K0 K1 K0 K1], k2 = [K2 K3 K2 K3] (by row)
-    uint32_t k1 = k0, k3 = k2;
-    swap16(k0, k1);  // k0 = K0 everywhere, k1 = K1
-    swap16(k2, k3);
-    const uint32_t row = threadIdx.x >> 4;
-    q0 = coop_piece(S, k0, row);
-    q1 = coop_piece(S, k1, row);
-    q2 = coop_piece(S, k2, row);
-    q3 = coop_piece(S, k3, row);
-    pin(q0); pin(q1); pin(q2); pin(q3);
-    // (load k, row r) holds piece r of record 16k + c; transpose to (piece, owner row)
-    swap32(q0, q2);
-    swap32(q1, q3);
-    swap16(q0, q1);
-    swap16(q2, q3);
-}
-
 // One wave iteration of one lane (mode != M_IDLE).  ANY: any-hit with the
 // fixed limit tlimit = the ray's tMax; else closest hit, tlimit = h.t.
 // Returns true when the ray is finished; for ANY, `occluded` tells the result.
-template <bool ANY, bool STATS, bool PRE = false, class Stack>
+template <bool ANY, bool STATS, class Stack>
 __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
-                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded,
-                                      float4 pq0 = float4{}, float4 pq1 = float4{}, float4 pq2 = float4{},
-                                      float4 pq3 = float4{}) {
+                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
     const bool in_leaf = mode == M_LEAF;
     const bool fetch = in_leaf || mode == M_NODE;
     const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
-    float4 q0 = pq0, q1 = pq1, q2 = pq2, q3 = pq3;  // PRE: the record, fetched by coop_fetch
-#ifdef KHP_PROBE_EXTRA_LOADS
-    float px0 = 0.0f, px1 = 0.0f, px2 = 0.0f, px3 = 0.0f;
-#endif
-    if (!PRE && fetch) {
+    float4 q0, q1, q2, q3;
+    if (fetch) {
         q0 = p[0];
         q1 = p[1];
         q2 = p[2];
         q3 = p[3];
         pin(q0); pin(q1); pin(q2); pin(q3);
-#ifdef KHP_PROBE_EXTRA_LOADS
-        // probe build only: 4 extra 4-B loads from the same 128-B lines, consumed at the end of the iteration
-        typedef const __attribute__((address_space(1))) float gfloat;
-        gfloat* pf = (gfloat*)(reinterpret_cast<const float*>(p));
-        asm volatile("" : "+v"(pf));  // hide the pointer so the loads are not merged with q0..q3
-        px0 = pf[0]; px1 = pf[4]; px2 = pf[8]; px3 = pf[12];
-#endif
     }
     bool need_pop = mode == M_POP;
     bool have = false;  // a new entry (ref, t0, t1) for take_entry
@@ -631,9 +545,6 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
             have = true;
         }
     }
-#ifdef KHP_PROBE_EXTRA_LOADS
-    asm volatile("" ::"v"(px0), "v"(px1), "v"(px2), "v"(px3));
-#endif
     if (have) take_entry<STATS>(S, eref, et0, et1, mode, c, lf, st);
     return false;
 }
