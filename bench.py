@@ -90,6 +90,8 @@ def parse():
     ap.add_argument("--iso-steps", type=int, default=8,
                     help="fused passes re-run with serial_stages=1 for the isolated per-kernel rooflines (0: skip)")
     ap.add_argument("--shade-order", type=int, default=None, help="khp_ctx_params.shade_order (1: hits sorted by shading class)")
+    ap.add_argument("--heavy-iters", type=int, default=None,
+                    help="khp_ctx_params.heavy_iters (longest-first queue threshold, traversal iterations)")
     ap.add_argument("--bdpt", default=None, metavar="PATHS,VERTICES",
                     help="light-path variant (khp_bdpt_params, SURVEY §8(f)4): not the metric's estimator")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -269,7 +271,8 @@ def main():
             f"({setup}), depth {st0['bvh_depth']}, nodes {st0['n_nodes']}, HBM {st0['device_bytes'] / 1e9:.2f} GB")
     frame = ShardedFrame(ctx, rank, world, dist, tile=args.tile)
     knobs = {k: v for k, v in (("fuse_frames", args.fuse), ("chunk_paths", args.chunk_paths),
-                               ("frames_in_flight", args.frames_in_flight), ("shade_order", args.shade_order))
+                               ("frames_in_flight", args.frames_in_flight), ("shade_order", args.shade_order),
+                               ("heavy_iters", args.heavy_iters))
              if v is not None}
     if knobs:
         ctx.set_params(**knobs)
