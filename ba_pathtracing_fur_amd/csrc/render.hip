@@ -1449,7 +1449,7 @@ struct khp_ctx {
     khp_stats st{};
     // rccl gather: pixel lists cached per (W, H, tile, nranks, rank, root)
     uint32_t gather_key[6] = {0, 0, 0, 0, 0, 0};
-    std::vector<size_t> gather_counts;   // root: pixels per rank; sender: [own count]
+    std::vector<uint64_t> gather_counts; // khp_gather_plan counts: root: per sender; sender: its own
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
 };
@@ -1595,6 +1595,32 @@ extern "C" void khp_destroy(khp_ctx* c) {
 
 static bool host_path(const khp_ctx* c) { return (c->flags & KHP_CTX_HOST_BUILD) != 0; }
 
+// khp_set_scene_device reads the per-object arrays from device memory but the
+// tables (materials, lights, cone_models, textures and their texels,
+// material_textures) on the host: cone_models is inverted on the host
+// (scene_models), the textures are validated and packed there.  A device
+// pointer in one of those fields is refused instead of dereferenced.
+static bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // plain (unregistered) host memory
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+static const char* device_table_field(const khp_scene* s) {
+    if (is_device_ptr(s->materials)) return "materials";
+    if (is_device_ptr(s->lights)) return "lights";
+    if (is_device_ptr(s->cone_models)) return "cone_models";
+    if (is_device_ptr(s->textures)) return "textures";
+    if (is_device_ptr(s->material_textures)) return "material_textures";
+    for (uint32_t i = 0; s->textures && i < s->n_textures; ++i)
+        if (is_device_ptr(s->textures[i].data)) return "textures[].data";
+    return nullptr;
+}
+
 static khp_status set_scene_impl(khp_ctx* c, const khp_scene* s, bool device_ptrs) {
     if (c) {  // complete asynchronous frames first
         khp_status dr = drain(c);
@@ -1604,6 +1630,11 @@ static khp_status set_scene_impl(khp_ctx* c, const khp_scene* s, bool device_ptr
     auto t0 = std::chrono::steady_clock::now();
     const bool host = host_path(c);
     if (host && device_ptrs) return fail(KHP_EUNSUPPORTED, "device scene arrays need the device build path");
+    if (device_ptrs && s) {
+        HIPCHK(hipSetDevice(c->device));
+        if (const char* f = device_table_field(s))
+            return fail(KHP_EINVAL, std::string("khp_set_scene_device: ") + f + " must be host memory");
+    }
     c->scene_set = false;
     c->built = false;
     std::string err = flatten_scene(s, c->hs, host);
@@ -1906,24 +1937,6 @@ static Wave wave_view(const khp_ctx* c, PathSet& w) {
     return Wv;
 }
 
-static void owned_pixels(uint32_t W, uint32_t H, uint32_t T, uint32_t rank, uint32_t nranks,
-                         std::vector<uint32_t>& out) {
-    out.clear();
-    uint32_t tx_n = (W + T - 1) / T, ty_n = (H + T - 1) / T;
-    uint32_t bpr = T / 8;
-    for (uint32_t tid = 0; tid < tx_n * ty_n; ++tid) {
-        if (nranks > 1 && tid % nranks != rank) continue;
-        uint32_t tx = tid % tx_n, ty = tid / tx_n;
-        for (uint32_t blk = 0; blk < bpr * bpr; ++blk) {
-            uint32_t bx = blk % bpr, by = blk / bpr;
-            for (uint32_t j = 0; j < 64; ++j) {
-                uint32_t x = tx * T + bx * 8 + (j & 7), y = ty * T + by * 8 + (j >> 3);
-                if (x < W && y < H) out.push_back(y * W + x);
-            }
-        }
-    }
-}
-
 static khp_status prepare_pixels(khp_ctx* c, const khp_render_params* p) {
     uint32_t T = p->tile_size ? p->tile_size : 64;
     uint32_t nranks = p->tile_nranks > 1 ? p->tile_nranks : 1;
@@ -2201,6 +2214,12 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         P_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(P_all, cap_paths));
         S_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(p->spp, cap_paths / P_chunk));
     }
+    if (bdm && nf == 1) {  // the light subpaths of a chunk's sample slots take at most a quarter of the free HBM
+        size_t free_b = 0, total_b = 0;
+        const size_t per_slot = (size_t)c->bd.light_paths * c->S.n_lights * c->bd.vertices * 48;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && per_slot)
+            S_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(S_chunk, free_b / 4 / per_slot));
+    }
     // a partial batch (flushed by a sync) reserves room for a full one, so the
     // first full batch does not allocate
     size_t want = (size_t)P_chunk * S_chunk * nf;
@@ -2211,8 +2230,24 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     PathSet& w = c->ps[slot];
     s = ensure_wave(c, w, want, sh_per_path);
     if (s != KHP_OK) return s;
-    const size_t lv_bytes = bdm ? (size_t)nf * S_chunk * c->bd.light_paths * c->S.n_lights * c->bd.vertices * 48 : 0;
-    if (bdm) HIPCHK(w.lvb.ensure(lv_bytes));
+    // light subpaths of a chunk: one per (frame, sample slot, subpath, light); k_light_paths
+    // indexes them with 32 bits, and their vertices (48 B each) must fit beside the path sets
+    size_t lv_bytes = 0;
+    if (bdm) {
+        const uint64_t nsub = (uint64_t)nf * S_chunk * c->bd.light_paths * (uint64_t)c->S.n_lights;
+        if (nsub >= ((uint64_t)1 << 31))
+            return fail(KHP_EINVAL, "light-path variant: frames x samples x light_paths x lights per chunk reaches "
+                                    "2^31 subpaths; lower light_paths or the samples per pass");
+        lv_bytes = (size_t)nsub * c->bd.vertices * 48;
+        if (lv_bytes > w.lvb.bytes) {
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && lv_bytes + (lv_bytes >> 3) > free_b)
+                return fail(KHP_ENOMEM, "light-path variant: " + std::to_string(lv_bytes >> 20) +
+                                            " MiB of light vertices per chunk exceed the free HBM; lower light_paths, "
+                                            "vertices or the samples per pass");
+        }
+        HIPCHK(w.lvb.ensure(lv_bytes));
+    }
     const int dump_b = (!async && !ops) ? c->prm.dump_bounce : -1;
     if (stats) {
         const size_t chunks = (size_t)((P_all + P_chunk - 1) / P_chunk) * ((p->spp + S_chunk - 1) / S_chunk);
@@ -2294,7 +2329,9 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 else
                     hipLaunchKernelGGL(k_shadow<false>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wi, sp_sh);
                 timed(c, f, 2, false, sA);
+                timed(c, f, 4, true, sA);
                 hipLaunchKernelGGL(k_shadow_finish<true>, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wi, 0);
+                timed(c, f, 4, false, sA);
             }
             hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
             for (uint32_t b = 0; b < p->depth; ++b) {
@@ -3011,15 +3048,9 @@ static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root) {
     uint32_t key[6] = {p->width, p->height, T, (uint32_t)c->nranks, (uint32_t)c->rank, (uint32_t)root};
     if (memcmp(key, c->gather_key, sizeof(key)) != 0) {
         // the pixel lists depend only on the frame geometry: build + upload once, not per frame
-        std::vector<uint32_t> flat, one;
-        c->gather_counts.assign((size_t)c->nranks, 0);
-        for (int r = 0; r < c->nranks; ++r) {
-            if ((c->rank == root) == (r == root)) continue;  // root: every sender; sender: itself
-            owned_pixels(p->width, p->height, T, (uint32_t)r, (uint32_t)c->nranks, one);
-            c->gather_counts[r] = one.size();
-            flat.insert(flat.end(), one.begin(), one.end());
-        }
-        if (c->rank != root) c->gather_counts[root] = 0;
+        std::vector<uint32_t> flat;
+        const std::string e = gather_plan(p->width, p->height, T, c->nranks, c->rank, root, c->gather_counts, flat);
+        if (!e.empty()) return fail(KHP_EINVAL, "khp_gather_framebuffer: " + e);
         HIPCHK(upload(c->stage_pix, flat.data(), flat.size(), c->stream));
         HIPCHK(c->stage.ensure(flat.size() * 3 * sizeof(float) + 16));
         HIPCHK(hipStreamSynchronize(c->stream));

@@ -486,6 +486,46 @@ void make_device_layout(HostScene& hs) {
     }
 }
 
+// Tile t (row-major over the frame) belongs to rank t % nranks;
+// KIRK's own segmentation is square segments in order (BufferSegmentation.h:34-75).
+void owned_pixels(uint32_t W, uint32_t H, uint32_t T, uint32_t rank, uint32_t nranks, std::vector<uint32_t>& out) {
+    out.clear();
+    const uint32_t tx_n = (W + T - 1) / T, ty_n = (H + T - 1) / T;
+    const uint32_t bpr = T / 8;
+    for (uint32_t tid = 0; tid < tx_n * ty_n; ++tid) {
+        if (nranks > 1 && tid % nranks != rank) continue;
+        const uint32_t tx = tid % tx_n, ty = tid / tx_n;
+        for (uint32_t blk = 0; blk < bpr * bpr; ++blk) {
+            const uint32_t bx = blk % bpr, by = blk / bpr;
+            for (uint32_t j = 0; j < 64; ++j) {
+                const uint32_t x = tx * T + bx * 8 + (j & 7), y = ty * T + by * 8 + (j >> 3);
+                if (x < W && y < H) out.push_back(y * W + x);
+            }
+        }
+    }
+}
+
+// Root: every other rank's owned pixels, in rank order (what it receives).
+// Sender: its own owned pixels (what it sends).  Both sides therefore agree on
+// counts[sender] for every sender, which is what ncclSend/ncclRecv need.
+std::string gather_plan(uint32_t W, uint32_t H, uint32_t T, int nranks, int rank, int root,
+                        std::vector<uint64_t>& counts, std::vector<uint32_t>& flat) {
+    if (W == 0 || H == 0) return "empty frame";
+    if (T == 0 || T % 8 != 0) return "tile size must be a positive multiple of 8";
+    if (nranks < 1 || rank < 0 || rank >= nranks || root < 0 || root >= nranks) return "bad rank/root";
+    counts.assign((size_t)nranks, 0);
+    flat.clear();
+    std::vector<uint32_t> one;
+    for (int r = 0; r < nranks; ++r) {
+        if (r == root) continue;               // the root's own tiles stay in place
+        if (rank != root && r != rank) continue;  // a sender lists only itself
+        owned_pixels(W, H, T, (uint32_t)r, (uint32_t)nranks, one);
+        counts[(size_t)r] = one.size();
+        flat.insert(flat.end(), one.begin(), one.end());
+    }
+    return std::string();
+}
+
 }  // namespace khp
 
 // ============================================================================
@@ -528,6 +568,19 @@ extern "C" khp_status khp_host_build(const khp_scene* scene, uint32_t* n_nodes, 
         }
         if (records) memcpy(records + 16 * (size_t)i, &hs.rec[16 * (size_t)i], 16 * sizeof(float));
     }
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_gather_plan(uint32_t width, uint32_t height, uint32_t tile_size, int nranks, int rank,
+                                      int root, uint64_t* counts, uint32_t* pixels, uint64_t* n_pixels) {
+    if (!n_pixels) return fail(KHP_EINVAL, "khp_gather_plan: n_pixels is null");
+    std::vector<uint64_t> cnt;
+    std::vector<uint32_t> flat;
+    const std::string e = gather_plan(width, height, tile_size ? tile_size : 64, nranks, rank, root, cnt, flat);
+    if (!e.empty()) return fail(KHP_EINVAL, "khp_gather_plan: " + e);
+    *n_pixels = flat.size();
+    if (counts) memcpy(counts, cnt.data(), cnt.size() * sizeof(uint64_t));
+    if (pixels) memcpy(pixels, flat.data(), flat.size() * sizeof(uint32_t));
     return KHP_OK;
 }
 

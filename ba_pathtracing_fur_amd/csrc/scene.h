@@ -113,6 +113,15 @@ void build_bvh(HostScene& hs, int n_threads);
 void make_device_layout(HostScene& hs);
 void light_init(DevLight& L, const khp_light& in);
 
+// The pixels (y*W + x) of the T x T tiles with id % nranks == rank, tile by
+// tile, each tile as 8x8 blocks of 64 pixels (the wavefront's path order).
+void owned_pixels(uint32_t W, uint32_t H, uint32_t T, uint32_t rank, uint32_t nranks, std::vector<uint32_t>& out);
+// The framebuffer gather as seen from `rank` (khp_gather_plan in kirk_hip.h):
+// counts[r] = pixels rank r sends to root in this rank's view, `flat` = their
+// lists concatenated in rank order.  Empty string on success.
+std::string gather_plan(uint32_t W, uint32_t H, uint32_t T, int nranks, int rank, int root,
+                        std::vector<uint64_t>& counts, std::vector<uint32_t>& flat);
+
 // Per-thread message behind khp_last_error(); every failing entry point sets it.
 khp_status fail(khp_status s, const std::string& msg);
 const char* last_error();

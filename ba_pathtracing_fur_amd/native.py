@@ -163,7 +163,7 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_read_layout", "khp_set_scene_device", "khp_gen_hairball_device", "khp_device_alloc",
             "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device",
             "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params", "khp_debug_shadow_queue",
-            "khp_bdpt_params_defaults", "khp_set_bdpt", "khp_get_bdpt"]
+            "khp_bdpt_params_defaults", "khp_set_bdpt", "khp_get_bdpt", "khp_gather_plan"]
 
 _lib = None
 
@@ -227,6 +227,8 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_comm_unique_id": (c_int, [P(c_uint8)]),
         "khp_comm_init": (c_int, [c_void_p, c_int, c_int, P(c_uint8)]),
         "khp_gather_framebuffer": (c_int, [c_void_p, P(RenderParams), c_int]),
+        "khp_gather_plan": (c_int, [c_uint32, c_uint32, c_uint32, c_int, c_int, c_int, P(c_uint64), P(c_uint32),
+                                    P(c_uint64)]),
         "khp_bsdf_kind_from_name": (c_int, [c_char_p]),
         "khp_bsdf_name": (c_char_p, [c_int]),
         "khp_shader_kind_from_name": (c_int, [c_char_p]),
@@ -281,3 +283,17 @@ def host_build(scene) -> dict:
                                   ip(count), ip(ids), fptr(bounds), fptr(rec)), "khp_host_build")
     return {"boxes": boxes, "first": first, "count": count, "ids": ids, "bounds": bounds, "records": rec,
             "depth": dep.value}
+
+
+def gather_plan(width: int, height: int, tile: int, nranks: int, rank: int, root: int = 0):
+    """khp_gather_plan (host only): (counts[nranks], pixel indices) that
+    khp_gather_framebuffer moves, as seen from `rank`."""
+    lib = load_library()
+    n = c_uint64()
+    check(lib, lib.khp_gather_plan(width, height, tile, nranks, rank, root, None, None, ctypes.byref(n)),
+          "khp_gather_plan")
+    counts = np.zeros(nranks, np.uint64)
+    pix = np.zeros(max(1, n.value), np.uint32)
+    check(lib, lib.khp_gather_plan(width, height, tile, nranks, rank, root, counts.ctypes.data_as(POINTER(c_uint64)),
+                                   uptr(pix), ctypes.byref(n)), "khp_gather_plan")
+    return counts, pix[:n.value]

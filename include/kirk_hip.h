@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 7
+#define KHP_ABI_VERSION 8
 
 typedef struct khp_ctx khp_ctx;
 
@@ -346,8 +346,12 @@ khp_status khp_get_bdpt(khp_ctx* ctx, khp_bdpt_params* out);
  * (render, read, gather, scene change) also completes in-flight frames first. */
 khp_status khp_sync(khp_ctx* ctx);
 
-/* khp_set_scene with the geometry arrays (tri_v, tri_n, tri_mat, cone_*) in
- * device memory of ctx's GPU (materials, lights, camera stay host structs).
+/* khp_set_scene with the per-object arrays in device memory of ctx's GPU:
+ *   device: tri_v, tri_n, tri_mat, tri_frame, tri_uv, cone_base_r0,
+ *           cone_apex_r1, cone_mat, cone_model;
+ *   host:   materials, lights, camera, env, cone_models (the matrix table,
+ *           inverted on the host), textures and their texel data,
+ *           material_textures -- a device pointer there is refused (EINVAL).
  * The objects are flattened on the device; the arrays are
  * read during the call only.  Not with KHP_CTX_HOST_BUILD. */
 khp_status khp_set_scene_device(khp_ctx* ctx, const khp_scene* scene);
@@ -420,6 +424,18 @@ khp_status khp_comm_init(khp_ctx* ctx, int nranks, int rank, const uint8_t id[12
 /* Gather every rank's owned tiles (per p->tile_*) into rank root's device
  * framebuffer over RCCL; root may then khp_read_framebuffer. Collective. */
 khp_status khp_gather_framebuffer(khp_ctx* ctx, const khp_render_params* p, int root);
+
+/* ABI 8: the pixel plan khp_gather_framebuffer moves, as seen from `rank`
+ * (host only, no device needed).  KIRK has no multi-device path; its analogue
+ * is the square-segment split of BufferSegmentation (Utils/BufferSegmentation.h:
+ * 34-75).  Tile t (tile_size px, 0 -> 64, row-major) is rendered by rank
+ * t % nranks.  counts (nullable, [nranks]): pixels rank r sends to root in
+ * this rank's view -- the root lists every sender, a sender lists only itself,
+ * the root's own entry is 0; pixels (nullable): their pixel indices y*W + x,
+ * concatenated in rank order, each tile as 8x8 blocks; *n_pixels = the total.
+ * A sender's counts[rank] equals the root's counts[rank] by construction. */
+khp_status khp_gather_plan(uint32_t width, uint32_t height, uint32_t tile_size, int nranks, int rank, int root,
+                           uint64_t* counts, uint32_t* pixels, uint64_t* n_pixels);
 
 /* The BVH khp_build_accel built (device or host path), in the layout of
  * khp_host_build below: call with null arrays for *n_nodes / *depth. */

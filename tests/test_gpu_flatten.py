@@ -52,6 +52,28 @@ def test_set_scene_device_matches_host_arrays():
     b.close()
 
 
+def test_set_scene_device_refuses_device_tables():
+    """khp_set_scene_device reads the tables (materials, cone_models, ...) on the
+    host: a device pointer there is refused with KHP_EINVAL, not dereferenced."""
+    import ctypes
+    from ba_pathtracing_fur_amd.pathtracer import DeviceBuffer
+    sd = S.config1(16, 16)
+    c = HipContext(0)
+    d = sd.desc()
+    mats = DeviceBuffer(c, ctypes.sizeof(N.Material) * max(1, d.n_materials))
+    d.materials = ctypes.cast(mats.ptr, ctypes.POINTER(N.Material))
+    st = c.lib.khp_set_scene_device(c.ptr, ctypes.byref(d))
+    assert st == N.KHP_EINVAL and b"materials" in c.lib.khp_last_error()
+    d = sd.desc()
+    models = DeviceBuffer(c, 64)
+    d.n_cone_models, d.cone_models = 1, ctypes.cast(models.ptr, ctypes.POINTER(ctypes.c_float))
+    st = c.lib.khp_set_scene_device(c.ptr, ctypes.byref(d))
+    assert st == N.KHP_EINVAL and b"cone_models" in c.lib.khp_last_error()
+    mats.free()
+    models.free()
+    c.close()
+
+
 def test_config3_device_equals_host_config3():
     w, h = 64, 36
     c = HipContext(0)

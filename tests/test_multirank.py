@@ -2,10 +2,13 @@
 
 Each rank drives sharding.ShardedFrame exactly as bench.py does.  The GPU
 context is replaced by a stand-in that renders this rank's tiles with the
-oracle and does the framebuffer gather over gloo with the same pixel lists as
-khp_gather_framebuffer's RCCL send/recv; rank 0's assembled frame must equal the
-single-process frame bit for bit.  The RCCL path itself runs on the GPU box
-(tests/test_gpu_parity.py renders every rank's tile set through the product).
+oracle and moves the framebuffer over gloo with the PRODUCT's gather plan
+(khp_gather_plan from libkirk_hip.so, the same host function
+khp_gather_framebuffer builds its ncclSend/ncclRecv lists with): a sender packs
+exactly the pixels its plan lists, the root receives counts[r] pixels from
+each sender and scatters them by its own plan.  Rank 0's assembled frame must
+equal the single-process frame bit for bit.  The RCCL transport itself runs on
+a multi-GPU node (tests/test_multigpu.py).
 """
 import os
 import socket
@@ -17,6 +20,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from ba_pathtracing_fur_amd import native
 from ba_pathtracing_fur_amd import scenes as S
 from ba_pathtracing_fur_amd import sharding
 
@@ -51,17 +55,22 @@ class OracleBackedCtx:
                       tile_size=tile_size, tile_rank=tile_rank, tile_nranks=tile_nranks)
 
     def gather_framebuffer(self, width, height, spp, depth, tile, nranks, rank, root):
-        if rank != root:
-            m = sharding.owned_mask(width, height, rank, nranks, tile)
-            dist.send(torch.from_numpy(self.fb[m].copy()), dst=root)
+        counts, pix = native.gather_plan(width, height, tile, nranks, rank, root)
+        flat = self.fb.reshape(-1, 3)
+        if rank != root:        # k_pack + ncclSend of counts[rank] pixels
+            assert int(counts.sum()) == int(counts[rank]) == len(pix)
+            dist.send(torch.from_numpy(flat[pix].copy()), dst=root)
             return
+        off = 0                 # ncclRecv of counts[r] pixels per sender, then k_unpack
         for r in range(nranks):
             if r == root:
                 continue
-            m = sharding.owned_mask(width, height, r, nranks, tile)
-            buf = torch.empty((int(m.sum()), 3), dtype=torch.float32)
+            n = int(counts[r])
+            buf = torch.empty((n, 3), dtype=torch.float32)
             dist.recv(buf, src=r)
-            self.fb[m] = buf.numpy()
+            flat[pix[off:off + n]] = buf.numpy()
+            off += n
+        assert off == len(pix)
 
     def sync(self):
         pass
@@ -128,3 +137,35 @@ def test_single_process_needs_no_dist():
     assert ctx.calls[0]["tile_nranks"] == 1 and f.max_over_ranks(2.5) == 2.5
     with pytest.raises(ValueError):
         sharding.ShardedFrame(ctx, 0, 2, None)
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+@pytest.mark.parametrize("w,h,t", [(1920, 1080, 64), (100, 37, 16), (40, 24, 8)])
+def test_gather_plan_sender_matches_root(nranks, w, h, t):
+    """khp_gather_plan: every sender sends exactly the pixels the root expects
+    from it (the round-2 plan had every sender list the ROOT's pixels and send
+    0 floats), and the root's lists are the senders' owned tiles."""
+    for root in sorted({0, nranks - 1}):
+        rc, rpix = native.gather_plan(w, h, t, nranks, root, root)
+        assert rc[root] == 0 and int(rc.sum()) == len(rpix)
+        off = 0
+        for r in range(nranks):
+            if r == root:
+                continue
+            sc, spix = native.gather_plan(w, h, t, nranks, r, root)
+            assert int(sc[r]) == int(rc[r]) == len(spix) > 0 or (int(rc[r]) == 0 and len(spix) == 0)
+            assert int(sc.sum()) == int(sc[r])                   # a sender lists only itself
+            assert np.array_equal(spix, rpix[off:off + len(spix)])
+            m = sharding.owned_mask(w, h, r, nranks, t).reshape(-1)
+            assert np.array_equal(np.sort(spix), np.flatnonzero(m))  # its own tiles, each pixel once
+            off += len(spix)
+        # root's own tiles + everything it receives = the whole frame, each pixel once
+        own = np.flatnonzero(sharding.owned_mask(w, h, root, nranks, t).reshape(-1))
+        allpix = np.concatenate([own, rpix])
+        assert len(allpix) == w * h and len(np.unique(allpix)) == w * h
+
+
+def test_gather_plan_rejects_bad_arguments():
+    for args in [(64, 64, 12, 2, 0, 0), (64, 64, 64, 2, 2, 0), (64, 64, 64, 2, 0, 5), (0, 64, 64, 2, 0, 0)]:
+        with pytest.raises(native.KhpError):
+            native.gather_plan(*args)
