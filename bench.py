@@ -87,6 +87,8 @@ def parse():
     ap.add_argument("--fuse", type=int, default=None, help="khp_ctx_params.fuse_frames (default: the library's)")
     ap.add_argument("--chunk-paths", type=int, default=None, help="khp_ctx_params.chunk_paths")
     ap.add_argument("--frames-in-flight", type=int, default=None, help="khp_ctx_params.frames_in_flight")
+    ap.add_argument("--gui-steps", type=int, default=8,
+                    help="KIRK GUI calls timed: 1 spp per synchronous render + 8-bit texture read (0: skip)")
     ap.add_argument("--iso-steps", type=int, default=8,
                     help="fused passes re-run with serial_stages=1 for the isolated per-kernel rooflines (0: skip)")
     ap.add_argument("--shade-order", type=int, default=None, help="khp_ctx_params.shade_order (1: hits sorted by shading class)")
@@ -323,6 +325,24 @@ def main():
                      "ms_per_step": round(sync_el / args.sync_check_steps * 1e3, 3), "steps": args.sync_check_steps,
                      "def": "one synchronous khp_render per pass (+ gather), no frame fusion"}
 
+    # KIRK's GUI pattern (CPU_PathTracer.cpp:17-52): every
+    # render() call adds ONE sample to every pixel synchronously and the viewer
+    # then reads the 8-bit texture (drawTexture -> Texture::setPixel)
+    gui_line = None
+    if args.gui_steps > 0 and rank == 0 and world == 1:
+        ctx.render(W, H, 1, depth, first_sample=k * spp, readback=False)
+        ctx.read_rgba8(W, H)
+        t1 = time.perf_counter()
+        for g in range(args.gui_steps):
+            ctx.render(W, H, 1, depth, first_sample=k * spp + 1 + g, readback=False)
+            ctx.read_rgba8(W, H)
+        gui_el = time.perf_counter() - t1
+        gui_line = {"value": round(args.gui_steps * W * H / gui_el / 1e6, 3),
+                    "ms_per_call": round(gui_el / args.gui_steps * 1e3, 3), "calls": args.gui_steps,
+                    "def": "KIRK GUI render() calls: one synchronous khp_render of 1 spp + khp_read_rgba8 "
+                           "(8-bit texture to the host) per call"}
+        k += 1   # those samples belong to the pass slot after the last timed one
+
     # the same fused passes with the shadow stage on the extend stream (serial_stages):
     # no two kernels overlap, so each kernel's HIP-event time is its own -- the
     # isolated per-kernel rooflines (k_shadow's overlapped launch time above also
@@ -400,6 +420,7 @@ def main():
             "objects": n_objects, "parallelism": f"tile-sharded {args.tile}px tiles x{world}, RCCL gather",
         },
         "sync_steps": sync_line,
+        "gui_steps": gui_line,
         "isolated": isolated,
         "roofline": {
             "bound": "hbm",
