@@ -213,6 +213,23 @@ def pmc_traffic(frames_per_launch: float, config: str):
         return None
 
 
+def pmc_per_bounce(config: str):
+    """Per-bounce measured / algorithmic read bytes of k_extend from the newest
+    committed PMC profile of this workload (tools/summarize_prof.py), or None."""
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_extend_*.json")))
+    files = [f for f in files if ("_cfg" not in f) == (config == "metric") and
+             (config == "metric" or f"_cfg{config}_" in f)]
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except Exception:
+            continue
+        if d.get("per_bounce"):
+            return os.path.basename(f), d["per_bounce"]
+    return None, None
+
+
 def build_scene(ctx, args, scenes):
     """The configured scene, in HBM.  The hairball of configs 3/5/metric is
     generated and flattened on the device unless --host-scene."""
@@ -368,6 +385,23 @@ def main():
     achieved = (bytes_per_launch * ext_launches) / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
     frames_per_launch = nfr * launches_frame / max(1, ext_launches)
     traffic = None if args.bdpt else pmc_traffic(frames_per_launch, args.config)  # profiles are of the default estimator
+    # per bounce: this run's algorithmic rate (exact visit counts, HIP-event launch
+    # times) next to the measured/algorithmic read ratio of the committed profile
+    prof_name, prof_pb = (None, None) if args.bdpt else pmc_per_bounce(args.config)
+    per_bounce_rl = []
+    for b in range(min(depth, 16)):
+        r_b = cnt["bounce_rays"][b]
+        if not r_b:
+            continue
+        alg_b = 44 * r_b + 32 * (cnt["bounce_nodes"][b] + cnt["bounce_prims"][b])
+        ms_b = last["bounce_extend_ms"][b] / nfr
+        row = {"bounce": b, "alg_GB_per_frame": round(alg_b / 1e9, 3), "ms_per_frame": round(ms_b, 3),
+               "alg_TBps": round(alg_b / (ms_b * 1e-3) / 1e12, 3) if ms_b > 0 else None}
+        pr = next((x for x in (prof_pb or []) if x["bounce"] == b), None)
+        if pr:
+            row["profile_read_over_alg"] = pr["measured_over_alg"]
+            row["profile_read_TBps"] = pr["measured_TBps"]
+        per_bounce_rl.append(row)
     # the any-hit kernel (k_shadow alone; the finish is a separate streaming kernel)
     sh_rays = cnt["shadow_rays"]
     sh_bytes_frame = 32 * sh_rays + 32 * (cnt["shadow_node_visits"] + cnt["shadow_prim_tests"])
@@ -440,6 +474,10 @@ def main():
                             "intervals (= bytes per launch / avg launch duration when launches do not overlap)",
             "per_ray": {"nodes": round(cnt["node_visits"] / max(1, rays), 2),
                         "prims": round(cnt["prim_tests"] / max(1, rays), 2)},
+            "per_bounce": per_bounce_rl,
+            "per_bounce_def": "alg = SURVEY §8(d) bytes of the bounce's exact visit counts; ms = the bounce's "
+                              "k_extend launches (HIP events) per frame; profile_read_* = 2 x FETCH_SIZE of "
+                              f"the bounce's launches in {prof_name} (L2 misses, Infinity-Cache hits included)",
             "shadow": {
                 "kernel": "k_shadow (any-hit BVH2 traversal)",
                 "achieved_def": "algorithmic bytes per launch / average launch duration of the overlapped "

@@ -750,7 +750,11 @@ static int32_t split(struct ko_ctx* c, uint32_t first, uint32_t second, const bo
 }
 
 /* --- traversal ------------------------------------------------------------ */
-typedef struct { uint64_t nodes, prims; } trav_stats_t;
+typedef struct {
+    uint64_t nodes, prims;
+    int32_t* log;        /* optional visit log (tools/treelet_sim.py): preorder ids of visited nodes */
+    uint64_t log_n, log_cap;
+} trav_stats_t;
 
 /* BVHNode::traverse(Intersection*) (CPU_BVH.cpp:148-199) + Container::closestIntersectionWithCandidates
  * (Container.cpp:13-25). */
@@ -758,7 +762,11 @@ static void trav_closest(const struct ko_ctx* c, int32_t ni, const ray_t* r, v3 
                          float tmax, hit_t* hit, trav_stats_t* st) {
     if (tmax < 0.0f || tmin > hit->lambda) return;
     const node_t* n = &c->nodes[ni];
-    if (st) st->nodes++;
+    if (st) {
+        st->nodes++;
+        if (st->log && st->log_n < st->log_cap) st->log[st->log_n] = ni;
+        if (st->log) st->log_n++;
+    }
     if (n->count > 0) {
         hit_t tmp; tmp.lambda = FLT_MAX; tmp.obj = -1; tmp.bu = tmp.bv = 0.0f;
         int found = 0;
@@ -1957,7 +1965,7 @@ int ko_render(ko_ctx* c, const khp_render_params* p, int n_threads, float* out_r
 
 int ko_trace_closest(ko_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out, int32_t* obj_out,
                      float* uv_out, uint64_t* node_visits, uint64_t* prim_tests) {
-    trav_stats_t st = {0, 0};
+    trav_stats_t st = {0, 0, NULL, 0, 0};
     for (uint32_t i = 0; i < n; ++i) {
         ray_t r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
         hit_t h;
@@ -1968,6 +1976,24 @@ int ko_trace_closest(ko_ctx* c, uint32_t n, const float* orig, const float* dir,
     }
     if (node_visits) *node_visits = st.nodes;
     if (prim_tests) *prim_tests = st.prims;
+    return KHP_OK;
+}
+
+/* Dev-tool hook (tools/treelet_sim.py): ko_trace_closest that also records, per
+ * ray, the preorder ids of the nodes KIRK's traversal visits, in visit order.
+ * offsets[n+1]: ray i's visits are log[offsets[i], offsets[i+1]); entries past
+ * cap are counted but not stored. */
+int ko_trace_closest_log(ko_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out, int32_t* log,
+                         uint64_t cap, uint64_t* offsets) {
+    trav_stats_t st = {0, 0, log, 0, cap};
+    for (uint32_t i = 0; i < n; ++i) {
+        offsets[i] = st.log_n;
+        ray_t r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
+        hit_t h;
+        bvh_closest(c, &r, &h, &st);
+        t_out[i] = h.lambda;
+    }
+    offsets[n] = st.log_n;
     return KHP_OK;
 }
 

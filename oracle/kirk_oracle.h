@@ -47,6 +47,8 @@ int ko_render_rows_step(ko_ctx* c, const khp_render_params* p, int n_threads, ui
 
 int ko_trace_closest(ko_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out,
                      int32_t* obj_out, float* uv_out, uint64_t* node_visits, uint64_t* prim_tests);
+int ko_trace_closest_log(ko_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out, int32_t* log,
+                         uint64_t cap, uint64_t* offsets);
 int ko_trace_any(ko_ctx* c, uint32_t n, const float* orig, const float* dir, const float* tmax,
                  uint8_t* hit_out);
 
