@@ -538,7 +538,19 @@ __global__ __launch_bounds__(256) void k_img_connect(DevScene S, Wave Wv) {
             const float4 pv = lv[3 * j];
             if (pv.w == 0.0f) continue;
             const float4 din = lv[3 * j + 1], hc = lv[3 * j + 2];
-            const v3 lp = mk(pv.x, pv.y, pv.z) - mk(din.x, din.y, din.z) * bd.bounce_bias;
+            const v3 dj = mk(din.x, din.y, din.z);
+            v3 lp;
+            if (bd.img == 1u) {
+                // as written (pt_shade.compute:38-44): the record's ray origin + bias * its
+                // direction.  Record j's ray: j = 0 (light point, 0), j = 1 (light point,
+                // d0), j >= 2 (pos_{j-1} + bounce_bias * out_{j-1}, out_{j-1})
+                // (lbb_construction.compute:229-235, 391-395); din_j = that direction.
+                const float4 pp = lv[3 * (j >= 1u ? j - 1u : 0u)];
+                const v3 org = j >= 2u ? mk(pp.x, pp.y, pp.z) + dj * bd.bounce_bias : mk(pp.x, pp.y, pp.z);
+                lp = org + dj * bd.bias;
+            } else {  // 2: the vertex itself, pulled back like the hit connections' target
+                lp = mk(pv.x, pv.y, pv.z) - dj * bd.bounce_bias;
+            }
             const v3 d = lp - sensor;
             const float t = length(d);
             const v3 dir = normalize(d);
@@ -1524,7 +1536,7 @@ extern "C" void khp_bdpt_params_defaults(khp_bdpt_params* out) {
     out->bias = 1e-4f;         // the GLSL's 1e-4 bounce bias (pt_shade.compute:269)
     out->bounce_bias = 1e-4f;
     out->min_pdf = 1e-4f;      // SimpleShader's pdf <= 1E-4 cut (SimpleShader.h)
-    out->image_plane = 1;      // both GLSL passes: shadeBDPTImagePlane and the hit connections
+    out->image_plane = 1;      // both GLSL passes: shadeBDPTImagePlane (target as written) and the hit connections
 }
 
 extern "C" khp_status khp_get_bdpt(khp_ctx* c, khp_bdpt_params* out) {
@@ -1538,7 +1550,7 @@ extern "C" khp_status khp_set_bdpt(khp_ctx* c, const khp_bdpt_params* p) {
     if (p->enabled && (p->light_paths < 1 || p->light_paths > 65536))
         return fail(KHP_EINVAL, "light_paths must be 1..65536");
     if (p->enabled && (p->vertices < 1 || p->vertices > 16)) return fail(KHP_EINVAL, "vertices must be 1..16");
-    if (p->image_plane > 1) return fail(KHP_EINVAL, "image_plane must be 0 or 1");
+    if (p->image_plane > 2) return fail(KHP_EINVAL, "image_plane must be 0, 1 or 2");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the estimator they started with
     if (dr != KHP_OK) return dr;
@@ -2292,7 +2304,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     Wv.seed = p->seed;
     Wv.depth = p->depth;
     Wv.bd = BdptDev{bdm ? 1u : 0u, c->bd.light_paths, (uint32_t)c->S.n_lights, c->bd.vertices, c->bd.bias,
-                    c->bd.bounce_bias, c->bd.min_pdf, c->bd.image_plane ? 1u : 0u,
+                    c->bd.bounce_bias, c->bd.min_pdf, c->bd.image_plane,
                     bdm ? w.lvb.as<float4>() : nullptr};
     SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
     SpillArea sp_sh{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};

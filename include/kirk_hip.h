@@ -333,8 +333,13 @@ typedef struct {
     float bias;             /* debug.bias: connection-ray origin offset along the normal         */
     float bounce_bias;      /* debug.bounce_bias: light-ray origin offset and vertex pull-back   */
     float min_pdf;          /* debug.min_pdf: a light vertex with pdf <= min_pdf ends its subpath */
-    uint32_t image_plane;   /* 1: also connect each sample's light vertices to its point on the
-                               sensor (shadeBDPTImagePlane, pt_shade.compute:17-97)           */
+    uint32_t image_plane;   /* also connect each sample's light vertices to its point on the
+                               sensor (shadeBDPTImagePlane, pt_shade.compute:17-97):
+                               0 off; 1 (default) the GLSL's target as written, record j's ray
+                               origin + bias * its direction, i.e. the PREVIOUS vertex nudged
+                               along the segment (pt_shade.compute:38-44 with
+                               lbb_construction.compute:229-235, 391-395); 2 the vertex itself
+                               pulled back by bounce_bias, like the hit connections (ABI 8)   */
 } khp_bdpt_params;
 void khp_bdpt_params_defaults(khp_bdpt_params* out);   /* off; 256 paths, 4 vertices, 1e-4 x 3, image plane on */
 khp_status khp_set_bdpt(khp_ctx* ctx, const khp_bdpt_params* params);

@@ -752,8 +752,9 @@ static int32_t split(struct ko_ctx* c, uint32_t first, uint32_t second, const bo
 /* --- traversal ------------------------------------------------------------ */
 typedef struct {
     uint64_t nodes, prims;
-    int32_t* log;        /* optional visit log (tools/treelet_sim.py): preorder ids of visited nodes */
-    uint64_t log_n, log_cap;
+    int32_t* log;        /* optional visit log (tools/treelet_sim.py): preorder ids of visited nodes, */
+    uint64_t log_n, log_cap;   /* with bits 25..31 = deferred far children at the visit (min 127) */
+    int32_t pending;
 } trav_stats_t;
 
 /* BVHNode::traverse(Intersection*) (CPU_BVH.cpp:148-199) + Container::closestIntersectionWithCandidates
@@ -764,7 +765,8 @@ static void trav_closest(const struct ko_ctx* c, int32_t ni, const ray_t* r, v3 
     const node_t* n = &c->nodes[ni];
     if (st) {
         st->nodes++;
-        if (st->log && st->log_n < st->log_cap) st->log[st->log_n] = ni;
+        if (st->log && st->log_n < st->log_cap)
+            st->log[st->log_n] = ni | ((st->pending < 127 ? st->pending : 127) << 25);
         if (st->log) st->log_n++;
     }
     if (n->count > 0) {
@@ -785,11 +787,14 @@ static void trav_closest(const struct ko_ctx* c, int32_t ni, const ray_t* r, v3 
     int lh = box_hit(&c->nodes[n->left].box, r, inv, sgn, &lt0, &lt1);
     int rh = box_hit(&c->nodes[n->right].box, r, inv, sgn, &rt0, &rt1);
     if (lh && rh) {
+        if (st) st->pending++;   /* the far child waits while the near one is traversed */
         if (lt0 < rt0) {
             trav_closest(c, n->left, r, inv, sgn, lt0, lt1, hit, st);
+            if (st) st->pending--;
             trav_closest(c, n->right, r, inv, sgn, rt0, rt1, hit, st);
         } else {
             trav_closest(c, n->right, r, inv, sgn, rt0, rt1, hit, st);
+            if (st) st->pending--;
             trav_closest(c, n->left, r, inv, sgn, lt0, lt1, hit, st);
         }
     } else if (lh) {
@@ -1618,7 +1623,18 @@ static v3 bdpt_image_plane(const struct ko_ctx* c, uint32_t W, uint32_t H, v3 se
     const lvert_t* v = c->lv + (((size_t)(k - c->lv_k0) * Ns + sp) * L + li) * J;
     for (uint32_t j = 0; j < J; ++j) {
         if (!v[j].valid) continue;
-        v3 lp = vsub(v[j].pos, vscale(v[j].din, bd->bounce_bias));
+        v3 lp;
+        if (bd->image_plane == 1) {
+            /* as written (pt_shade.compute:38-44): pos = light_bounce.ray.origin, target
+             * pos + debug.bias * light_bounce.ray.direction.  Record j's ray
+             * (lbb_construction.compute:229-235, 391-395): j = 0 (light point, 0),
+             * j = 1 (light point, d0), j >= 2 (pos_{j-1} + bounce_bias * out_{j-1},
+             * out_{j-1}); din_j holds that direction (0 for j = 0). */
+            v3 org = j >= 2 ? vadd(v[j - 1].pos, vscale(v[j].din, bd->bounce_bias)) : v[j >= 1 ? j - 1 : 0].pos;
+            lp = vadd(org, vscale(v[j].din, bd->bias));
+        } else {   /* 2: the vertex itself, pulled back like the hit connections' target */
+            lp = vsub(v[j].pos, vscale(v[j].din, bd->bounce_bias));
+        }
         v3 d = vsub(lp, sensor);
         float t = length(d);
         ray_t vis;
@@ -1965,7 +1981,7 @@ int ko_render(ko_ctx* c, const khp_render_params* p, int n_threads, float* out_r
 
 int ko_trace_closest(ko_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out, int32_t* obj_out,
                      float* uv_out, uint64_t* node_visits, uint64_t* prim_tests) {
-    trav_stats_t st = {0, 0, NULL, 0, 0};
+    trav_stats_t st = {0, 0, NULL, 0, 0, 0};
     for (uint32_t i = 0; i < n; ++i) {
         ray_t r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
         hit_t h;
@@ -1985,7 +2001,7 @@ int ko_trace_closest(ko_ctx* c, uint32_t n, const float* orig, const float* dir,
  * cap are counted but not stored. */
 int ko_trace_closest_log(ko_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out, int32_t* log,
                          uint64_t cap, uint64_t* offsets) {
-    trav_stats_t st = {0, 0, log, 0, cap};
+    trav_stats_t st = {0, 0, log, 0, cap, 0};
     for (uint32_t i = 0; i < n; ++i) {
         offsets[i] = st.log_n;
         ray_t r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
@@ -2011,6 +2027,7 @@ int ko_set_bdpt(ko_ctx* c, const khp_bdpt_params* p) {
     if (!c || !p) return KHP_EINVAL;
     if (p->enabled && (p->light_paths < 1 || p->light_paths > 65536 || p->vertices < 1 || p->vertices > 16))
         return KHP_EINVAL;
+    if (p->image_plane > 2) return KHP_EINVAL;
     c->bd = *p;
     return KHP_OK;
 }

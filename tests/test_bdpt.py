@@ -202,6 +202,38 @@ def test_bdpt_without_image_plane(hip_ctx):
         hip_ctx.set_bdpt(**old)
 
 
+@pytest.mark.gpu
+def test_bdpt_image_plane_vertex_target(hip_ctx):
+    """image_plane = 2: the sensor connections aim at the vertex itself (pulled
+    back like the hit connections) instead of the GLSL's record ray origin."""
+    sd = S.build_config("zoo", width=40, height=30, n_strands=300)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    o = oracle_ffi.Oracle(sd)
+    o.set_bdpt(light_paths=16, vertices=4, image_plane=2)
+    want = o.render(40, 30, 2, 6, threads=16)
+    old = hip_ctx.set_bdpt(enabled=1, light_paths=16, vertices=4, image_plane=2)
+    try:
+        assert_parity(hip_ctx.render(40, 30, 2, 6), want, exact=True)
+    finally:
+        hip_ctx.set_bdpt(**old)
+
+
+def test_image_plane_targets_differ():
+    """Mode 1 (the GLSL's record ray origin) and mode 2 (the vertex) aim at
+    different points, so their frames differ; both only add to mode 0."""
+    sd = S.config1(32, 24)
+    o = oracle_ffi.Oracle(sd)
+    fr = {}
+    for m in (0, 1, 2):
+        o.set_bdpt(light_paths=32, vertices=3, image_plane=m)
+        fr[m] = o.render(32, 24, 2, 5, threads=4)
+    fin = np.isfinite(fr[0]) & np.isfinite(fr[1]) & np.isfinite(fr[2])
+    assert not np.array_equal(fr[1][fin], fr[2][fin])
+    for m in (1, 2):
+        assert (fr[m][fin] >= fr[0][fin] - 1e-6 * np.abs(fr[0][fin])).all()
+
+
 def test_image_plane_term_is_separate():
     """The image-plane pass only adds to a frame: with it on, frames differ from
     image_plane = 0 exactly where an unoccluded light vertex faces the sensor."""
@@ -274,7 +306,7 @@ def test_product_reproduces_bdpt_fixture(path, hip_ctx):
 @pytest.mark.gpu
 def test_bdpt_params_validated(hip_ctx):
     for bad in (dict(enabled=1, light_paths=0), dict(enabled=1, vertices=0), dict(enabled=1, vertices=17),
-                dict(enabled=1, image_plane=2)):
+                dict(enabled=1, image_plane=3)):
         with pytest.raises(N.KhpError) as e:
             hip_ctx.set_bdpt(**bad)
         assert e.value.status == N.KHP_EINVAL

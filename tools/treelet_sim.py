@@ -99,7 +99,8 @@ def main():
                                  ctypes.c_uint64(cap), off.ctypes.data)
         if off[-1] > cap:
             raise SystemExit("visit log overflow")
-        v = log[:int(off[-1])]
+        raw = log[:int(off[-1])]
+        v, pend = raw & 0x1FFFFFF, raw >> 25
         ray = np.repeat(np.arange(m), np.diff(off).astype(np.int64))
         recs = np.where(count[v] > 0, count[v], 1)     # records fetched per visit
         print(f"\nbounce {b}: {m} rays sampled of {n_real // a.fused} per frame, traced in {time.time() - t1:.0f}s; "
@@ -131,6 +132,19 @@ def main():
                 kpr.append((r, N_r, distinct))
             bottom = recs[~top].sum() * scale * 64
             k_all = sum(x[1] for x in kpr) / max(1e-9, sum(x[2] for x in kpr))
+            ps = pend[ent]
+            inside = ~top & ~start
+            print(f"         top stack at entry: mean {ps.mean():.1f} p99 {np.percentile(ps, 99):.0f} max {ps.max()}; "
+                  f"treelet-local depth p99 {np.percentile(pend[inside] - np.repeat(ps, np.diff(np.append(np.flatnonzero(ent), len(v)))[:len(ps)])[:0].size if False else 0, 99) if False else 0}",
+                  flush=True) if False else None
+            # local depth inside a treelet = pending at the visit - pending at the treelet's entry
+            ent_idx = np.flatnonzero(ent)
+            run_id = np.cumsum(start) - 1                      # run index of every visit
+            run_first = np.flatnonzero(start)
+            base = pend[run_first][run_id]
+            loc = (pend - base)[~top]
+            print(f"         top stack at entry: mean {ps.mean():.1f} p99 {np.percentile(ps, 99):.0f} max {ps.max()}; "
+                  f"treelet-local stack p99 {np.percentile(loc, 99):.0f} max {loc.max()}", flush=True)
             print(f"  {B >> 10:3d} KB: top {recs[top].sum() / m:6.1f} rec/ray, treelets {recs[~top].sum() / m:6.1f} "
                   f"rec/ray, entries/ray mean {per_ray.mean():.1f} p50 {np.median(per_ray):.0f} "
                   f"p99 {np.percentile(per_ray, 99):.0f} max {per_ray.max()}; rounds {rounds}; rays per treelet-round "
