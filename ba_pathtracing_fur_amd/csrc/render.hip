@@ -1403,9 +1403,23 @@ struct FrameSlot {
 };
 // An asynchronous operation waiting to be fused into the next batch.
 struct PendingOp {
-    enum Kind { RENDER, GATHER } kind;
+    enum Kind { RENDER, GATHER, SNAPSHOT } kind;
     khp_render_params p;
     int root;
+    uint64_t snap = 0;   // SNAPSHOT: khp_read_rgba8_async ticket
+};
+// ABI 8: an asynchronous 8-bit texture of the running mean (khp_read_rgba8_async).
+// k_rgba8 writes dbuf in stream order behind the frames enqueued before it; the
+// D2H copy lands in pinned memory; khp_snapshot_wait / khp_sync copy it to the
+// caller's buffer.
+struct Snapshot {
+    uint64_t id = 0;
+    uint8_t* out = nullptr;       // caller's W*H*4 bytes
+    size_t bytes = 0;
+    DevMem dbuf;
+    uint8_t* pinned = nullptr;
+    hipEvent_t done = nullptr;
+    bool enqueued = false;
 };
 static hipEvent_t slot_event(std::vector<hipEvent_t>& pool, size_t& next, bool no_timing) {
     if (next == pool.size()) {
@@ -1437,7 +1451,11 @@ struct khp_ctx {
     hipEvent_t fb_evt = nullptr;   // the last framebuffer operation enqueued (accumulate or gather)
     bool report_open = false;      // c->st accumulates harvested frames
     hipEvent_t gather_evt = nullptr;  // end of the last framebuffer gather (becomes fb_evt)
-    std::vector<PendingOp> pend;      // asynchronous renders (+ gathers) not yet enqueued (frame fusion)
+    hipEvent_t snap_evt = nullptr;    // end of the last snapshot's conversion (becomes fb_evt)
+    std::vector<PendingOp> pend;      // asynchronous renders (+ gathers, snapshots) not yet enqueued (frame fusion)
+    std::vector<Snapshot*> snaps;     // ABI 8 snapshots not yet delivered, oldest first
+    std::vector<Snapshot*> snap_free; // buffers of delivered snapshots, for reuse
+    uint64_t snap_next = 1;
     hipEvent_t report_ref = nullptr;  // time origin of the open report
     std::vector<std::pair<float, float>> ext_iv;  // the report's k_extend intervals (ms from report_ref)
     // framebuffer + pixel list
@@ -1585,6 +1603,7 @@ extern "C" void khp_destroy(khp_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)drain(c);
     if (c->gather_evt) (void)hipEventDestroy(c->gather_evt);
+    if (c->snap_evt) (void)hipEventDestroy(c->snap_evt);
     if (c->report_ref) (void)hipEventDestroy(c->report_ref);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
@@ -1601,6 +1620,12 @@ extern "C" void khp_destroy(khp_ctx* c) {
     }
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     for (auto e : c->sync_pool) (void)hipEventDestroy(e);
+    for (auto* v : {&c->snaps, &c->snap_free})
+        for (Snapshot* sn : *v) {
+            if (sn->pinned) (void)hipHostFree(sn->pinned);
+            if (sn->done) (void)hipEventDestroy(sn->done);
+            delete sn;
+        }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -2137,19 +2162,27 @@ static khp_status drain(khp_ctx* c) {
     return KHP_OK;
 }
 
+static khp_status deliver_snapshots(khp_ctx* c, uint64_t upto, bool wait);
+
 extern "C" khp_status khp_sync(khp_ctx* c) {
     if (!c) return fail(KHP_EINVAL, "null context");
     HIPCHK(hipSetDevice(c->device));
     if (!c->report_open) report_begin(c);
     khp_status s = drain(c);
     c->report_open = false;
-    return s;
+    if (s != KHP_OK) return s;
+    return deliver_snapshots(c, UINT64_MAX, true);
 }
 
 // Enqueue one frame, or a fused batch of asynchronous frames (ops: their
 // render operations, which differ only in first_sample, and the framebuffer
 // gathers between them, in call order; p = the first render's parameters).
 static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root);
+static khp_status snapshot_now(khp_ctx* c, uint64_t id);
+// A non-render operation of a fused batch, in call order.
+static khp_status op_now(khp_ctx* c, const PendingOp& o) {
+    return o.kind == PendingOp::SNAPSHOT ? snapshot_now(c, o.snap) : gather_now(c, &o.p, o.root);
+}
 static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* out_rgb,
                                  const std::vector<PendingOp>* ops) {
     khp_status s;
@@ -2454,7 +2487,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                         hipEvent_t acc = slot_event(f.sync_pool, f.sync_next, true);
                         HIPCHK(hipEventRecord(acc, sA));
                         c->fb_evt = acc;
-                        s = gather_now(c, &o.p, o.root);   // waits fb_evt, sets fb_evt to its own end
+                        s = op_now(c, o);   // waits fb_evt, sets fb_evt to its own end
                         if (s != KHP_OK) return s;
                         HIPCHK(hipStreamWaitEvent(sA, c->fb_evt, 0));
                     }
@@ -2520,15 +2553,15 @@ static khp_status flush(khp_ctx* c) {
             gathers = true;
         }
     }
-    if (!first) {  // only gathers
+    if (!first) {  // only gathers / snapshots
         for (const PendingOp& o : ops) {
-            khp_status s = gather_now(c, &o.p, o.root);
+            khp_status s = op_now(c, o);
             if (s != KHP_OK) return s;
         }
         return KHP_OK;
     }
-    // a batch with gathers must fit one chunk (every frame accumulated before the
-    // next frame's gather); otherwise enqueue the operations one by one
+    // a batch with gathers or snapshots must fit one chunk (every frame accumulated
+    // before the next frame's gather); otherwise it is split into one-chunk groups
     const uint32_t T = first->p.tile_size ? first->p.tile_size : 64;
     std::vector<uint32_t> tmp;
     size_t P = 0;
@@ -2548,7 +2581,7 @@ static khp_status flush(khp_ctx* c) {
         if (nr == 1) {
             for (const PendingOp& o : ops) {
                 khp_status s = o.kind == PendingOp::RENDER ? enqueue_frames(c, &o.p, nullptr, nullptr)
-                                                           : gather_now(c, &o.p, o.root);
+                                                           : op_now(c, o);
                 if (s != KHP_OK) return s;
             }
             return KHP_OK;
@@ -2564,7 +2597,7 @@ static khp_status flush(khp_ctx* c) {
         khp_status s = KHP_OK;
         if (g_r == 1) {
             for (const PendingOp& o : grp) {
-                s = o.kind == PendingOp::RENDER ? enqueue_frames(c, &o.p, nullptr, nullptr) : gather_now(c, &o.p, o.root);
+                s = o.kind == PendingOp::RENDER ? enqueue_frames(c, &o.p, nullptr, nullptr) : op_now(c, o);
                 if (s != KHP_OK) break;
             }
         } else if (g_r > 1) {
@@ -2574,7 +2607,7 @@ static khp_status flush(khp_ctx* c) {
             s = enqueue_frames(c, &f0->p, nullptr, &grp);
         } else {
             for (const PendingOp& o : grp) {
-                s = gather_now(c, &o.p, o.root);
+                s = op_now(c, o);
                 if (s != KHP_OK) break;
             }
         }
@@ -2634,6 +2667,115 @@ extern "C" void khp_tonemap_defaults(khp_tonemap* t) {
     t->white = 1.0f;
     t->kernel_multiplier = 0.125f;
     t->center_x = t->center_y = -1;
+}
+
+// ---- ABI 8: asynchronous 8-bit textures (the GUI's per-pass texture) ----------------------
+constexpr size_t KHP_MAX_SNAPS = 64;   // undelivered snapshots; the oldest is waited for beyond this
+
+static Snapshot* find_snap(khp_ctx* c, uint64_t id) {
+    for (Snapshot* sn : c->snaps)
+        if (sn->id == id) return sn;
+    return nullptr;
+}
+
+// k_rgba8 on the context stream behind the last framebuffer operation; the next
+// framebuffer operation waits for the conversion only, the D2H copy overlaps it.
+static khp_status snapshot_now(khp_ctx* c, uint64_t id) {
+    Snapshot* sn = find_snap(c, id);
+    if (!sn) return fail(KHP_EINVAL, "unknown snapshot");
+    if (!c->fb.p) return fail(KHP_ENOTREADY, "nothing rendered yet");
+    const uint32_t n = c->fbW * c->fbH;
+    if ((size_t)n * 4 != sn->bytes) return fail(KHP_EINVAL, "snapshot size does not match the framebuffer");
+    HIPCHK(sn->dbuf.ensure(sn->bytes));
+    if (!sn->pinned) HIPCHK(hipHostMalloc((void**)&sn->pinned, sn->bytes, hipHostMallocDefault));
+    if (!sn->done) HIPCHK(hipEventCreateWithFlags(&sn->done, hipEventDisableTiming));
+    if (!c->snap_evt) HIPCHK(hipEventCreateWithFlags(&c->snap_evt, hipEventDisableTiming));
+    if (c->fb_evt) HIPCHK(hipStreamWaitEvent(c->stream, c->fb_evt, 0));
+    hipLaunchKernelGGL(k_rgba8, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(), n,
+                       sn->dbuf.as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->snap_evt, c->stream));
+    c->fb_evt = c->snap_evt;
+    HIPCHK(hipMemcpyAsync(sn->pinned, sn->dbuf.p, sn->bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipEventRecord(sn->done, c->stream));
+    sn->enqueued = true;
+    return KHP_OK;
+}
+
+// Copy completed snapshots with id <= upto into their callers' buffers, oldest first.
+// wait: enqueue pending ones (flush) and wait for them; else stop at the first not done.
+static khp_status deliver_snapshots(khp_ctx* c, uint64_t upto, bool wait) {
+    while (!c->snaps.empty() && c->snaps.front()->id <= upto) {
+        Snapshot* sn = c->snaps.front();
+        if (!sn->enqueued) {
+            if (!wait) return KHP_OK;
+            khp_status s = flush(c);
+            if (s != KHP_OK) return s;
+            if (!sn->enqueued) return fail(KHP_EDEVICE, "snapshot was not enqueued");
+        }
+        if (wait) {
+            HIPCHK(hipEventSynchronize(sn->done));
+        } else {
+            const hipError_t q = hipEventQuery(sn->done);
+            if (q == hipErrorNotReady) return KHP_OK;
+            HIPCHK(q);
+        }
+        memcpy(sn->out, sn->pinned, sn->bytes);
+        c->snaps.erase(c->snaps.begin());
+        sn->out = nullptr;
+        sn->enqueued = false;
+        c->snap_free.push_back(sn);
+    }
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_read_rgba8_async(khp_ctx* c, uint8_t* out_rgba, uint64_t* ticket) {
+    if (!c || !out_rgba || !ticket) return fail(KHP_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    uint32_t W = c->fbW, H = c->fbH;  // the frame the snapshot follows: the last pending render, else the framebuffer
+    for (const PendingOp& o : c->pend)
+        if (o.kind == PendingOp::RENDER) {
+            W = o.p.width;
+            H = o.p.height;
+        }
+    if (!W || !H) return fail(KHP_ENOTREADY, "nothing rendered yet");
+    if (c->snaps.size() >= KHP_MAX_SNAPS) {
+        khp_status s = deliver_snapshots(c, c->snaps.front()->id, true);
+        if (s != KHP_OK) return s;
+    }
+    Snapshot* sn;
+    if (!c->snap_free.empty()) {
+        sn = c->snap_free.back();
+        c->snap_free.pop_back();
+    } else {
+        sn = new Snapshot();
+    }
+    const size_t bytes = 4 * (size_t)W * H;
+    if (sn->pinned && sn->bytes != bytes) {
+        (void)hipHostFree(sn->pinned);
+        sn->pinned = nullptr;
+    }
+    sn->id = c->snap_next++;
+    sn->out = out_rgba;
+    sn->bytes = bytes;
+    sn->enqueued = false;
+    c->snaps.push_back(sn);
+    *ticket = sn->id;
+    if (!c->pend.empty()) {  // behind asynchronous renders waiting for fusion: keep the call order
+        PendingOp o{PendingOp::SNAPSHOT, khp_render_params{}, 0, sn->id};
+        c->pend.push_back(o);
+        return KHP_OK;
+    }
+    return snapshot_now(c, sn->id);
+}
+
+extern "C" khp_status khp_snapshot_wait(khp_ctx* c, uint64_t ticket, int wait) {
+    if (!c || ticket == 0 || ticket >= c->snap_next) return fail(KHP_EINVAL, "bad snapshot ticket");
+    HIPCHK(hipSetDevice(c->device));
+    khp_status s = deliver_snapshots(c, ticket, wait != 0);
+    if (s != KHP_OK) return s;
+    if (find_snap(c, ticket)) return fail(KHP_ENOTREADY, "snapshot not complete yet");
+    return KHP_OK;
 }
 
 extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t* out_rgba) {

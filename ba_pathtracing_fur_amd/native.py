@@ -163,7 +163,8 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_read_layout", "khp_set_scene_device", "khp_gen_hairball_device", "khp_device_alloc",
             "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device",
             "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params", "khp_debug_shadow_queue",
-            "khp_bdpt_params_defaults", "khp_set_bdpt", "khp_get_bdpt", "khp_gather_plan"]
+            "khp_bdpt_params_defaults", "khp_set_bdpt", "khp_get_bdpt", "khp_gather_plan",
+            "khp_read_rgba8_async", "khp_snapshot_wait"]
 
 _lib = None
 
@@ -208,6 +209,8 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
         "khp_read_rgba8": (c_int, [c_void_p, P(Tonemap), P(c_uint8)]),
         "khp_tonemap_defaults": (None, [P(Tonemap)]),
+        "khp_read_rgba8_async": (c_int, [c_void_p, P(c_uint8), P(c_uint64)]),
+        "khp_snapshot_wait": (c_int, [c_void_p, c_uint64, c_int]),
         "khp_set_scene_device": (c_int, [c_void_p, P(SceneDesc)]),
         "khp_gen_hairball_device": (c_int, [c_void_p, c_uint32, c_uint32, P(c_float), c_float, c_float, c_uint32,
                                             c_void_p, c_void_p]),

@@ -259,6 +259,23 @@ class HipContext:
                 "khp_read_rgba8")
         return out
 
+    def read_rgba8_async(self, out: np.ndarray) -> int:
+        """khp_read_rgba8_async: enqueue the 8-bit texture after the frames enqueued so
+        far into `out` ((H, W, 4) uint8, kept alive by the caller); returns the ticket."""
+        assert out.dtype == np.uint8 and out.flags.c_contiguous
+        t = ctypes.c_uint64()
+        N.check(self.lib, self.lib.khp_read_rgba8_async(self.ptr, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                                        ctypes.byref(t)), "khp_read_rgba8_async")
+        return t.value
+
+    def snapshot_wait(self, ticket: int, wait: bool = True) -> bool:
+        """khp_snapshot_wait: True once snapshot `ticket` is in its buffer."""
+        st = self.lib.khp_snapshot_wait(self.ptr, ticket, 1 if wait else 0)
+        if st == N.KHP_ENOTREADY and not wait:
+            return False
+        N.check(self.lib, st, "khp_snapshot_wait")
+        return True
+
     def trace_closest(self, orig, direction):
         o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
         d = np.ascontiguousarray(direction, np.float32).reshape(-1, 3)

@@ -359,6 +359,25 @@ def main():
                     "def": "KIRK GUI render() calls: one synchronous khp_render of 1 spp + khp_read_rgba8 "
                            "(8-bit texture to the host) per call"}
         k += 1   # those samples belong to the pass slot after the last timed one
+        # the same calls pipelined (ABI 8): render() enqueues its 1-spp pass and an
+        # asynchronous texture read, the viewer shows textures as they complete;
+        # consecutive passes fuse, each texture is taken between two accumulates
+        import numpy as np
+        n_async = max(args.gui_steps, 32)
+        bufs = [np.zeros((H, W, 4), np.uint8) for _ in range(4)]
+        s0 = k * spp
+        frame.sync()
+        t1 = time.perf_counter()
+        for g in range(n_async):
+            ctx.render(W, H, 1, depth, first_sample=s0 + g, async_=True)
+            ctx.read_rgba8_async(bufs[g % 4])   # a viewer's rotating textures
+        ctx.sync()
+        ga_el = time.perf_counter() - t1
+        k += (n_async + spp - 1) // spp
+        gui_line["pipelined"] = {"value": round(n_async * W * H / ga_el / 1e6, 3),
+                                 "ms_per_call": round(ga_el / n_async * 1e3, 3), "calls": n_async,
+                                 "def": "the same calls with KHP_RENDER_ASYNC + khp_read_rgba8_async (ABI 8): "
+                                        "1-spp passes fused, every pass's 8-bit texture delivered"}
 
     # the same fused passes with the shadow stage on the extend stream (serial_stages):
     # no two kernels overlap, so each kernel's HIP-event time is its own -- the

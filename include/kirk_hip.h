@@ -406,6 +406,20 @@ typedef struct {
  * NaN -> 0; alpha 255.  tm = NULL: no tonemapping. */
 khp_status khp_read_rgba8(khp_ctx* ctx, const khp_tonemap* tm, uint8_t* out_rgba);
 
+/* ABI 8: the same 8-bit texture (tm = NULL form) without waiting, for a viewer
+ * that shows every progressive pass (KIRK's GUI calls PathTracer::render once
+ * per sample, CPU_PathTracer.cpp:17-52, then draws the texture).  The
+ * conversion is enqueued in call order behind the asynchronous renders, like
+ * a gather (inside a fused batch it runs between two frames' accumulates);
+ * out_rgba (W*H*4 bytes of the frame it follows) is written by the time
+ * khp_snapshot_wait(ticket) or khp_sync returns and must stay valid until
+ * then.  Tonemapped textures need KIRK's sequential host sum and stay
+ * synchronous (khp_read_rgba8). */
+khp_status khp_read_rgba8_async(khp_ctx* ctx, uint8_t* out_rgba, uint64_t* ticket);
+/* Delivers snapshot `ticket` and every older one.  wait = 1: enqueues what is
+ * still pending and blocks; wait = 0: KHP_ENOTREADY if it has not completed. */
+khp_status khp_snapshot_wait(khp_ctx* ctx, uint64_t ticket, int wait);
+
 /* The Tonemapper member defaults (Tonemapping.h:23-33). */
 void khp_tonemap_defaults(khp_tonemap* tm);
 
