@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <string>
 #include <thread>
 #include <type_traits>
@@ -1482,7 +1483,15 @@ struct khp_ctx {
     std::vector<uint64_t> gather_counts; // khp_gather_plan counts: root: per sender; sender: its own
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // ABI 8 in-process group (khp_comm_init_local): the gather's transport between
+    // contexts of one process instead of RCCL; a sender's k-th gather packs into
+    // ring slot k % LG_SLOTS, the root's k-th gather copies every sender's slot k
+    std::shared_ptr<std::vector<khp_ctx*>> lgroup;
+    DevMem lg_slots[64];
+    hipEvent_t lg_evts[64] = {};
+    uint64_t lg_seq = 0;
 };
+constexpr size_t LG_SLOTS = 64;
 
 static khp_status drain(khp_ctx* c);
 
@@ -1607,6 +1616,11 @@ extern "C" void khp_destroy(khp_ctx* c) {
     if (c->report_ref) (void)hipEventDestroy(c->report_ref);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->lgroup)
+        for (auto& m : *c->lgroup)
+            if (m == c) m = nullptr;
+    for (auto e : c->lg_evts)
+        if (e) (void)hipEventDestroy(e);
     for (auto& w : c->ps) {
         for (hipStream_t s : {w.sA, w.sB}) {
             if (!s) continue;
@@ -3177,10 +3191,32 @@ extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint
     return KHP_OK;
 }
 
+extern "C" khp_status khp_comm_init_local(khp_ctx* const* ctxs, int nranks) {
+    if (!ctxs || nranks < 1) return fail(KHP_EINVAL, "bad local group");
+    for (int r = 0; r < nranks; ++r)
+        if (!ctxs[r]) return fail(KHP_EINVAL, "null context in local group");
+    auto g = std::make_shared<std::vector<khp_ctx*>>(ctxs, ctxs + nranks);
+    for (int r = 0; r < nranks; ++r) {
+        khp_ctx* c = ctxs[r];
+        khp_status dr = drain(c);
+        if (dr != KHP_OK) return dr;
+        if (c->comm) {
+            ncclCommDestroy(c->comm);
+            c->comm = nullptr;
+        }
+        c->lgroup = g;
+        c->nranks = nranks;
+        c->rank = r;
+        c->lg_seq = 0;
+        memset(c->gather_key, 0, sizeof(c->gather_key));
+    }
+    return KHP_OK;
+}
+
 extern "C" khp_status khp_gather_framebuffer(khp_ctx* c, const khp_render_params* p, int root) {
     khp_status s = check_params(c, p);
     if (s != KHP_OK) return s;
-    if (!c->comm) return fail(KHP_ENOTREADY, "khp_comm_init first");
+    if (!c->comm && !c->lgroup) return fail(KHP_ENOTREADY, "khp_comm_init first");
     if (root < 0 || root >= c->nranks) return fail(KHP_EINVAL, "bad root");
     if (p->tile_nranks != (uint32_t)c->nranks) return fail(KHP_EINVAL, "tile_nranks must equal the comm size");
     if (!c->pend.empty()) {  // behind asynchronous renders waiting for fusion: keep the call order
@@ -3193,7 +3229,7 @@ extern "C" khp_status khp_gather_framebuffer(khp_ctx* c, const khp_render_params
 static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root) {
     khp_status s = check_params(c, p);
     if (s != KHP_OK) return s;
-    if (!c->comm) return fail(KHP_ENOTREADY, "khp_comm_init first");
+    if (!c->comm && !c->lgroup) return fail(KHP_ENOTREADY, "khp_comm_init first");
     if (!c->fb.p || c->fbW != p->width || c->fbH != p->height) return fail(KHP_ENOTREADY, "render first");
     if (root < 0 || root >= c->nranks) return fail(KHP_EINVAL, "bad root");
     if (p->tile_nranks != (uint32_t)c->nranks) return fail(KHP_EINVAL, "tile_nranks must equal the comm size");
@@ -3217,6 +3253,18 @@ static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root) {
     if (c->fb_evt) HIPCHK(hipStreamWaitEvent(c->stream, c->fb_evt, 0));
     if (c->rank != root) {
         uint32_t P = (uint32_t)c->gather_counts[c->rank];
+        if (c->lgroup) {  // in-process group: pack into this gather's ring slot, the root copies it
+            const size_t k = c->lg_seq++ % LG_SLOTS;
+            HIPCHK(c->lg_slots[k].ensure((size_t)P * 3 * sizeof(float) + 16));
+            if (!c->lg_evts[k]) HIPCHK(hipEventCreateWithFlags(&c->lg_evts[k], hipEventDisableTiming));
+            if (P) hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
+                                      c->stage_pix.as<uint32_t>(), P, c->lg_slots[k].as<float>());
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(c->lg_evts[k], c->stream));
+            HIPCHK(hipEventRecord(c->gather_evt, c->stream));
+            c->fb_evt = c->gather_evt;
+            return KHP_OK;
+        }
         if (P) hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
                                   c->stage_pix.as<uint32_t>(), P, c->stage.as<float>());
         NCCLCHK(ncclSend(c->stage.p, (size_t)P * 3, ncclFloat32, root, c->comm, c->stream));
@@ -3227,14 +3275,30 @@ static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root) {
     }
     // root: receive every other rank's pixels (one grouped recv), then scatter them into the framebuffer
     size_t total = 0;
-    NCCLCHK(ncclGroupStart());
-    for (int r = 0; r < c->nranks; ++r) {
-        if (r == root) continue;
-        NCCLCHK(ncclRecv(c->stage.as<float>() + total * 3, c->gather_counts[r] * 3, ncclFloat32, r, c->comm,
-                         c->stream));
-        total += c->gather_counts[r];
+    if (c->lgroup) {  // in-process group: the senders' slot k of this gather (their k-th gather)
+        const size_t k = c->lg_seq++ % LG_SLOTS;
+        for (int r = 0; r < c->nranks; ++r) {
+            if (r == root) continue;
+            khp_ctx* sc = (*c->lgroup)[r];
+            if (!sc || !sc->lg_evts[k])
+                return fail(KHP_ENOTREADY, "local group: a sender has not enqueued this gather yet");
+            HIPCHK(hipStreamWaitEvent(c->stream, sc->lg_evts[k], 0));
+            const size_t n = c->gather_counts[r];
+            if (n)
+                HIPCHK(hipMemcpyAsync(c->stage.as<float>() + total * 3, sc->lg_slots[k].p, n * 3 * sizeof(float),
+                                      hipMemcpyDeviceToDevice, c->stream));
+            total += n;
+        }
+    } else {
+        NCCLCHK(ncclGroupStart());
+        for (int r = 0; r < c->nranks; ++r) {
+            if (r == root) continue;
+            NCCLCHK(ncclRecv(c->stage.as<float>() + total * 3, c->gather_counts[r] * 3, ncclFloat32, r, c->comm,
+                             c->stream));
+            total += c->gather_counts[r];
+        }
+        NCCLCHK(ncclGroupEnd());
     }
-    NCCLCHK(ncclGroupEnd());
     if (total)
         hipLaunchKernelGGL(k_unpack, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, c->stream,
                            c->fb.as<float>(), c->stage_pix.as<uint32_t>(), (uint32_t)total, c->stage.as<float>());

@@ -164,7 +164,7 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device",
             "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params", "khp_debug_shadow_queue",
             "khp_bdpt_params_defaults", "khp_set_bdpt", "khp_get_bdpt", "khp_gather_plan",
-            "khp_read_rgba8_async", "khp_snapshot_wait"]
+            "khp_read_rgba8_async", "khp_snapshot_wait", "khp_comm_init_local"]
 
 _lib = None
 
@@ -230,6 +230,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_comm_unique_id": (c_int, [P(c_uint8)]),
         "khp_comm_init": (c_int, [c_void_p, c_int, c_int, P(c_uint8)]),
         "khp_gather_framebuffer": (c_int, [c_void_p, P(RenderParams), c_int]),
+        "khp_comm_init_local": (c_int, [P(c_void_p), c_int]),
         "khp_gather_plan": (c_int, [c_uint32, c_uint32, c_uint32, c_int, c_int, c_int, P(c_uint64), P(c_uint32),
                                     P(c_uint64)]),
         "khp_bsdf_kind_from_name": (c_int, [c_char_p]),

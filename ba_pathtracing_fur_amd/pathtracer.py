@@ -328,6 +328,14 @@ class HipContext:
         N.check(self.lib, self.lib.khp_gather_framebuffer(self.ptr, ctypes.byref(p), root), "khp_gather_framebuffer")
 
 
+def comm_init_local(ctxs) -> None:
+    """khp_comm_init_local: contexts of this process as the ranks of one gather group
+    (rank = position), the framebuffer gather moving over device copies, not RCCL."""
+    lib = N.load_library()
+    arr = (ctypes.c_void_p * len(ctxs))(*[c.ptr.value for c in ctxs])
+    N.check(lib, lib.khp_comm_init_local(arr, len(ctxs)), "khp_comm_init_local")
+
+
 def comm_unique_id() -> bytes:
     lib = N.load_library()
     buf = (ctypes.c_uint8 * 128)()

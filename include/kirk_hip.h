@@ -444,6 +444,17 @@ khp_status khp_comm_init(khp_ctx* ctx, int nranks, int rank, const uint8_t id[12
  * framebuffer over RCCL; root may then khp_read_framebuffer. Collective. */
 khp_status khp_gather_framebuffer(khp_ctx* ctx, const khp_render_params* p, int root);
 
+/* ABI 8: an in-process group of contexts (rank = index in ctxs) for
+ * khp_gather_framebuffer without RCCL -- RCCL needs one GPU per rank, this
+ * transport lets one process (e.g. a single-GPU test box) run every rank's
+ * contexts and the product's gather plan, pack and unpack kernels.  A
+ * sender's k-th gather packs into ring slot k % 64 and records an event; the
+ * root's k-th gather waits for every sender's slot k, so each sender must have
+ * ENQUEUED its k-th gather (khp_sync flushes fused frames) before the root's
+ * k-th gather is enqueued, and no sender may run 64 gathers ahead.  Destroy
+ * the members together. */
+khp_status khp_comm_init_local(khp_ctx* const* ctxs, int nranks);
+
 /* ABI 8: the pixel plan khp_gather_framebuffer moves, as seen from `rank`
  * (host only, no device needed).  KIRK has no multi-device path; its analogue
  * is the square-segment split of BufferSegmentation (Utils/BufferSegmentation.h:

@@ -53,3 +53,37 @@ def test_bench_launches_its_own_ranks():
                          timeout=300, capture_output=True, text=True).stdout
     line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("async_", [False, True])
+def test_local_group_gather_assembles_the_frame(world, async_):
+    """The product's gather on ONE GPU: `world` contexts of this process as the
+    ranks (khp_comm_init_local), each rendering its tiles (t % world == rank),
+    the gather moving the senders' pixels with the same plan (khp_gather_plan),
+    k_pack and k_unpack as the RCCL path -- only the transport differs (device
+    copies instead of ncclSend/ncclRecv).  Rank 0's frame must be the oracle's
+    single-rank frame bit for bit, for synchronous passes and for fused
+    asynchronous passes with a gather after each."""
+    from ba_pathtracing_fur_amd.pathtracer import HipContext, comm_init_local
+    W, H, SPP, TILE, PASSES = 96, 64, 2, 16, 3
+    sd = S.config2(W, H, n_strands=1500)
+    want = oracle_ffi.Oracle(sd).render(W, H, SPP * PASSES, 5, threads=16)
+    ctxs = [HipContext(0) for _ in range(world)]
+    try:
+        for c in ctxs:
+            c.set_scene(sd)
+            c.build_accel()
+        comm_init_local(ctxs)
+        for k in range(PASSES):
+            for r in reversed(range(world)):   # senders enqueue their k-th gather before the root
+                ctxs[r].render(W, H, SPP, 5, first_sample=k * SPP, tile_size=TILE, tile_rank=r, tile_nranks=world,
+                               readback=False, async_=async_)
+                ctxs[r].gather_framebuffer(W, H, SPP, 5, TILE, world, r, 0)
+        for c in ctxs[1:]:                     # flush the senders' fused batches first
+            c.sync()
+        ctxs[0].sync()
+        assert_parity(ctxs[0].read_framebuffer(W, H), want, exact=True)
+    finally:
+        for c in ctxs:
+            c.close()
