@@ -2268,6 +2268,14 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     if (nf > 1) {
         P_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(std::max<uint32_t>(1, P_all),
                                                                  cap_paths / ((size_t)p->spp * nf)));
+        // equal chunks (in whole 64-pixel blocks where that stays under the cap): 20 fused
+        // 8-spp 1080p frames are 3 chunks of 691k pixels instead of 839k + 839k + 395k, so
+        // no chunk's launches run a short, tail-dominated wavefront
+        const uint32_t n_ch = (P_all + P_chunk - 1) / std::max<uint32_t>(1, P_chunk);
+        if (n_ch > 1) {
+            const uint32_t even = (P_all + n_ch - 1) / n_ch, blk = (even + 63u) & ~63u;
+            P_chunk = blk <= P_chunk ? blk : even;
+        }
         S_chunk = p->spp;
     } else {
         P_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(P_all, cap_paths));
