@@ -9,7 +9,7 @@ PASSES=${@:-trace fetch write sq}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/bench.py --no-cpu-baseline --sync-check-steps 0 --iso-steps 0 --config ${CFG:-metric}"  # every k_extend launch of the run then carries the same fused frames
+B="python3 $R/bench.py --no-cpu-baseline --sync-check-steps 0 --iso-steps 0 --gui-steps 0 --config ${CFG:-metric}"  # every k_extend launch of the run then carries the same fused frames
 for p in $PASSES; do
   case $p in
     list)  timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true ;;
