@@ -394,239 +394,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wa
                     &Wv.cnt->lanes_busy, &Wv.cnt->spills);
 }
 
-// ---- extend with mode-sorted lanes (khp_ctx_params.lane_sort = 1, round 3) -------------------
-// In k_extend a wave whose lanes hold both interior entries and opened leaves
-// issues the slab pair AND KIRK's cone test every iteration (both branches of
-// iter2, ~250 VALU), and lanes whose ray is done sit idle until 24 are.  Here
-// every wave runs ONE kind per iteration -- interior steps (step_node) or
-// candidate tests (step_leaf) -- on lanes that all hold that kind: a lane
-// whose ray needs the other kind parks it in the wave's LDS pool and takes a
-// parked ray of the running kind (or a new one from the queue).  A ray's
-// stack ring stays in its ray slot (SidStack), so parking moves only its
-// registers.  Each ray still runs iter2's steps in iter2's order, so hits and
-// visit counts are k_extend's.
-namespace ls {
-constexpr int RING = 6;             // stack ring entries per ray slot
-constexpr int POOL = 32;            // parked rays per wave
-constexpr int SLOTS = 64 + POOL;    // ray slots (stack owners) per wave
-constexpr int NST = 26;             // dwords of a parked ray
-constexpr int OFF_POOL = 3 * RING * SLOTS;
-constexpr int OFF_LIST = OFF_POOL + NST * POOL;  // [3][POOL]: parked node-kind, parked leaf-kind, free pool slots
-constexpr int OFF_SID = OFF_LIST + 3 * POOL;     // [SLOTS] free ray slots
-constexpr int WORDS = OFF_SID + SLOTS;
-constexpr size_t LDS_BYTES = (size_t)WORDS * 4;
-constexpr int WAVES = 4;            // __launch_bounds__ waves per SIMD (LDS allows ~3.6)
-constexpr uint32_t KEEP = 40;       // a wave keeps its kind while this many rays of it are at hand
-}  // namespace ls
-
-// The registers of one ray (what parking moves).
-struct LsRay {
-    TravRay tr;
-    Hit h;
-    Cur c;
-    LeafCur lf;
-    uint32_t mode, idx, it, sid;
-    int sp, lo;
-};
-
-__device__ __forceinline__ void ls_store(uint32_t* pool, uint32_t q, const LsRay& r) {
-    uint32_t* P = pool + q;
-    auto W = [&](int f, uint32_t v) { P[f * ls::POOL] = v; };
-    W(0, __float_as_uint(r.tr.r.o.x)); W(1, __float_as_uint(r.tr.r.o.y)); W(2, __float_as_uint(r.tr.r.o.z));
-    W(3, __float_as_uint(r.tr.r.d.x)); W(4, __float_as_uint(r.tr.r.d.y)); W(5, __float_as_uint(r.tr.r.d.z));
-    W(6, __float_as_uint(r.tr.inv.x)); W(7, __float_as_uint(r.tr.inv.y)); W(8, __float_as_uint(r.tr.inv.z));
-    W(9, __float_as_uint(r.h.t)); W(10, (uint32_t)r.h.slot); W(11, __float_as_uint(r.h.u)); W(12, __float_as_uint(r.h.v));
-    W(13, r.c.ref); W(14, __float_as_uint(r.c.t0)); W(15, __float_as_uint(r.c.t1));
-    W(16, r.lf.slot); W(17, r.lf.left); W(18, __float_as_uint(r.lf.tmax)); W(19, __float_as_uint(r.lf.tl));
-    W(20, __float_as_uint(r.lf.lu)); W(21, __float_as_uint(r.lf.lv)); W(22, (uint32_t)r.lf.sl);
-    W(23, r.mode | (r.tr.fin ? 4u : 0u) | (r.sid << 3) | ((uint32_t)r.sp << 10) | ((uint32_t)r.lo << 17));
-    W(24, r.idx); W(25, r.it);
-}
-__device__ __forceinline__ void ls_load(const uint32_t* pool, uint32_t q, LsRay& r) {
-    const uint32_t* P = pool + q;
-    auto R = [&](int f) { return P[f * ls::POOL]; };
-    r.tr.r.o = mk(__uint_as_float(R(0)), __uint_as_float(R(1)), __uint_as_float(R(2)));
-    r.tr.r.d = mk(__uint_as_float(R(3)), __uint_as_float(R(4)), __uint_as_float(R(5)));
-    r.tr.inv = mk(__uint_as_float(R(6)), __uint_as_float(R(7)), __uint_as_float(R(8)));
-    r.h.t = __uint_as_float(R(9)); r.h.slot = (int32_t)R(10); r.h.u = __uint_as_float(R(11)); r.h.v = __uint_as_float(R(12));
-    r.c.ref = R(13); r.c.t0 = __uint_as_float(R(14)); r.c.t1 = __uint_as_float(R(15)); r.c.valid = true;
-    r.lf.slot = R(16); r.lf.left = R(17); r.lf.tmax = __uint_as_float(R(18)); r.lf.tl = __uint_as_float(R(19));
-    r.lf.lu = __uint_as_float(R(20)); r.lf.lv = __uint_as_float(R(21)); r.lf.sl = (int32_t)R(22);
-    const uint32_t pk = R(23);
-    r.mode = pk & 3u;
-    r.tr.fin = (pk & 4u) != 0u;
-    r.sid = (pk >> 3) & 127u;
-    r.sp = (int)((pk >> 10) & 127u);
-    r.lo = (int)((pk >> 17) & 127u);
-    r.idx = R(24);
-    r.it = R(25);
-}
-
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-template <bool STATS>
-__global__ __launch_bounds__(TRAV_BLOCK, ls::WAVES) void k_extend_ls(DevScene S, Wave Wv, int cur, SpillArea spill) {
-    static_assert(TRAV_BLOCK == 64, "one wave per block");
-    extern __shared__ uint32_t lds[];
-    const uint32_t lane = lane_id();
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    uint32_t* pool = lds + ls::OFF_POOL;
-    uint32_t* plist = lds + ls::OFF_LIST;  // [0] parked node-kind, [1] parked leaf-kind, [2] free pool slots
-    uint32_t* fsid = lds + ls::OFF_SID;
-    if (lane < (uint32_t)ls::POOL) plist[2 * ls::POOL + lane] = lane;
-    for (uint32_t k = lane; k < (uint32_t)ls::SLOTS; k += 64) fsid[k] = k;
-    uint32_t nP0 = 0, nP1 = 0, nF = ls::POOL, nFS = ls::SLOTS;  // wave-uniform list counts
-    const uint32_t nf = Wv.cnt->nq[cur], nb = Wv.cnt->nqb[cur];
-    SidStack<ls::RING, ls::SLOTS, STATS> stk;
-    stk.init(lds, spill.base, spill.stride);
-    TravStats st{0, 0, 0};
-    LsRay r;
-    r.mode = M_IDLE;
-    r.it = 0;
-    r.idx = 0;
-    r.sid = 0;
-    r.c = Cur{0u, 0.0f, 0.0f, false};
-    r.lf = LeafCur{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
-    bool exhausted = false;
-    uint32_t W = 0u;  // kind this wave runs: 0 interior (M_NODE / M_POP), 1 candidate tests (M_LEAF)
-    unsigned long long wit = 0, wbusy = 0;
-    Claimer cl;
-    cl.init(Wv.cnt->fetch_ext, nf, nb, Wv.cap);
-    auto finish = [&]() {
-        Wv.ht[r.idx] = r.h.t;
-        Wv.hslot[r.idx] = r.h.slot;
-        Wv.hu[r.idx] = r.h.u;
-        Wv.hv[r.idx] = r.h.v;
-        Wv.heavy[r.idx] = r.it > Wv.heavy_T ? 1 : 0;
-    };
-    for (;;) {
-        // A. new rays from the queue for idle lanes (one claim per >= REFILL idle lanes)
-        bool done_now = false;
-        const unsigned long long idle = __ballot(r.mode == M_IDLE);
-        if (!exhausted && __popcll(idle) >= REFILL) {
-            uint32_t my;
-            const bool got = cl.claim(idle, my, exhausted);
-            const unsigned long long gm = __ballot(got && r.mode == M_IDLE);
-            if (got && r.mode == M_IDLE) {
-                r.sid = fsid[nFS - 1u - (uint32_t)__popcll(gm & lt)];
-                r.idx = cl.phys(my);
-                r.it = 0;
-                Ray ray;
-                ray.o = mk(Wv.qo[cur][0][r.idx], Wv.qo[cur][1][r.idx], Wv.qo[cur][2][r.idx]);
-                ray.d = mk(Wv.qd[cur][0][r.idx], Wv.qd[cur][1][r.idx], Wv.qd[cur][2][r.idx]);
-                trav_setup(r.tr, ray);
-                r.h.t = FLT_MAX_;
-                r.h.slot = -1;
-                r.h.u = r.h.v = 0.0f;
-                r.lf.left = 0;
-                stk.sid = r.sid;
-                const bool has = (STATS || !ray_has_nan(ray)) && trav2_begin<STATS>(S, r.tr, r.h.t, stk, r.mode, r.c, r.lf, st);
-                r.sp = stk.sp;
-                r.lo = stk.lo;
-                if (!has) {  // missed the root box, or a NaN ray (no hit)
-                    r.mode = M_IDLE;
-                    finish();
-                    done_now = true;
-                }
-            }
-            nFS -= uni((uint32_t)__popcll(gm));
-            // release the ray slots of rays that ended at their root test (before C2 reuses the lane)
-            const unsigned long long fm = __ballot(done_now);
-            if (done_now) fsid[nFS + (uint32_t)__popcll(fm & lt)] = r.sid;
-            nFS += uni((uint32_t)__popcll(fm));
-            done_now = false;
-        }
-        // B. the kind to run: keep it while KEEP rays of it are at hand, else switch to the larger
-        const unsigned long long act = __ballot(r.mode != M_IDLE);
-        const unsigned long long lfm = __ballot(r.mode == M_LEAF);
-        const uint32_t cL = (uint32_t)__popcll(lfm) + nP1, cN = (uint32_t)__popcll(act & ~lfm) + nP0;
-        if (cL + cN == 0u) {
-            if (exhausted) break;
-            continue;
-        }
-        {
-            const uint32_t cW = W ? cL : cN, cO = W ? cN : cL;
-            if (cW < ls::KEEP && cO > cW) W ^= 1u;
-        }
-        // C1. lanes holding the other kind swap with parked rays of this kind, or park in a free slot
-        const uint32_t nW = W ? nP1 : nP0, nO = W ? nP0 : nP1;
-        const bool off = r.mode != M_IDLE && ((r.mode == M_LEAF) != (W == 1u));
-        const unsigned long long om = __ballot(off);
-        const uint32_t nOff = (uint32_t)__popcll(om);
-        const uint32_t m1 = nOff < nW ? nOff : nW;
-        const uint32_t m2 = (nOff - m1) < nF ? (nOff - m1) : nF;
-        if (off) {
-            const uint32_t p = (uint32_t)__popcll(om & lt);
-            if (p < m1 + m2) {
-                uint32_t q;
-                if (p < m1) q = plist[W * ls::POOL + nW - 1u - p];
-                else q = plist[2 * ls::POOL + nF - 1u - (p - m1)];
-                r.sp = stk.sp;
-                r.lo = stk.lo;
-                r.sid = stk.sid;
-                if (p < m1) {  // exchange
-                    LsRay in;
-                    ls_load(pool, q, in);
-                    ls_store(pool, q, r);
-                    r = in;
-                } else {       // park
-                    ls_store(pool, q, r);
-                    r.mode = M_IDLE;
-                }
-                plist[(W ^ 1u) * ls::POOL + nO + p] = q;
-                stk.sid = r.sid;
-                stk.sp = r.sp;
-                stk.lo = r.lo;
-            }
-        }
-        uint32_t nWp = nW - m1, nOp = nO + m1 + m2, nFp = nF - m2;
-        // C2. idle lanes take parked rays of this kind
-        const unsigned long long im = __ballot(r.mode == M_IDLE);
-        const uint32_t nIdle = (uint32_t)__popcll(im);
-        const uint32_t m3 = nIdle < nWp ? nIdle : nWp;
-        if (r.mode == M_IDLE) {
-            const uint32_t p = (uint32_t)__popcll(im & lt);
-            if (p < m3) {
-                const uint32_t q = plist[W * ls::POOL + nWp - 1u - p];
-                ls_load(pool, q, r);
-                plist[2 * ls::POOL + nFp + p] = q;
-                stk.sid = r.sid;
-                stk.sp = r.sp;
-                stk.lo = r.lo;
-            }
-        }
-        nWp -= m3;
-        nFp += m3;
-        if (W) { nP1 = uni(nWp); nP0 = uni(nOp); } else { nP0 = uni(nWp); nP1 = uni(nOp); }
-        nF = uni(nFp);
-        // D. one step of this kind on every lane that holds it
-        const bool run = r.mode != M_IDLE && ((r.mode == M_LEAF) == (W == 1u));
-        if (STATS) {
-            ++wit;
-            wbusy += (uint32_t)__popcll(__ballot(run && (r.mode == M_NODE || r.mode == M_LEAF)));
-        }
-        if (run) {
-            bool occ_unused;
-            ++r.it;
-            const bool fin = W ? step_leaf<false, STATS>(S, r.tr, r.h, 0.0f, stk, r.mode, r.c, r.lf, st, occ_unused)
-                               : step_node<false, STATS>(S, r.tr, r.h, 0.0f, stk, r.mode, r.c, r.lf, st, occ_unused);
-            if (fin) {
-                finish();
-                done_now = true;
-            }
-        }
-        // E. release the ray slots of the rays that ended
-        const unsigned long long fm = __ballot(done_now);
-        if (done_now) fsid[nFS + (uint32_t)__popcll(fm & lt)] = stk.sid;
-        nFS += uni((uint32_t)__popcll(fm));
-    }
-    if (STATS) {
-        // flush_stats wants a stack with `spills`
-        flush_stats(st, stk, wit, wbusy, &Wv.cnt->node_visits, &Wv.cnt->prim_tests, &Wv.cnt->pruned, &Wv.cnt->iters,
-                    &Wv.cnt->lanes_busy, &Wv.cnt->spills);
-    }
-}
-
 // ---- light-path variant (khp_bdpt_params, ABI 7; lightpath.h) ----------------------------
 // The surface at a closest hit: normal, hair frame and material (k_shade's
 // calcNormal / calcTcoord code; Cylinder.cpp:230-260, Triangle.cpp:244-254).
@@ -1709,7 +1476,7 @@ struct khp_ctx {
     std::vector<hipEvent_t> ev_pool;
     size_t ev_next = 0;
     std::vector<TimedLaunch> launches;
-    int grid_ext = 0, grid_sh = 0, grid_shade = 0, grid_ls = 0;
+    int grid_ext = 0, grid_sh = 0, grid_shade = 0;
     khp_stats st{};
     // rccl gather: pixel lists cached per (W, H, tile, nranks, rank, root)
     uint32_t gather_key[6] = {0, 0, 0, 0, 0, 0};
@@ -1761,7 +1528,6 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->trace_kernels = 0;
     out->shade_order = 0;       // hit sorting measured, off
     out->serial_stages = 0;
-    out->lane_sort = 0;
 }
 
 extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {
@@ -1780,7 +1546,6 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     if (prm->trace_kernels > 2) return fail(KHP_EINVAL, "trace_kernels must be 0, 1 or 2");
     if (prm->shade_order > 1) return fail(KHP_EINVAL, "shade_order must be 0 or 1");
     if (prm->serial_stages > 1) return fail(KHP_EINVAL, "serial_stages must be 0 or 1");
-    if (prm->lane_sort > 1) return fail(KHP_EINVAL, "lane_sort must be 0 or 1");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
     if (dr != KHP_OK) return dr;
@@ -2143,12 +1908,6 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, TRAV_BLOCK, EXT_LDS_BYTES));
     c->grid_ext = std::max(1, nb) * c->n_cu;
     nb = 0;
-    if (c->flags & KHP_CTX_STATS)
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend_ls<true>, TRAV_BLOCK, ls::LDS_BYTES));
-    else
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend_ls<false>, TRAV_BLOCK, ls::LDS_BYTES));
-    c->grid_ls = std::max(1, nb) * c->n_cu;
-    nb = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, TRAV_BLOCK, LDS_BYTES));
     c->grid_sh = std::max(1, nb) * c->n_cu;
     nb = 0;
@@ -2187,8 +1946,7 @@ static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap, size_t sh_per_
     HIPCHK(w.cnt.ensure(sizeof(Counters)));
     // traversal-stack spill columns: one per resident lane, STACK_MAX entries deep
     // separate spill columns: k_extend and k_shadow may run at the same time
-    HIPCHK(w.spill.ensure(std::max((size_t)c->grid_ext * TRAV_BLOCK, (size_t)c->grid_ls * ls::SLOTS) * STACK_MAX *
-                          sizeof(int4)));
+    HIPCHK(w.spill.ensure((size_t)c->grid_ext * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
     HIPCHK(w.spill_sh.ensure((size_t)c->grid_sh * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
     if (!w.sA) {
         HIPCHK(hipStreamCreateWithFlags(&w.sA, hipStreamNonBlocking));
@@ -2433,22 +2191,6 @@ extern "C" khp_status khp_sync(khp_ctx* c) {
 // Enqueue one frame, or a fused batch of asynchronous frames (ops: their
 // render operations, which differ only in first_sample, and the framebuffer
 // gathers between them, in call order; p = the first render's parameters).
-// The extension kernel of a launch: k_extend, or k_extend_ls with khp_ctx_params.lane_sort
-// (its own grid, and the spill area indexed by ray slot instead of lane).
-static void launch_extend(khp_ctx* c, bool stats, int G, hipStream_t st, const Wave& Wb, int cur, int4* spill) {
-    if (c->prm.lane_sort) {
-        const int grid = std::max(1, c->grid_ls / G);
-        const SpillArea sp{spill, (uint32_t)c->grid_ls * (uint32_t)ls::SLOTS};
-        if (stats) hipLaunchKernelGGL(k_extend_ls<true>, dim3(grid), dim3(TRAV_BLOCK), ls::LDS_BYTES, st, c->S, Wb, cur, sp);
-        else hipLaunchKernelGGL(k_extend_ls<false>, dim3(grid), dim3(TRAV_BLOCK), ls::LDS_BYTES, st, c->S, Wb, cur, sp);
-        return;
-    }
-    const int grid = std::max(1, c->grid_ext / G);
-    const SpillArea sp{spill, (uint32_t)c->grid_ext * TRAV_BLOCK};
-    if (stats) hipLaunchKernelGGL(k_extend<true>, dim3(grid), dim3(TRAV_BLOCK), EXT_LDS_BYTES, st, c->S, Wb, cur, sp);
-    else hipLaunchKernelGGL(k_extend<false>, dim3(grid), dim3(TRAV_BLOCK), EXT_LDS_BYTES, st, c->S, Wb, cur, sp);
-}
-
 static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root);
 static khp_status snapshot_now(khp_ctx* c, uint64_t id);
 // A non-render operation of a fused batch, in call order.
@@ -2513,7 +2255,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     f.snaps.clear();
     f.nf = nf;
     const int G = async ? F : 1;
-    const int grid_sh = std::max(1, c->grid_sh / G);
+    const int grid_ext = std::max(1, c->grid_ext / G), grid_sh = std::max(1, c->grid_sh / G);
     // Chunks: the owned pixels x samples (x fused frames) are cut into chunks
     // of at most chunk_paths() paths, pixel-major; a fused chunk carries all
     // samples of all frames of its pixels.
@@ -2619,6 +2361,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     Wv.bd = BdptDev{bdm ? 1u : 0u, c->bd.light_paths, (uint32_t)c->S.n_lights, c->bd.vertices, c->bd.bias,
                     c->bd.bounce_bias, c->bd.min_pdf, c->bd.image_plane,
                     bdm ? w.lvb.as<float4>() : nullptr};
+    SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
     SpillArea sp_sh{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
     for (uint32_t p0 = 0; p0 < P_all; p0 += P_chunk) {
         const uint32_t P = std::min(P_chunk, P_all - p0);
@@ -2681,7 +2424,10 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 }
                 hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
                 timed(c, f, 0, true, sA);
-                launch_extend(c, stats, G, sA, Wb, cur, w.spill.as<int4>());
+                if (stats)
+                    hipLaunchKernelGGL(k_extend<true>, dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                else
+                    hipLaunchKernelGGL(k_extend<false>, dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
                 timed(c, f, 0, false, sA);
                 if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
                 timed(c, f, 1, true, sA);
@@ -3327,7 +3073,9 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(hit_out, Wv.vis, n, hipMemcpyDeviceToHost, c->stream));
     } else {
-        launch_extend(c, !prod, 1, c->stream, Wv, 0, w.spill.as<int4>());
+        SpillArea sp{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
+        if (prod) hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, c->stream, c->S, Wv, 0, sp);
+        else hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, c->stream, c->S, Wv, 0, sp);
         (void)hipEventRecord(e1, c->stream);
         HIPCHK(t.ensure(4 * (size_t)n));
         HIPCHK(ob.ensure(4 * (size_t)n));

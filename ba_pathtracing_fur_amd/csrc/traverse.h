@@ -549,162 +549,6 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
     return false;
 }
 
-// ---- mode-sorted lanes (khp_ctx_params.lane_sort = 1, round 3) ----------------------------
-// iter2 split by the kind of work, for waves whose lanes all hold one kind:
-// step_node runs an interior entry (M_NODE: fetch the node record, both child
-// boxes, push and take) or a pending pop (M_POP); step_leaf tests the next
-// candidate of an opened leaf (M_LEAF).  The arithmetic, the visit order and
-// the counters are iter2's, branch for branch -- only the other kind's branch
-// is absent, so a homogeneous wave issues one of them instead of both.
-
-// The pop that follows a finished entry (iter2's need_pop tail) and the take.
-template <bool ANY, bool STATS, class Stack>
-__device__ __forceinline__ bool pop_and_take(const DevScene& S, float tlimit, Stack& stk, uint32_t& mode, Cur& c,
-                                             LeafCur& lf, TravStats& st, bool& occluded) {
-    if (stk.empty()) {
-        mode = M_IDLE;
-        occluded = false;
-        return true;
-    }
-    uint32_t eref;
-    float et0, et1;
-    stk.pop(eref, et0, et1);
-    if (et1 < 0.0f || et0 > tlimit) {
-        if (STATS) st.pruned++;
-        mode = M_POP;
-    } else {
-        take_entry<STATS>(S, eref, et0, et1, mode, c, lf, st);
-    }
-    return false;
-}
-
-template <bool ANY, bool STATS, class Stack>
-__device__ __forceinline__ bool step_node(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
-                                          uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
-    const bool fetch = mode == M_NODE;
-    bool have = false, push = false;
-    uint32_t eref = 0u, pref = 0u;
-    float et0 = 0.0f, et1 = 0.0f, pt0 = 0.0f, pt1 = 0.0f;
-    if (fetch) {
-        const float4* p = reinterpret_cast<const float4*>(S.nodes + c.ref);
-        float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-        pin(q0); pin(q1); pin(q2); pin(q3);
-        if (STATS) st.nodes++;
-        const float tlimit = ANY ? tmax_any : h.t;
-        float l0, l1, r0, r1;
-        bool lh, rh;
-        if (__ballot(!tr.fin) == 0ull) {  // wave-uniform
-            lh = slab_fast(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, tr, l0, l1);
-            rh = slab_fast(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, tr, r0, r1);
-        } else {
-            lh = slab_sel(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, tr, l0, l1);
-            rh = slab_sel(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, tr, r0, r1);
-        }
-        lh = lh && !(l1 < 0.0f || l0 > tlimit);
-        rh = rh && !(r1 < 0.0f || r0 > tlimit);
-        const uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
-        const bool nearl = lh && (!rh || l0 < r0);  // KIRK: left first iff l0 < r0 (ties: right)
-        have = lh || rh;
-        push = lh && rh;
-        eref = nearl ? lref : rref;
-        et0 = nearl ? l0 : r0;
-        et1 = nearl ? l1 : r1;
-        pref = nearl ? rref : lref;
-        pt0 = nearl ? r0 : l0;
-        pt1 = nearl ? r1 : l1;
-    }
-    if (push) stk.push(pref, pt0, pt1);
-    if (have) {
-        take_entry<STATS>(S, eref, et0, et1, mode, c, lf, st);
-        return false;
-    }
-    return pop_and_take<ANY, STATS>(S, ANY ? tmax_any : h.t, stk, mode, c, lf, st, occluded);
-}
-
-template <bool ANY, bool STATS, class Stack>
-__device__ __forceinline__ bool step_leaf(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
-                                          uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
-    const float4* p = S.prims + 4 * (size_t)lf.slot;
-    float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-    pin(q0); pin(q1); pin(q2); pin(q3);
-    if (STATS) st.prims++;
-    if (ANY) {
-        if (any_candidate(q0, q1, q2, q3, tr.r, tmax_any)) {
-            occluded = true;
-            return true;
-        }
-    } else {
-        leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);
-    }
-    ++lf.slot;
-    --lf.left;
-    if (lf.left != 0u) return false;
-    if (!ANY && lf.sl >= 0 && lf.tl < h.t) {
-        h.t = lf.tl;
-        h.slot = lf.sl;
-        h.u = lf.lu;
-        h.v = lf.lv;
-    }
-    return pop_and_take<ANY, STATS>(S, ANY ? tmax_any : h.t, stk, mode, c, lf, st, occluded);
-}
-
-// A stack ring per RAY SLOT (not per lane): rays move between the lanes of a
-// wave and its pool of parked rays, their stacks stay where they are.  LDS
-// image [3][R][slots] (ref, tmin bits, tmax bits); the spill column of ray
-// slot `sid` of this block is spill + e * stride + blockIdx.x * slots + sid.
-template <int R, int SLOTS, bool COUNT>
-struct SidStack {
-    static_assert(R >= 2 && R <= 16, "ring size");
-    uint32_t* lds;
-    int4* spill;
-    uint32_t stride;
-    uint32_t sid;
-    int sp, lo;
-    uint32_t spills;
-    __device__ __forceinline__ void init(uint32_t* lds_base, int4* spill_base, uint32_t stride_) {
-        lds = lds_base;
-        spill = spill_base;
-        stride = stride_;
-        sid = 0;
-        sp = lo = 0;
-        spills = 0;
-    }
-    __device__ __forceinline__ void clear() { sp = lo = 0; }
-    __device__ __forceinline__ bool empty() const { return sp == 0; }
-    __device__ __forceinline__ uint32_t slot(int e) const { return (uint32_t)((uint32_t)e % (uint32_t)R) * SLOTS + sid; }
-    __device__ __forceinline__ int4* gcell(int e) const {
-        return spill + (size_t)e * stride + (size_t)blockIdx.x * SLOTS + sid;
-    }
-    __device__ __forceinline__ void push(uint32_t r, float a, float b) {
-        if (sp - lo == R) {
-            const uint32_t k = slot(lo);
-            *gcell(lo) = make_int4((int)lds[k], (int)lds[k + R * SLOTS], (int)lds[k + 2 * R * SLOTS], 0);
-            ++lo;
-            if (COUNT) ++spills;
-        }
-        const uint32_t k = slot(sp);
-        lds[k] = r;
-        lds[k + R * SLOTS] = bits_from_f(a);
-        lds[k + 2 * R * SLOTS] = bits_from_f(b);
-        ++sp;
-    }
-    __device__ __forceinline__ void pop(uint32_t& r, float& a, float& b) {
-        --sp;
-        const uint32_t k = slot(sp);
-        r = lds[k];
-        a = f_from_bits(lds[k + R * SLOTS]);
-        b = f_from_bits(lds[k + 2 * R * SLOTS]);
-        asm volatile("" : "+v"(r), "+v"(a), "+v"(b));
-        if (sp < lo) {
-            const int4 e = *gcell(sp);
-            r = (uint32_t)e.x;
-            a = f_from_bits((uint32_t)e.y);
-            b = f_from_bits((uint32_t)e.z);
-            lo = sp;
-        }
-    }
-};
-
 // Whole-ray forms (batch query kernels).
 template <bool STATS, class Stack>
 __device__ __forceinline__ void trace_closest(const DevScene& S, const Ray& r, Hit& h, Stack& stk, TravStats& st) {

@@ -92,7 +92,6 @@ def parse():
     ap.add_argument("--iso-steps", type=int, default=8,
                     help="fused passes re-run with serial_stages=1 for the isolated per-kernel rooflines (0: skip)")
     ap.add_argument("--shade-order", type=int, default=None, help="khp_ctx_params.shade_order (1: hits sorted by shading class)")
-    ap.add_argument("--lane-sort", type=int, default=None, help="khp_ctx_params.lane_sort (1: mode-sorted waves)")
     ap.add_argument("--heavy-iters", type=int, default=None,
                     help="khp_ctx_params.heavy_iters (longest-first queue threshold, traversal iterations)")
     ap.add_argument("--bdpt", default=None, metavar="PATHS,VERTICES",
@@ -292,7 +291,7 @@ def main():
     frame = ShardedFrame(ctx, rank, world, dist, tile=args.tile)
     knobs = {k: v for k, v in (("fuse_frames", args.fuse), ("chunk_paths", args.chunk_paths),
                                ("frames_in_flight", args.frames_in_flight), ("shade_order", args.shade_order),
-                               ("heavy_iters", args.heavy_iters), ("lane_sort", args.lane_sort))
+                               ("heavy_iters", args.heavy_iters))
              if v is not None}
     if knobs:
         ctx.set_params(**knobs)

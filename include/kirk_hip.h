@@ -290,10 +290,6 @@ typedef struct {
                                     kernels of a frame overlap and each kernel's timing is its own
                                     (bench.py's isolated per-kernel rooflines); 0 (default) = two
                                     streams, shadow stage b beside extend b+1                         */
-    uint32_t lane_sort;          /* ABI 8: 1 = the closest-hit traversal runs mode-sorted waves: each wave
-                                    iteration runs interior steps OR candidate tests on lanes that all
-                                    hold that kind, rays of the other kind wait in an LDS pool (DESIGN.md
-                                    §4); 0 (default) = k_extend, both kinds in every iteration            */
 } khp_ctx_params;
 
 /* ---- context --------------------------------------------------------------- */

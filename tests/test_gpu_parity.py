@@ -159,7 +159,7 @@ def test_chunked_and_instrumented_frames(hip_ctx, chunk):
 
 def test_params_are_validated(hip_ctx):
     for bad in (dict(fuse_frames=0), dict(fuse_frames=33), dict(frames_in_flight=4), dict(chunk_paths=100),
-                dict(trace_kernels=3), dict(shade_order=2), dict(serial_stages=2), dict(lane_sort=2)):
+                dict(trace_kernels=3), dict(shade_order=2), dict(serial_stages=2)):
         with pytest.raises(N.KhpError) as e:
             hip_ctx.set_params(**bad)
         assert e.value.status == N.KHP_EINVAL
@@ -532,66 +532,5 @@ def test_production_traversal_kernels_ray_by_ray(hip_ctx, mode, name, kw):
     assert np.array_equal(t.view(np.uint32), t0.view(np.uint32))
     assert np.array_equal(uv.view(np.uint32), uv0.view(np.uint32))
     assert np.array_equal(a, any0)
-    if mode == "1":
-        assert (st["node_visits"], st["prim_tests"]) == (nodes, prims)
-
-
-# ---- khp_ctx_params.lane_sort (mode-sorted waves, k_extend_ls) --------------------------------
-@pytest.mark.parametrize("name,kw,w,h,spp,depth", [CASES[1], CASES[3], CASES[4], CASES[5], CASES[8]],
-                         ids=["config2", "config3", "config5", "zoo", "textured"])
-def test_lane_sort_frames(hip_ctx, name, kw, w, h, spp, depth):
-    """lane_sort 1 moves rays between lanes and an LDS pool so each wave runs one
-    kind of step; every ray keeps iter2's steps in iter2's order, so synchronous,
-    instrumented, chunked and fused asynchronous frames are the oracle's bit for
-    bit, and the instrumented counts are k_extend's."""
-    sd = S.build_config(name, width=w, height=h, **kw)
-    hip_ctx.set_scene(sd)
-    hip_ctx.build_accel()
-    want = oracle_ffi.Oracle(sd).render(w, h, spp, depth, threads=16)
-    hip_ctx.render(w, h, spp, depth, stats=True)
-    ref_st = hip_ctx.stats()
-    old = hip_ctx.set_params(lane_sort=1)
-    try:
-        assert_parity(hip_ctx.render(w, h, spp, depth), want, exact=True)
-        assert_parity(hip_ctx.render(w, h, spp, depth, stats=True), want, exact=True)
-        st = hip_ctx.stats()
-        for k in ("node_visits", "prim_tests", "extend_rays", "extend_pruned_pops"):
-            assert st[k] == ref_st[k], k
-        hip_ctx.set_params(chunk_paths=4096)
-        assert_parity(hip_ctx.render(w, h, spp, depth), want, exact=True)
-        hip_ctx.set_params(chunk_paths=0)
-        for k in range(spp):
-            hip_ctx.render(w, h, 1, depth, first_sample=k, async_=True)
-        hip_ctx.sync()
-        assert_parity(hip_ctx.read_framebuffer(w, h), want, exact=True)
-    finally:
-        hip_ctx.set_params(**old)
-
-
-@pytest.mark.parametrize("mode", ["1", "2"])
-def test_lane_sort_queries_ray_by_ray(hip_ctx, mode):
-    """The batch queries through k_extend_ls (trace_kernels 1: KIRK's visit counts;
-    2: the production build), NaN rays included."""
-    sd = S.build_config("config5", width=32, height=32, n_strands=2000, torus_grid=30)
-    hip_ctx.set_scene(sd)
-    hip_ctx.build_accel()
-    o = oracle_ffi.Oracle(sd)
-    rng = np.random.default_rng(23)
-    n = 100000
-    orig = rng.uniform(-1.5, 1.5, (n, 3)).astype(np.float32) + np.float32([0, 1, 0])
-    d = rng.normal(size=(n, 3)).astype(np.float32)
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    d[:40] = np.nan
-    orig[80:100, 2] = np.nan
-    t0, obj0, uv0, nodes, prims = o.trace_closest(orig, d)
-    old = hip_ctx.set_params(trace_kernels=int(mode), lane_sort=1)
-    try:
-        t, obj, uv = hip_ctx.trace_closest(orig, d)
-        st = hip_ctx.stats()
-    finally:
-        hip_ctx.set_params(**old)
-    assert np.array_equal(obj, obj0)
-    assert np.array_equal(t.view(np.uint32), t0.view(np.uint32))
-    assert np.array_equal(uv.view(np.uint32), uv0.view(np.uint32))
     if mode == "1":
         assert (st["node_visits"], st["prim_tests"]) == (nodes, prims)
