@@ -85,7 +85,8 @@ struct Wave {
     uint32_t seed;
     uint32_t sample0;     // global sample index of chunk sample 0
     uint32_t n_samples;   // samples in this chunk (per frame)
-    uint32_t n_frames;    // fused frames in this chunk (paths: frame-major blocks of P x n_samples)
+    uint32_t n_frames;    // fused frames in this chunk
+    uint32_t pix_major;   // path numbering (khp_ctx_params.path_order): 0 frame-major, 1 pixel-major
     uint32_t fsample0[KHP_MAX_FUSE];  // per fused frame: global sample index of chunk sample 0
     uint32_t depth;
     uint8_t* heavy;       // per queue slot: the ray's traversal took more than heavy_T iterations
@@ -97,6 +98,33 @@ struct Wave {
     uint32_t* hcls;       // [0,16): entries per class, [16,32): scatter cursors per class
     BdptDev bd;           // light-path variant (ABI 7); bd.on = 0: next-event estimate
 };
+
+// Path numbering of a chunk.  Frame-major: path = (frame * P + pixel) * n_samples
+// + sample.  Pixel-major: path = (pixel * n_frames + frame) * n_samples + sample,
+// so every fused frame's samples of one pixel are adjacent.  Paths are
+// independent and each pixel's samples are summed in (frame, sample) order either
+// way, so the numbering changes no result.
+__device__ __forceinline__ void path_coords(const Wave& Wv, uint32_t pid, uint32_t& fr, uint32_t& p_local,
+                                            uint32_t& s_local) {
+    if (Wv.pix_major) {
+        const uint32_t per_pix = Wv.n_frames * Wv.n_samples;
+        p_local = pid / per_pix;
+        const uint32_t r = pid - p_local * per_pix;
+        fr = r / Wv.n_samples;
+        s_local = r - fr * Wv.n_samples;
+    } else {
+        const uint32_t per_frame = Wv.P * Wv.n_samples;
+        fr = pid / per_frame;
+        const uint32_t pf = pid - fr * per_frame;
+        p_local = pf / Wv.n_samples;
+        s_local = pf - p_local * Wv.n_samples;
+    }
+}
+
+__device__ __forceinline__ size_t path_index(const Wave& Wv, uint32_t fr, uint32_t p_local, uint32_t s_local) {
+    return Wv.pix_major ? ((size_t)p_local * Wv.n_frames + fr) * Wv.n_samples + s_local
+                        : ((size_t)fr * Wv.P + p_local) * Wv.n_samples + s_local;
+}
 
 
 
@@ -153,18 +181,17 @@ __device__ __forceinline__ T wave_sum(T v) {
 // ---- generate: camera rays (PathTracer::generatePrimaryRays, CPU_PathTracer.cpp:118-127;
 //      Camera::getRayFromPixel, Camera.cpp:59-66) -------------------------------------------
 __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
-    const uint32_t per_frame = Wv.P * Wv.n_samples;
-    uint32_t n = per_frame * Wv.n_frames;
+    uint32_t n = Wv.P * Wv.n_samples * Wv.n_frames;
     uint32_t pid = blockIdx.x * blockDim.x + threadIdx.x;
     if (pid == 0) {
         Wv.cnt->nq[0] = n;   // primary rays: all in the front part
         Wv.cnt->nqb[0] = 0;
     }
     if (pid >= n) return;
-    // pixel-major: the samples of one pixel are adjacent paths, so a wave traces
-    // 64/n_samples neighbouring pixels x all their samples (cache reuse)
-    const uint32_t fr = pid / per_frame, pf = pid - fr * per_frame;
-    uint32_t p_local = pf / Wv.n_samples, s_local = pf - p_local * Wv.n_samples;
+    // the samples of one pixel are adjacent paths (path_coords), so a wave traces
+    // a few neighbouring pixels x all their samples (cache reuse)
+    uint32_t fr, p_local, s_local;
+    path_coords(Wv, pid, fr, p_local, s_local);
     uint32_t pixel = Wv.pix[Wv.p_off + p_local];
     uint32_t x = pixel % Wv.W, y = pixel / Wv.W;
     uint32_t key = path_key(Wv.seed, pixel, Wv.fsample0[fr] + s_local);
@@ -505,11 +532,10 @@ __global__ __launch_bounds__(64) void k_light_paths(DevScene S, Wave Wv) {
 // the shadow buffers of parity 1, which bounce 0 does not use.
 __global__ __launch_bounds__(256) void k_img_connect(DevScene S, Wave Wv) {
     const BdptDev& bd = Wv.bd;
-    const uint32_t per_frame = Wv.P * Wv.n_samples;
     const uint32_t pid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pid >= per_frame * Wv.n_frames) return;
-    const uint32_t fr = pid / per_frame, pf = pid - fr * per_frame;
-    const uint32_t p_local = pf / Wv.n_samples, s_local = pf - p_local * Wv.n_samples;
+    if (pid >= Wv.P * Wv.n_samples * Wv.n_frames) return;
+    uint32_t fr, p_local, s_local;
+    path_coords(Wv, pid, fr, p_local, s_local);
     const uint32_t pixel = Wv.pix[Wv.p_off + p_local];
     const uint32_t x = pixel % Wv.W, y = pixel / Wv.W;
     const uint32_t key = path_key(Wv.seed, pixel, Wv.fsample0[fr] + s_local);
@@ -882,8 +908,9 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                         li = (uint32_t)((float)bd.L * draw_u01(key, dim_of(bounce, P_LIGHT_SEL)));
                         sp = sp < bd.Ns ? sp : bd.Ns - 1u;
                         li = li < bd.L ? li : bd.L - 1u;
-                        const uint32_t per_frame = Wv.P * Wv.n_samples, fr = pid / per_frame;
-                        const uint32_t q = fr * Wv.n_samples + (pid - fr * per_frame) % Wv.n_samples;
+                        uint32_t fr, p_local, s_local;
+                        path_coords(Wv, pid, fr, p_local, s_local);
+                        const uint32_t q = fr * Wv.n_samples + s_local;
                         lv = bd.lv + 3 * ((((size_t)q * bd.Ns + sp) * bd.L + li) * bd.J);
                         for (uint32_t j = 0; j < bd.J; ++j) {
                             Ray sh;
@@ -1148,10 +1175,9 @@ __global__ __launch_bounds__(256) void k_accumulate(Wave Wv, float* fb, uint32_t
     uint32_t pixel = Wv.pix[Wv.p_off + p];
     float* o = fb + 3 * (size_t)pixel;
     float r = o[0], g = o[1], b = o[2];
-    const size_t base = (size_t)fr * Wv.P * Wv.n_samples;
+    const size_t base = path_index(Wv, fr, p, 0);
     for (uint32_t s = 0; s < Wv.n_samples; ++s) {
-        size_t pid = base + (size_t)p * Wv.n_samples + s;
-        const float4 ck = Wv.CK[pid];
+        const float4 ck = Wv.CK[base + s];
         float cr = ck.x, cg = ck.y, cb = ck.z;
         uint32_t k = Wv.fsample0[fr] + s;
         if (k == 0) {
@@ -1528,6 +1554,7 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->trace_kernels = 0;
     out->shade_order = 0;       // hit sorting measured, off
     out->serial_stages = 0;
+    out->path_order = 1;       // pixel-major fused chunks, +5-7%
 }
 
 extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {
@@ -1546,6 +1573,7 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     if (prm->trace_kernels > 2) return fail(KHP_EINVAL, "trace_kernels must be 0, 1 or 2");
     if (prm->shade_order > 1) return fail(KHP_EINVAL, "shade_order must be 0 or 1");
     if (prm->serial_stages > 1) return fail(KHP_EINVAL, "serial_stages must be 0 or 1");
+    if (prm->path_order > 1) return fail(KHP_EINVAL, "path_order must be 0 or 1");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
     if (dr != KHP_OK) return dr;
@@ -2358,6 +2386,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     Wv.H = p->height;
     Wv.seed = p->seed;
     Wv.depth = p->depth;
+    Wv.pix_major = c->prm.path_order;
     Wv.bd = BdptDev{bdm ? 1u : 0u, c->bd.light_paths, (uint32_t)c->S.n_lights, c->bd.vertices, c->bd.bias,
                     c->bd.bounce_bias, c->bd.min_pdf, c->bd.image_plane,
                     bdm ? w.lvb.as<float4>() : nullptr};

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 8
+#define KHP_ABI_VERSION 9
 
 typedef struct khp_ctx khp_ctx;
 
@@ -290,6 +290,10 @@ typedef struct {
                                     kernels of a frame overlap and each kernel's timing is its own
                                     (bench.py's isolated per-kernel rooflines); 0 (default) = two
                                     streams, shadow stage b beside extend b+1                         */
+    uint32_t path_order;         /* ABI 9: how a fused chunk numbers its paths.  0: frame-major (frame f's
+                                    pixels x samples form one block); 1 (default): pixel-major (all fused
+                                    frames' samples of one pixel are adjacent paths, so a wave traces one
+                                    pixel of 8 frames at 8 spp).  Measured in DESIGN.md §5a            */
 } khp_ctx_params;
 
 /* ---- context --------------------------------------------------------------- */

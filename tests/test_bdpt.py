@@ -143,8 +143,10 @@ def test_bdpt_frame_parity(hip_ctx, name, kw, w, h, spp, depth, ns, nv):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("prm", [dict(shade_order=1), dict(serial_stages=1), dict(frames_in_flight=2, fuse_frames=1),
-                                 dict(fuse_frames=3, chunk_paths=8192)],
-                         ids=["hit-sorting", "serial-stages", "2-in-flight", "fused-chunked"])
+                                 dict(fuse_frames=3, chunk_paths=8192), dict(fuse_frames=3, chunk_paths=8192, path_order=1),
+                                 dict(fuse_frames=4, path_order=1)],
+                         ids=["hit-sorting", "serial-stages", "2-in-flight", "fused-chunked", "fused-chunked-pixel-major",
+                              "fused-pixel-major"])
 def test_bdpt_with_schedules(hip_ctx, prm):
     """The variant under every scheduling parameter: frames stay the oracle's."""
     sd = S.build_config("zoo", width=48, height=36, n_strands=300)
