@@ -2299,7 +2299,17 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         // equal chunks (in whole 64-pixel blocks where that stays under the cap): 20 fused
         // 8-spp 1080p frames are 3 chunks of 691k pixels instead of 839k + 839k + 395k, so
         // no chunk's launches run a short, tail-dominated wavefront
-        const uint32_t n_ch = (P_all + P_chunk - 1) / std::max<uint32_t>(1, P_chunk);
+        uint32_t n_ch = (P_all + P_chunk - 1) / std::max<uint32_t>(1, P_chunk);
+        // automatic chunk size: one chunk fewer when the chunks then stay within 5/4
+        // of the cap (20 fused 8-spp 1080p frames: 2 chunks of 166M paths instead of
+        // 3 of 111M, +1.2% measured; 32 frames stay 4 chunks of 133M)
+        if (n_ch > 1 && c->prm.chunk_paths == 0) {
+            const uint64_t lo_px = (P_all + (n_ch - 1) - 1) / (n_ch - 1);
+            if (lo_px * p->spp * nf <= cap_paths + cap_paths / 4) {
+                --n_ch;
+                P_chunk = (uint32_t)lo_px;
+            }
+        }
         if (n_ch > 1) {
             const uint32_t even = (P_all + n_ch - 1) / n_ch, blk = (even + 63u) & ~63u;
             P_chunk = blk <= P_chunk ? blk : even;
@@ -2317,10 +2327,12 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     }
     // a partial batch (flushed by a sync) reserves room for a full one, so the
     // first full batch does not allocate
+    // (automatic chunks may reach 5/4 of the cap, see above)
     size_t want = (size_t)P_chunk * S_chunk * nf;
     if (nf > 1) {
         const uint32_t fuse = std::max<uint32_t>(1, std::min<uint32_t>(c->prm.fuse_frames, KHP_MAX_FUSE));
-        want = std::max(want, std::min<size_t>(cap_paths, (size_t)P_chunk * S_chunk * fuse));
+        const size_t most = cap_paths + (c->prm.chunk_paths == 0 ? cap_paths / 4 : 0);
+        want = std::max(want, std::min<size_t>(most, (size_t)P_all * S_chunk * fuse));
     }
     PathSet& w = c->ps[slot];
     s = ensure_wave(c, w, want, sh_per_path);

@@ -423,6 +423,31 @@ def test_fused_full_size_matches_passes():
         ctx.close()
 
 
+def test_driver_batch_chunks():
+    """The driver's bench command: 20 fused 8-spp passes at the metric size
+    (332M paths).  The automatic chunk size makes 2 chunks of 166M paths (within
+    5/4 of the 2^27 cap) instead of 3; an explicit chunk_paths is a hard cap
+    (2^27: 3 chunks, 2^26: 5).  All give the same framebuffer, bit for bit."""
+    ctx = HipContext(0)
+    try:
+        S.config3_device(ctx, 1920, 1080, n_strands=1_000_000)
+        ctx.build_accel()
+        got = {}
+        for cap in (0, 1 << 27, 1 << 26):
+            ctx.set_params(chunk_paths=cap)
+            for k in range(20):
+                ctx.render(1920, 1080, 8, 5, first_sample=8 * k, async_=True)
+            ctx.sync()
+            st = ctx.stats()
+            assert st["frames"] == 20
+            got[cap] = (st["extend_launches"], ctx.read_framebuffer(1920, 1080))
+        assert [got[c][0] for c in (0, 1 << 27, 1 << 26)] == [2 * 5, 3 * 5, 5 * 5]
+        for cap in (1 << 27, 1 << 26):
+            assert np.array_equal(got[cap][1].view(np.uint32), got[0][1].view(np.uint32)), cap
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("max_paths", ["14000", "4096"])
 def test_fused_frames_with_gathers_split(max_paths):
     """A fused batch with gathers that does not fit one chunk is split into
