@@ -2049,6 +2049,14 @@ static size_t chunk_paths(khp_ctx* c) {
     return cap;
 }
 
+// The most paths one fused chunk may hold: the cap, or with automatic chunking
+// 5/4 of it (enqueue_frames cuts a batch into one chunk fewer when the chunks
+// then stay within this; flush() groups gathered frames by the same limit).
+static size_t chunk_most(khp_ctx* c) {
+    const size_t cap = chunk_paths(c);
+    return cap + (c->prm.chunk_paths == 0 ? cap / 4 : 0);
+}
+
 static khp_status check_params(khp_ctx* c, const khp_render_params* p) {
     if (!c || !p) return fail(KHP_EINVAL, "null argument");
     if (!c->built) return fail(KHP_ENOTREADY, "khp_build_accel first");
@@ -2305,7 +2313,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         // 3 of 111M, +1.2% measured; 32 frames stay 4 chunks of 133M)
         if (n_ch > 1 && c->prm.chunk_paths == 0) {
             const uint64_t lo_px = (P_all + (n_ch - 1) - 1) / (n_ch - 1);
-            if (lo_px * p->spp * nf <= cap_paths + cap_paths / 4) {
+            if (lo_px * p->spp * nf <= chunk_most(c) / sh_per_path) {
                 --n_ch;
                 P_chunk = (uint32_t)lo_px;
             }
@@ -2319,6 +2327,11 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         P_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(P_all, cap_paths));
         S_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(p->spp, cap_paths / P_chunk));
     }
+    if (ops && (P_chunk < P_all || S_chunk < p->spp)) {
+        for (const PendingOp& o : *ops)  // flush() groups gathered frames so that each group is one chunk
+            if (o.kind != PendingOp::RENDER)
+                return fail(KHP_EINVAL, "internal: a fused batch with gathers or snapshots spans more than one chunk");
+    }
     if (bdm && nf == 1) {  // the light subpaths of a chunk's sample slots take at most a quarter of the free HBM
         size_t free_b = 0, total_b = 0;
         const size_t per_slot = (size_t)c->bd.light_paths * c->S.n_lights * c->bd.vertices * 48;
@@ -2331,8 +2344,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     size_t want = (size_t)P_chunk * S_chunk * nf;
     if (nf > 1) {
         const uint32_t fuse = std::max<uint32_t>(1, std::min<uint32_t>(c->prm.fuse_frames, KHP_MAX_FUSE));
-        const size_t most = cap_paths + (c->prm.chunk_paths == 0 ? cap_paths / 4 : 0);
-        want = std::max(want, std::min<size_t>(most, (size_t)P_all * S_chunk * fuse));
+        want = std::max(want, std::min<size_t>(chunk_most(c) / sh_per_path, (size_t)P_all * S_chunk * fuse));
     }
     PathSet& w = c->ps[slot];
     s = ensure_wave(c, w, want, sh_per_path);
@@ -2638,7 +2650,8 @@ static khp_status flush(khp_ctx* c) {
             P = tmp.size();
         }
     }
-    const size_t cap_paths = chunk_paths(c);
+    const uint32_t sh_per_path = (c->bd.enabled != 0 && c->S.n_lights > 0) ? c->bd.vertices : 1u;
+    const size_t cap_paths = chunk_most(c) / sh_per_path;
     const bool one_chunk = P * (size_t)first->p.spp * nr <= cap_paths;
     if (nr == 1 || !gathers || one_chunk) {
         if (nr == 1) {

@@ -87,3 +87,38 @@ def test_local_group_gather_assembles_the_frame(world, async_):
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_local_group_driver_batch_two_ranks():
+    """The driver's 2-GPU bench at the metric size, on one GPU: each of 2 ranks
+    renders its tiles of 20 fused 8-spp passes with a gather after every pass
+    (bench.py at N > 1).  A rank's 20 passes are 166M paths, within 5/4 of the
+    2^27 cap, so flush() keeps them one group and enqueue_frames one chunk (5
+    k_extend launches, not a 16 + 4 split).  Rank 0's frame equals the single-rank
+    frame of the same passes, bit for bit."""
+    from ba_pathtracing_fur_amd.pathtracer import HipContext, comm_init_local
+    W, H, SPP, PASSES, TILE = 1920, 1080, 8, 20, 64
+    ctxs = [HipContext(0) for _ in range(2)]
+    try:
+        for c in ctxs:
+            S.config3_device(c, W, H, n_strands=1_000_000)
+            c.build_accel()
+        for k in range(PASSES):
+            ctxs[0].render(W, H, SPP, 5, first_sample=k * SPP, readback=False, async_=True)
+        ctxs[0].sync()
+        want = ctxs[0].read_framebuffer(W, H)
+        comm_init_local(ctxs)
+        for k in range(PASSES):
+            for r in (1, 0):
+                ctxs[r].render(W, H, SPP, 5, first_sample=k * SPP, tile_size=TILE, tile_rank=r, tile_nranks=2,
+                               readback=False, async_=True)
+                ctxs[r].gather_framebuffer(W, H, SPP, 5, TILE, 2, r, 0)
+        ctxs[1].sync()
+        assert ctxs[1].stats()["extend_launches"] == 5
+        ctxs[0].sync()
+        assert ctxs[0].stats()["extend_launches"] == 5
+        got = ctxs[0].read_framebuffer(W, H)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    finally:
+        for c in ctxs:
+            c.close()
