@@ -1192,6 +1192,33 @@ __global__ __launch_bounds__(256) void k_accumulate(Wave Wv, float* fb, uint32_t
     o[0] = r; o[1] = g; o[2] = b;
 }
 
+// All fused frames of a chunk in one launch (a batch with no gather or snapshot
+// between its frames): the same running mean, frame after frame in call order,
+// with one framebuffer read and write per pixel instead of one per frame.
+__global__ __launch_bounds__(256) void k_accumulate_all(Wave Wv, float* fb) {
+    uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= Wv.P) return;
+    uint32_t pixel = Wv.pix[Wv.p_off + p];
+    float* o = fb + 3 * (size_t)pixel;
+    float r = o[0], g = o[1], b = o[2];
+    for (uint32_t fr = 0; fr < Wv.n_frames; ++fr) {
+        const size_t base = path_index(Wv, fr, p, 0);
+        for (uint32_t s = 0; s < Wv.n_samples; ++s) {
+            const float4 ck = Wv.CK[base + s];
+            const uint32_t k = Wv.fsample0[fr] + s;
+            if (k == 0) {
+                r = ck.x; g = ck.y; b = ck.z;
+            } else {
+                const float kk = (float)(k + 1);
+                r = r + (ck.x - r) / kk;
+                g = g + (ck.y - g) / kk;
+                b = b + (ck.z - b) / kk;
+            }
+        }
+    }
+    o[0] = r; o[1] = g; o[2] = b;
+}
+
 // ---- output stage: Texture::setPixel byte conversion and Tonemapper::map ---------------
 // Texture::toByte (Texture.h:252-254): (uchar)std::max(std::min(f * 255, 255), 0).
 // std::min(a, b) = (b < a) ? b : a and std::max(a, b) = (a < b) ? b : a, so a
@@ -2547,8 +2574,13 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 acc_waited = true;
             }
             timed(c, f, 3, true, sA);
+            bool only_renders = true;
+            if (ops)
+                for (const PendingOp& o : *ops) only_renders = only_renders && o.kind == PendingOp::RENDER;
             if (!ops) {
                 hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, c->fb.as<float>(), 0u);
+            } else if (only_renders) {
+                hipLaunchKernelGGL(k_accumulate_all, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, c->fb.as<float>());
             } else {
                 // fused frames in call order; a gather between two of them runs on the
                 // context stream after the first's accumulate and before the second's
