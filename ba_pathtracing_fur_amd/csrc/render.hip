@@ -234,11 +234,15 @@ __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
 #ifndef KHP_EXT_WAVES
 #define KHP_EXT_WAVES 6
 #endif
+#ifndef KHP_EXT_REFILL
+#define KHP_EXT_REFILL 24
+#endif
 constexpr int RING = 8;        // LDS ring entries per lane (3 x 4 B each), k_shadow
 constexpr int REFILL = 24;     // refill when >= REFILL lanes are idle
 constexpr int TRAV_WAVES = 6;  // __launch_bounds__ waves per SIMD, k_shadow
 constexpr int EXT_RING = KHP_EXT_RING;    // the same for k_extend
 constexpr int EXT_WAVES = KHP_EXT_WAVES;
+constexpr int EXT_REFILL = KHP_EXT_REFILL;  // k_extend's refill threshold
 constexpr size_t LDS_BYTES = 3 * RING * TRAV_BLOCK * sizeof(uint32_t);
 constexpr size_t EXT_LDS_BYTES = 3 * EXT_RING * TRAV_BLOCK * sizeof(uint32_t);
 template <bool STATS>
@@ -365,7 +369,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wa
     cl.init(Wv.cnt->fetch_ext, nf, nb, Wv.cap);
     for (;;) {
         unsigned long long idle = __ballot(!has);
-        if (!exhausted && __popcll(idle) >= REFILL) {
+        if (!exhausted && __popcll(idle) >= EXT_REFILL) {
             uint32_t my;
             const bool got = cl.claim(idle, my, exhausted);
             if (!has && got) {
@@ -413,7 +417,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wa
                 }
             }
             act = __ballot(has);
-            if (act == 0 || (!exhausted && 64 - __popcll(act) >= REFILL)) break;
+            if (act == 0 || (!exhausted && 64 - __popcll(act) >= EXT_REFILL)) break;
         }
     }
     if (STATS)

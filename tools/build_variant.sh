@@ -1,14 +1,16 @@
 #!/bin/bash
-# Build libkirk_hip.so with extra compile definitions into ba_pathtracing_fur_amd/lib/variants/<name>/
-# for A/B runs (KHP_LIB=<that .so> python bench.py ...).  usage: tools/build_variant.sh <name> -DFOO=1 ...
+# Build a variant of libkirk_hip.so with extra -D flags for an A/B on the GPU box
+# (bench.py / tests pick it up with KHP_LIB=<path>).  Run here, on the CPU, after
+# the regular build (it links the regular scene/bvh/flatten objects).
+# usage: tools/build_variant.sh <name> -DKHP_EXT_REFILL=32 ...   -> variants/libkirk_<name>.so
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
-C=$R/ba_pathtracing_fur_amd/csrc
-O=$R/ba_pathtracing_fur_amd/lib/variants/$NAME
-mkdir -p $O
-FL="-O3 -ffp-contract=off -fno-fast-math -fPIC -std=c++17 -Wall -Wno-unused-function --offload-arch=gfx950 -fno-slp-vectorize"
-/opt/rocm/bin/hipcc $FL "$@" -c ${SRC:-$C/render.hip} -o $O/render.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $O/libkirk_hip.so $O/render.o $R/ba_pathtracing_fur_amd/lib/obj/scene.o \
-  $R/ba_pathtracing_fur_amd/lib/obj/bvh_build.o $R/ba_pathtracing_fur_amd/lib/obj/flatten.o -L/opt/rocm/lib -lrccl -lpthread -Wl,-rpath,/opt/rocm/lib
-echo "built $O/libkirk_hip.so ($*)"
+mkdir -p "$R/variants"
+cd "$R/ba_pathtracing_fur_amd/csrc"
+/opt/rocm/bin/hipcc -O3 -ffp-contract=off -fno-fast-math -fPIC -std=c++17 -Wall -Wno-unused-function \
+  --offload-arch=gfx950 -fno-slp-vectorize "$@" -c render.hip -o "$R/variants/render_$NAME.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$R/variants/libkirk_$NAME.so" "$R/variants/render_$NAME.o" \
+  ../lib/obj/scene.o ../lib/obj/bvh_build.o ../lib/obj/flatten.o -L/opt/rocm/lib -lrccl -lpthread -Wl,-rpath,/opt/rocm/lib
+rm -f "$R/variants/render_$NAME.o"
+echo "$R/variants/libkirk_$NAME.so"
