@@ -266,6 +266,29 @@ struct SpillArea {
 constexpr uint32_t SEG_PER_XCD = 4;
 constexpr uint32_t NSEG = 8u * SEG_PER_XCD;
 static_assert(NSEG <= KHP_MAX_SEG, "claim cursors");
+// Claim blocks (KHP_CLAIM_BLOCK_LOG2 = L > 0): instead of one contiguous slice
+// per segment, the queue is cut into blocks of 2^L entries dealt round-robin to
+// the NSEG segments (block b to segment b % NSEG), so all segments sweep the
+// queue side by side and the rays in flight on the chip come from one window
+// of NSEG x 2^L entries.  L = 0: contiguous slices.
+#ifndef KHP_CLAIM_BLOCK_LOG2
+#define KHP_CLAIM_BLOCK_LOG2 0
+#endif
+constexpr uint32_t CB_LOG = KHP_CLAIM_BLOCK_LOG2;
+// first index (in a part of n entries) of segment g's share, g = 0..NSEG
+__device__ __forceinline__ uint32_t seg_start(uint32_t n, uint32_t g) {
+    if (CB_LOG == 0) return (uint32_t)((uint64_t)n * g / NSEG);
+    if (n == 0) return 0u;
+    const uint32_t nb = (n + (1u << CB_LOG) - 1u) >> CB_LOG;
+    uint32_t s = ((nb / NSEG) * g + (nb % NSEG < g ? nb % NSEG : g)) << CB_LOG;
+    if ((nb - 1u) % NSEG < g) s -= (nb << CB_LOG) - n;  // the last, partial block lies before segment g
+    return s;
+}
+// index in the part of local entry i of segment g (a bijection onto [0, n))
+__device__ __forceinline__ uint32_t seg_map(uint32_t n, uint32_t g, uint32_t i) {
+    if (CB_LOG == 0) return seg_start(n, g) + i;
+    return (((i >> CB_LOG) * NSEG + g) << CB_LOG) | (i & ((1u << CB_LOG) - 1u));
+}
 struct Claimer {
     uint32_t* fetch;  // NSEG cursors, one 128-B line each
     uint32_t n;       // queue length
@@ -274,8 +297,9 @@ struct Claimer {
     uint32_t rseg;    // segment of the current reservation
     uint32_t tried;   // segments found exhausted
     uint32_t res_lo, res_hi;  // reserved, not yet handed out
-    // Segment g holds the front-part slice [nf*g/NSEG, nf*(g+1)/NSEG) followed by
-    // the back-part slice [nl*g/NSEG, nl*(g+1)/NSEG): long rays first everywhere.
+    // Segment g holds its share of the front part (seg_start / seg_map: the slice
+    // [nf*g/NSEG, nf*(g+1)/NSEG), or every NSEG-th claim block) followed by its
+    // share of the back part: long rays first everywhere.
     __device__ __forceinline__ void init(uint32_t* f, uint32_t front, uint32_t back, uint32_t capacity) {
         fetch = f;
         nf = front;
@@ -287,13 +311,13 @@ struct Claimer {
         tried = 0;
         res_lo = res_hi = 0;
     }
-    __device__ __forceinline__ uint32_t hlo(uint32_t g) const { return (uint32_t)((uint64_t)nf * g / NSEG); }
-    __device__ __forceinline__ uint32_t llo(uint32_t g) const { return (uint32_t)((uint64_t)nl * g / NSEG); }
+    __device__ __forceinline__ uint32_t hlo(uint32_t g) const { return seg_start(nf, g); }
+    __device__ __forceinline__ uint32_t llo(uint32_t g) const { return seg_start(nl, g); }
     __device__ __forceinline__ uint32_t lo(uint32_t g) const { return hlo(g) + llo(g); }
     // physical queue slot of virtual index v of the current reservation
     __device__ __forceinline__ uint32_t phys(uint32_t v) const {
         const uint32_t local = v - lo(rseg), hf = hlo(rseg + 1) - hlo(rseg);
-        return local < hf ? hlo(rseg) + local : cap - 1u - (llo(rseg) + (local - hf));
+        return local < hf ? seg_map(nf, rseg, local) : cap - 1u - seg_map(nl, rseg, local - hf);
     }
     // Reserve up to `want` indices from the current segment (moving on when it runs dry).
     __device__ __forceinline__ void reserve(uint32_t want) {
