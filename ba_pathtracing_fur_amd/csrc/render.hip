@@ -87,6 +87,7 @@ struct Wave {
     uint32_t n_samples;   // samples in this chunk (per frame)
     uint32_t n_frames;    // fused frames in this chunk
     uint32_t pix_major;   // path numbering (khp_ctx_params.path_order): 0 frame-major, 1 pixel-major
+    uint32_t cam0;        // bounce 0 computes camera rays in place (no k_generate queue)
     uint32_t fsample0[KHP_MAX_FUSE];  // per fused frame: global sample index of chunk sample 0
     uint32_t depth;
     uint8_t* heavy;       // per queue slot: the ray's traversal took more than heavy_T iterations
@@ -180,6 +181,24 @@ __device__ __forceinline__ T wave_sum(T v) {
 
 // ---- generate: camera rays (PathTracer::generatePrimaryRays, CPU_PathTracer.cpp:118-127;
 //      Camera::getRayFromPixel, Camera.cpp:59-66) -------------------------------------------
+// Camera ray and RNG key of path pid.  k_generate writes them to the bounce-0
+// queue; with Wave::cam0 set, k_extend and k_shade compute them in place at
+// bounce 0 instead (queue slot = path there), the same operations.
+__device__ __forceinline__ Ray camera_path(const DevScene& S, const Wave& Wv, uint32_t pid, uint32_t& key) {
+    // the samples of one pixel are adjacent paths (path_coords), so a wave traces
+    // a few neighbouring pixels x all their samples (cache reuse)
+    uint32_t fr, p_local, s_local;
+    path_coords(Wv, pid, fr, p_local, s_local);
+    const uint32_t pixel = Wv.pix[Wv.p_off + p_local];
+    const uint32_t x = pixel % Wv.W, y = pixel / Wv.W;
+    key = path_key(Wv.seed, pixel, Wv.fsample0[fr] + s_local);
+    const float u1 = draw_u01(key, dim_of(0, P_CAM_X)), u2 = draw_u01(key, dim_of(0, P_CAM_Y));
+    const khp_camera& cam = S.cam;
+    const float s1 = ((float)x + u1) * cam.pixel_size, s2 = ((float)y + u2) * cam.pixel_size;
+    const v3 dir = ((ld3(cam.bottom_left) + ld3(cam.axis_x) * s1) + ld3(cam.axis_y) * s2) - ld3(cam.position);
+    return make_ray(ld3(cam.position), dir);
+}
+
 __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
     uint32_t n = Wv.P * Wv.n_samples * Wv.n_frames;
     uint32_t pid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -188,23 +207,19 @@ __global__ __launch_bounds__(256) void k_generate(DevScene S, Wave Wv) {
         Wv.cnt->nqb[0] = 0;
     }
     if (pid >= n) return;
-    // the samples of one pixel are adjacent paths (path_coords), so a wave traces
-    // a few neighbouring pixels x all their samples (cache reuse)
-    uint32_t fr, p_local, s_local;
-    path_coords(Wv, pid, fr, p_local, s_local);
-    uint32_t pixel = Wv.pix[Wv.p_off + p_local];
-    uint32_t x = pixel % Wv.W, y = pixel / Wv.W;
-    uint32_t key = path_key(Wv.seed, pixel, Wv.fsample0[fr] + s_local);
-    float u1 = draw_u01(key, dim_of(0, P_CAM_X)), u2 = draw_u01(key, dim_of(0, P_CAM_Y));
-    const khp_camera& cam = S.cam;
-    float s1 = ((float)x + u1) * cam.pixel_size, s2 = ((float)y + u2) * cam.pixel_size;
-    v3 dir = ((ld3(cam.bottom_left) + ld3(cam.axis_x) * s1) + ld3(cam.axis_y) * s2) - ld3(cam.position);
-    Ray r = make_ray(ld3(cam.position), dir);
+    uint32_t key;
+    const Ray r = camera_path(S, Wv, pid, key);
     Wv.qo[0][0][pid] = r.o.x; Wv.qo[0][1][pid] = r.o.y; Wv.qo[0][2][pid] = r.o.z;
     Wv.qd[0][0][pid] = r.d.x; Wv.qd[0][1][pid] = r.d.y; Wv.qd[0][2][pid] = r.d.z;
     Wv.qpid[0][pid] = pid;
     Wv.TFq[0][pid] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));  // queue slot = path at bounce 0
     Wv.CKq[0][pid] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));
+}
+
+// Wave::cam0: the bounce-0 queue is implicit (every path, in path order).
+__global__ void k_start(Counters* c, uint32_t n) {
+    c->nq[0] = n;
+    c->nqb[0] = 0;
 }
 
 __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
@@ -376,7 +391,9 @@ __device__ __forceinline__ void flush_stats(const TravStats& st, const Stack& st
 }
 
 // ---- extend: closest hit for every queued ray ------------------------------------------
-template <bool STATS>
+// CAM: bounce 0 with Wave::cam0 -- the ray of queue slot idx (= path idx) is
+// the camera ray, computed here instead of loaded.
+template <bool STATS, bool CAM = false>
 __global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t nf = Wv.cnt->nq[cur], nb = Wv.cnt->nqb[cur];
@@ -402,8 +419,13 @@ __global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wa
                 idx = cl.phys(my);
                 it = 0;
                 Ray r;
-                r.o = mk(Wv.qo[cur][0][idx], Wv.qo[cur][1][idx], Wv.qo[cur][2][idx]);
-                r.d = mk(Wv.qd[cur][0][idx], Wv.qd[cur][1][idx], Wv.qd[cur][2][idx]);
+                if (CAM) {
+                    uint32_t key_unused;
+                    r = camera_path(S, Wv, idx, key_unused);
+                } else {
+                    r.o = mk(Wv.qo[cur][0][idx], Wv.qo[cur][1][idx], Wv.qo[cur][2][idx]);
+                    r.d = mk(Wv.qd[cur][0][idx], Wv.qd[cur][1][idx], Wv.qd[cur][2][idx]);
+                }
                 trav_setup(tr, r);
                 h.t = FLT_MAX_;
                 h.slot = -1;
@@ -819,13 +841,23 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
         uint32_t bd_head = 0xFFFFFFFFu;  // BD: the group's head record (its rec[4] is written with the destination)
         float4 tfo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cko = tfo;  // the path state after this bounce
         if (active) {
-            pid = Wv.qpid[cur][i];
             Ray r;
-            r.o = mk(Wv.qo[cur][0][i], Wv.qo[cur][1][i], Wv.qo[cur][2][i]);
-            r.d = mk(Wv.qd[cur][0][i], Wv.qd[cur][1][i], Wv.qd[cur][2][i]);
+            float4 tf, ck;
+            if (bounce == 0 && Wv.cam0) {  // the bounce-0 state k_generate would have queued
+                uint32_t key0;
+                pid = i;
+                r = camera_path(S, Wv, i, key0);
+                tf = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));
+                ck = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key0));
+            } else {
+                pid = Wv.qpid[cur][i];
+                r.o = mk(Wv.qo[cur][0][i], Wv.qo[cur][1][i], Wv.qo[cur][2][i]);
+                r.d = mk(Wv.qd[cur][0][i], Wv.qd[cur][1][i], Wv.qd[cur][2][i]);
+                tf = Wv.TFq[cur][i];
+                ck = Wv.CKq[cur][i];
+            }
             float lambda = Wv.ht[i];
             int32_t slot = Wv.hslot[i];
-            const float4 tf = Wv.TFq[cur][i], ck = Wv.CKq[cur][i];
             v3 T = mk(tf.x, tf.y, tf.z);
             v3 C = mk(ck.x, ck.y, ck.z);
             int flags = (int)bits_from_f(tf.w);
@@ -2487,6 +2519,10 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     Wv.seed = p->seed;
     Wv.depth = p->depth;
     Wv.pix_major = c->prm.path_order;
+    // camera rays in place at bounce 0 (no generate pass): not for the light-path
+    // variant (its image-plane connections add to the queued bounce-0 state) nor
+    // when bounce 0's queue is dumped
+    Wv.cam0 = (!bdm && dump_b != 0) ? 1u : 0u;
     Wv.bd = BdptDev{bdm ? 1u : 0u, c->bd.light_paths, (uint32_t)c->S.n_lights, c->bd.vertices, c->bd.bias,
                     c->bd.bounce_bias, c->bd.min_pdf, c->bd.image_plane,
                     bdm ? w.lvb.as<float4>() : nullptr};
@@ -2504,7 +2540,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
             for (uint32_t q = 0; q < nf; ++q) Wv.fsample0[q] = fs0[q] + s0;
             const uint32_t npaths = P * ns * nf;
             timed(c, f, 3, true, sA);
-            hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wv);
+            if (Wv.cam0) hipLaunchKernelGGL(k_start, dim3(1), dim3(1), 0, sA, Wv.cnt, npaths);
+            else hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wv);
             if (bdm) {  // the light subpaths of this chunk's sample slots (frames x samples)
                 const uint32_t nsub = nf * ns * c->bd.light_paths * (uint32_t)c->S.n_lights;
                 hipLaunchKernelGGL(k_light_paths, dim3((nsub + 63) / 64), dim3(64), 0, sA, c->S, Wv);
@@ -2553,8 +2590,13 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 }
                 hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
                 timed(c, f, 0, true, sA);
-                if (stats)
+                const bool cam = b == 0 && Wv.cam0;
+                if (stats && cam)
+                    hipLaunchKernelGGL((k_extend<true, true>), dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                else if (stats)
                     hipLaunchKernelGGL(k_extend<true>, dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                else if (cam)
+                    hipLaunchKernelGGL((k_extend<false, true>), dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
                 else
                     hipLaunchKernelGGL(k_extend<false>, dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
                 timed(c, f, 0, false, sA);
