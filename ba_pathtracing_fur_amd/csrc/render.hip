@@ -292,49 +292,51 @@ static_assert(NSEG <= KHP_MAX_SEG, "claim cursors");
 #define KHP_CLAIM_BLOCK_LOG2 9
 #endif
 constexpr uint32_t CB_LOG = KHP_CLAIM_BLOCK_LOG2;
-// first index (in a part of n entries) of segment g's share, g = 0..NSEG
-__device__ __forceinline__ uint32_t seg_start(uint32_t n, uint32_t g) {
-    if (CB_LOG == 0) return (uint32_t)((uint64_t)n * g / NSEG);
-    if (n == 0) return 0u;
-    const uint32_t nb = (n + (1u << CB_LOG) - 1u) >> CB_LOG;
-    uint32_t s = ((nb / NSEG) * g + (nb % NSEG < g ? nb % NSEG : g)) << CB_LOG;
-    if ((nb - 1u) % NSEG < g) s -= (nb << CB_LOG) - n;  // the last, partial block lies before segment g
-    return s;
-}
-// index in the part of local entry i of segment g (a bijection onto [0, n))
-__device__ __forceinline__ uint32_t seg_map(uint32_t n, uint32_t g, uint32_t i) {
-    if (CB_LOG == 0) return seg_start(n, g) + i;
-    return (((i >> CB_LOG) * NSEG + g) << CB_LOG) | (i & ((1u << CB_LOG) - 1u));
-}
+constexpr uint32_t CB_MASK = (1u << CB_LOG) - 1u;
 struct Claimer {
     uint32_t* fetch;  // NSEG cursors, one 128-B line each
-    uint32_t n;       // queue length
     uint32_t nf, nl, cap;  // front / back parts, buffer capacity (longest-first queues)
+    uint32_t sf, sl;  // claim blocks: entries of each part per segment (padded to whole blocks)
     uint32_t sg;      // segment this wave is draining (wave-uniform)
     uint32_t rseg;    // segment of the current reservation
     uint32_t tried;   // segments found exhausted
     uint32_t res_lo, res_hi;  // reserved, not yet handed out
-    // Segment g holds its share of the front part (seg_start / seg_map: the slice
-    // [nf*g/NSEG, nf*(g+1)/NSEG), or every NSEG-th claim block) followed by its
-    // share of the back part: long rays first everywhere.
+    // Segment g holds its share of the front part followed by its share of the
+    // back part: long rays first everywhere.  Contiguous slices (L = 0): the
+    // slice [nf*g/NSEG, nf*(g+1)/NSEG) of each part.  Claim blocks (L > 0): each
+    // part is padded to NSEG*K blocks of 2^L entries, and segment g takes blocks
+    // g, g + NSEG, g + 2*NSEG, ...; entries in the padding are handed out as
+    // empty (the lane stays idle) -- at most NSEG*2^L per part.
     __device__ __forceinline__ void init(uint32_t* f, uint32_t front, uint32_t back, uint32_t capacity) {
         fetch = f;
         nf = front;
         nl = back;
         cap = capacity;
-        n = front + back;
+        const uint32_t per = NSEG << CB_LOG;
+        sf = CB_LOG ? ((front + per - 1u) / per) << CB_LOG : 0u;
+        sl = CB_LOG ? ((back + per - 1u) / per) << CB_LOG : 0u;
         rseg = 0;
         sg = (blockIdx.x % 8u) * SEG_PER_XCD + (blockIdx.x / 8u) % SEG_PER_XCD;
         tried = 0;
         res_lo = res_hi = 0;
     }
-    __device__ __forceinline__ uint32_t hlo(uint32_t g) const { return seg_start(nf, g); }
-    __device__ __forceinline__ uint32_t llo(uint32_t g) const { return seg_start(nl, g); }
-    __device__ __forceinline__ uint32_t lo(uint32_t g) const { return hlo(g) + llo(g); }
-    // physical queue slot of virtual index v of the current reservation
-    __device__ __forceinline__ uint32_t phys(uint32_t v) const {
-        const uint32_t local = v - lo(rseg), hf = hlo(rseg + 1) - hlo(rseg);
-        return local < hf ? seg_map(nf, rseg, local) : cap - 1u - seg_map(nl, rseg, local - hf);
+    __device__ __forceinline__ uint32_t hlo(uint32_t g) const { return (uint32_t)((uint64_t)nf * g / NSEG); }
+    __device__ __forceinline__ uint32_t llo(uint32_t g) const { return (uint32_t)((uint64_t)nl * g / NSEG); }
+    __device__ __forceinline__ uint32_t lo(uint32_t g) const { return CB_LOG ? g * (sf + sl) : hlo(g) + llo(g); }
+    // Physical queue slot of virtual index v of the current reservation; false
+    // for an entry of the claim-block padding (no ray).
+    __device__ __forceinline__ bool phys(uint32_t v, uint32_t& idx) const {
+        const uint32_t local = v - lo(rseg);
+        if (CB_LOG == 0) {
+            const uint32_t hf = hlo(rseg + 1) - hlo(rseg);
+            idx = local < hf ? hlo(rseg) + local : cap - 1u - (llo(rseg) + (local - hf));
+            return true;
+        }
+        const bool front = local < sf;
+        const uint32_t j = front ? local : local - sf;
+        const uint32_t m = (((j >> CB_LOG) * NSEG + rseg) << CB_LOG) | (j & CB_MASK);
+        idx = front ? m : cap - 1u - m;
+        return m < (front ? nf : nl);
     }
     // Reserve up to `want` indices from the current segment (moving on when it runs dry).
     __device__ __forceinline__ void reserve(uint32_t want) {
@@ -415,8 +417,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wa
         if (!exhausted && __popcll(idle) >= EXT_REFILL) {
             uint32_t my;
             const bool got = cl.claim(idle, my, exhausted);
-            if (!has && got) {
-                idx = cl.phys(my);
+            if (!has && got && cl.phys(my, idx)) {
                 it = 0;
                 Ray r;
                 if (CAM) {
@@ -1181,8 +1182,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, W
         if (!exhausted && __popcll(idle) >= REFILL) {
             uint32_t my;
             const bool got = cl.claim(idle, my, exhausted);
-            if (!has && got) {
-                idx = cl.phys(my);
+            if (!has && got && cl.phys(my, idx)) {
                 const float4* rec = Wv.sh + 6 * (size_t)idx;
                 float4 a = rec[0], b = rec[1];
                 Ray r;
