@@ -24,6 +24,7 @@ struct DevScene {
     const float* __restrict__ tri_nrm;   // object-id order, 9 floats per triangle
     const float* __restrict__ tri_frame; // object-id order, 9 floats per triangle: hair frame u v w
     const DevNode* __restrict__ nodes;   // interior nodes
+    const float4* __restrict__ wide;     // two-level records (traverse.h iterw), 8 float4 per node; null: not built
     const khp_material* __restrict__ mats;
     const DevLight* __restrict__ lights;
     int32_t n_lights;
@@ -188,6 +189,21 @@ __device__ __forceinline__ bool tri_test(float4 r0, float4 r1, float4 r2, const 
     t = dot(wu, ac) * inv;
     if ((t < tMin) || (t > tMax)) return false;
     return true;
+}
+
+// The barycentrics tri_test computes for an accepted triangle (the same
+// operations; they depend on the ray and the triangle only, not on the
+// window).  The closest-hit traversal keeps only t and the slot; the shading
+// side recomputes u, v from the ray it already has (triangles; cones: 0, 0).
+__device__ __forceinline__ void tri_uv(float4 r0, float4 r1, float4 r2, const Ray& r, float& u, float& v) {
+    v3 A = mk(r0.x, r0.y, r0.z), ab = mk(r1.x, r1.y, r1.z), ac = mk(r2.x, r2.y, r2.z);
+    v3 dv = cross(r.d, ac);
+    float det = dot(dv, ab);
+    float inv = 1.0f / det;
+    v3 w = r.o - A;
+    u = dot(dv, w) * inv;
+    v3 wu = cross(w, ab);
+    v = dot(wu, r.d) * inv;
 }
 
 // Cylinder::closestIntersection (Common/Cylinder.cpp:73-156), open cone frustum.

@@ -66,8 +66,6 @@ struct Wave {
     uint32_t* qpid[2];
     float* ht;
     int32_t* hslot;
-    float* hu;
-    float* hv;
     // Per-path state, one 16-B record per array so that k_shade and
     // k_shadow_finish, which reach paths in queue order (scattered pids after
     // bounce 0), touch one line per array instead of one per component:
@@ -257,6 +255,10 @@ constexpr int REFILL = 24;     // refill when >= REFILL lanes are idle
 constexpr int TRAV_WAVES = 6;  // __launch_bounds__ waves per SIMD, k_shadow
 constexpr int EXT_RING = KHP_EXT_RING;    // the same for k_extend
 constexpr int EXT_WAVES = KHP_EXT_WAVES;
+#ifndef KHP_EXT_WAVES_W
+#define KHP_EXT_WAVES_W 6
+#endif
+constexpr int EXT_WAVES_W = KHP_EXT_WAVES_W;  // k_extend over the two-level records (32 B more per record in flight)
 constexpr int EXT_REFILL = KHP_EXT_REFILL;  // k_extend's refill threshold
 constexpr size_t LDS_BYTES = 3 * RING * TRAV_BLOCK * sizeof(uint32_t);
 constexpr size_t EXT_LDS_BYTES = 3 * EXT_RING * TRAV_BLOCK * sizeof(uint32_t);
@@ -290,6 +292,18 @@ static_assert(NSEG <= KHP_MAX_SEG, "claim cursors");
 // Measured: 2^7..2^9 +0.9..1.3% over contiguous slices; 2^9 kept.
 #ifndef KHP_CLAIM_BLOCK_LOG2
 #define KHP_CLAIM_BLOCK_LOG2 9
+#endif
+// Two-level node records for k_extend (traverse.h iterw); 0: the 64-B loop only.
+// KHP_WIDE_FROM: the default first bounce that uses them (khp_ctx_params.wide_from,
+// ABI 10).  The camera and first
+// secondary bounces are cache-served and issue-bound, where the two-level step
+// (more VALU per iteration, 5 instead of 6 waves per SIMD) loses; the deep
+// bounces are bound by line fetches, which it cuts by a third.
+#ifndef KHP_WIDE
+#define KHP_WIDE 1
+#endif
+#ifndef KHP_WIDE_FROM
+#define KHP_WIDE_FROM 2   // default of khp_ctx_params.wide_from
 #endif
 constexpr uint32_t CB_LOG = KHP_CLAIM_BLOCK_LOG2;
 constexpr uint32_t CB_MASK = (1u << CB_LOG) - 1u;
@@ -395,8 +409,9 @@ __device__ __forceinline__ void flush_stats(const TravStats& st, const Stack& st
 // ---- extend: closest hit for every queued ray ------------------------------------------
 // CAM: bounce 0 with Wave::cam0 -- the ray of queue slot idx (= path idx) is
 // the camera ray, computed here instead of loaded.
-template <bool STATS, bool CAM = false>
-__global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
+// WIDE: the two-level records (S.wide, traverse.h iterw) instead of the 64-B loop.
+template <bool STATS, bool CAM = false, bool WIDE = false>
+__global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : EXT_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t nf = Wv.cnt->nq[cur], nb = Wv.cnt->nqb[cur];
     ExtStack<STATS> stk;
@@ -436,8 +451,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wa
                 if (!has) {  // missed the root box, or a NaN ray (no hit, see ray_has_nan)
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = -1;
-                    Wv.hu[idx] = 0.0f;
-                    Wv.hv[idx] = 0.0f;
                     Wv.heavy[idx] = 0;
                 }
             }
@@ -456,12 +469,15 @@ __global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wa
             if (has) {
                 bool occ_unused;
                 ++it;
-                if (iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused)) {
-                    Wv.ht[idx] = h.t;
-                    Wv.hslot[idx] = h.slot;
-                    Wv.hu[idx] = h.u;
-                    Wv.hv[idx] = h.v;
-                    Wv.heavy[idx] = it > Wv.heavy_T ? 1 : 0;
+                const bool fin = WIDE ? iterw<STATS>(S, tr, h, stk, mode, c, lf, st)
+                                      : iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused);
+                if (fin) {
+                    // the output addresses are formed here, not kept live through the loop
+                    uint32_t j = idx;
+                    asm volatile("" : "+v"(j));
+                    Wv.ht[j] = h.t;
+                    Wv.hslot[j] = h.slot;
+                    Wv.heavy[j] = it > Wv.heavy_T ? 1 : 0;
                     has = false;
                 }
             }
@@ -472,6 +488,21 @@ __global__ __launch_bounds__(TRAV_BLOCK, EXT_WAVES) void k_extend(DevScene S, Wa
     if (STATS)
         flush_stats(st, stk, wit, wbusy, &Wv.cnt->node_visits, &Wv.cnt->prim_tests, &Wv.cnt->pruned, &Wv.cnt->iters,
                     &Wv.cnt->lanes_busy, &Wv.cnt->spills);
+}
+
+// Host-side launch of the k_extend instance for (stats, camera rays in place, wide records).
+static void launch_extend(bool stats, bool cam, bool wide, int grid, hipStream_t s, const DevScene& S, const Wave& W,
+                          int cur, SpillArea sp) {
+    const dim3 g(grid), b(TRAV_BLOCK);
+#define KHP_EXT(ST, CA, WI) hipLaunchKernelGGL((k_extend<ST, CA, WI>), g, b, EXT_LDS_BYTES, s, S, W, cur, sp)
+    if (wide) {
+        if (stats) { if (cam) KHP_EXT(true, true, true); else KHP_EXT(true, false, true); }
+        else { if (cam) KHP_EXT(false, true, true); else KHP_EXT(false, false, true); }
+    } else {
+        if (stats) { if (cam) KHP_EXT(true, true, false); else KHP_EXT(true, false, false); }
+        else { if (cam) KHP_EXT(false, true, false); else KHP_EXT(false, false, false); }
+    }
+#undef KHP_EXT
 }
 
 // ---- light-path variant (khp_bdpt_params, ABI 7; lightpath.h) ----------------------------
@@ -486,6 +517,7 @@ __device__ __forceinline__ v3 surface_at(const DevScene& S, const Ray& r, const 
     const float4* pr = S.prims + 4 * (size_t)h.slot;
     s.m = &S.mats[ax.mat];
     v3 nrm;
+    float bu = 0.0f, bv = 0.0f;  // barycentrics of a triangle hit (Hit::u, v are not used: tri_uv)
     if (ax.flags & 1u) {
         const float4 c0 = pr[0], c1 = pr[1], c2 = pr[2], c3 = pr[3];
         s.U = mk(c1.x, c1.y, c1.z);
@@ -497,9 +529,10 @@ __device__ __forceinline__ v3 surface_at(const DevScene& S, const Ray& r, const 
         const v3 nn = normalize(q1 - mk(c0.x, c0.y, c0.z));
         nrm = normalize(nn + s.V * c1.w);
     } else {
+        tri_uv(pr[0], pr[1], pr[2], r, bu, bv);  // the hit's barycentrics (traversal keeps t and slot only)
         const float* tn = S.tri_nrm + 9 * (size_t)ax.obj;
-        const float bx = (1.0f - h.u) - h.v;
-        nrm = normalize((ld3(tn) * bx + ld3(tn + 3) * h.u) + ld3(tn + 6) * h.v);
+        const float bx = (1.0f - bu) - bv;
+        nrm = normalize((ld3(tn) * bx + ld3(tn + 3) * bu) + ld3(tn + 6) * bv);
         const float* tf = S.tri_frame + 9 * (size_t)ax.obj;
         s.U = ld3(tf);
         s.V = ld3(tf + 3);
@@ -508,7 +541,7 @@ __device__ __forceinline__ v3 surface_at(const DevScene& S, const Ray& r, const 
     s.n = nrm;
     if (TEX) {  // calcTcoord (traceRay, CPU_PathTracer.cpp:178-179), then the textured parameters
         mres = S.mats[ax.mat];
-        textured_material(S, ax, pr, follow(r, h.t), s, h.u, h.v, mres);
+        textured_material(S, ax, pr, follow(r, h.t), s, bu, bv, mres);
         s.m = &mres;
     }
     return nrm;
@@ -888,7 +921,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uin
                 // normal and hair frame (Cylinder::calcNormal / Triangle::calcNormal), material
                 ShadeCtx s;
                 khp_material mres;
-                const Hit hh{lambda, slot, Wv.hu[i], Wv.hv[i]};
+                const Hit hh{lambda, slot, 0.0f, 0.0f};  // u, v: surface_at recomputes them
                 const v3 nrm = surface_at<TEX>(S, r, hh, s, mres);
                 const v3 loc = follow(r, lambda);
                 const khp_material* m = s.m;
@@ -1469,6 +1502,51 @@ __global__ void k_tri_slots(const float4* prims, const Aux* aux, uint32_t n_slot
     if (o < n_tris) out[o] = s;
 }
 
+// Two-level records (traverse.h iterw) from the 64-B node records, one thread
+// per record.  Sets *bad when an interior child's box is not the std::min /
+// std::max union of its children's boxes, or a child box of it is not ordered
+// (mn <= mx on every axis, NaN fails): the composition in iterw would not be
+// KIRK's slab then, and the context keeps the 64-B loop.
+__global__ void k_wide_records(const DevNode* nodes, uint32_t n, float4* wide, uint32_t* bad) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const DevNode X = nodes[r];
+    const bool pad = X.ref[0] == 0 && X.ref[1] == 0;  // unused record of a pair (no node has the root as child)
+    float4 o[6];
+    int32_t gref[4] = {0, 0, 0, 0};
+    bool ok = true;
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t cr = (uint32_t)X.ref[k];
+        // C's box as stored in X (left: a0 a1 a2 | a3 b0 b1; right: b2 b3 c0 | c1 c2 c3)
+        const float cb[6] = {k ? X.b[2] : X.a[0], k ? X.b[3] : X.a[1], k ? X.c[0] : X.a[2],
+                             k ? X.c[1] : X.a[3], k ? X.c[2] : X.b[0], k ? X.c[3] : X.b[1]};
+        if (pad || (cr & LEAF_BIT)) {
+            o[3 * k] = make_float4(cb[0], cb[1], cb[2], cb[3]);
+            o[3 * k + 1] = make_float4(cb[4], cb[5], 0.0f, 0.0f);
+            o[3 * k + 2] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            continue;
+        }
+        const DevNode C = nodes[cr];
+        o[3 * k] = make_float4(C.a[0], C.a[1], C.a[2], C.a[3]);
+        o[3 * k + 1] = make_float4(C.b[0], C.b[1], C.b[2], C.b[3]);
+        o[3 * k + 2] = make_float4(C.c[0], C.c[1], C.c[2], C.c[3]);
+        gref[2 * k] = C.ref[0];
+        gref[2 * k + 1] = C.ref[1];
+        const float l[6] = {C.a[0], C.a[1], C.a[2], C.a[3], C.b[0], C.b[1]};
+        const float rr[6] = {C.b[2], C.b[3], C.c[0], C.c[1], C.c[2], C.c[3]};
+        for (int a = 0; a < 3; ++a) {
+            ok = ok && l[a] <= l[a + 3] && rr[a] <= rr[a + 3];
+            ok = ok && __float_as_uint(wmin(l[a], rr[a])) == __float_as_uint(cb[a]);
+            ok = ok && __float_as_uint(wmax(l[a + 3], rr[a + 3])) == __float_as_uint(cb[a + 3]);
+        }
+    }
+    float4* w = wide + 8 * (size_t)r;
+    for (int k = 0; k < 6; ++k) w[k] = o[k];
+    w[6] = make_float4(__int_as_float(X.ref[0]), __int_as_float(X.ref[1]), __int_as_float(gref[0]), __int_as_float(gref[1]));
+    w[7] = make_float4(__int_as_float(gref[2]), __int_as_float(gref[3]), 0.0f, 0.0f);
+    if (!ok) atomicOr(bad, 1u);
+}
+
 // ---- multi-GPU: pack owned pixels / scatter a rank's pixels ------------------------------
 __global__ void k_pack(const float* fb, const uint32_t* pix, uint32_t P, float* out) {
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1509,7 +1587,7 @@ struct TimedLaunch {
 // extend / shade / accumulate; B: the shadow stage).
 struct PathSet {
     size_t cap = 0;
-    DevMem qbuf[2][7], ht, hslot, hu, hv, TFq[2], CKq[2], CKb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
+    DevMem qbuf[2][7], ht, hslot, TFq[2], CKq[2], CKb, shb[2], visb[2], shqb, cnt, spill, spill_sh;
     DevMem heavyb;
     DevMem permb, hkeyb, hclsb;   // shade_order 1
     DevMem lvb;                   // light-path variant: subpath vertices of a chunk's sample slots
@@ -1574,6 +1652,7 @@ struct khp_ctx {
     HostScene hs;
     bool scene_set = false, built = false;
     DevMem prims, aux, trinrm, trifrm, nodes, mats, lights, trislot;
+    DevMem wide, wide_bad;   // two-level node records (KHP_WIDE), the build's union check flag
     DevMem triuv, coneh, texd, texels, mtex;   // ABI 6 textures
     DevScene S{};
     khp_ctx_params prm{};
@@ -1610,7 +1689,7 @@ struct khp_ctx {
     std::vector<hipEvent_t> ev_pool;
     size_t ev_next = 0;
     std::vector<TimedLaunch> launches;
-    int grid_ext = 0, grid_sh = 0, grid_shade = 0;
+    int grid_ext = 0, grid_ext_w = 0, grid_sh = 0, grid_shade = 0;  // grid_ext_w: k_extend on wide records
     khp_stats st{};
     // rccl gather: pixel lists cached per (W, H, tile, nranks, rank, root)
     uint32_t gather_key[6] = {0, 0, 0, 0, 0, 0};
@@ -1663,6 +1742,7 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->shade_order = 0;       // hit sorting measured, off
     out->serial_stages = 0;
     out->path_order = 1;       // pixel-major fused chunks, +5-7%
+    out->wide_from = KHP_WIDE_FROM;  // two-level records from bounce 2
 }
 
 extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {
@@ -1998,6 +2078,22 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         HIPCHK(upload(c->texels, hs.texels.data(), hs.texels.size(), c->stream));
         HIPCHK(upload(c->mtex, hs.mtex.data(), hs.mtex.size(), c->stream));
     }
+    // Two-level node records for k_extend (traverse.h iterw), when every node's
+    // box is the union of its children's (always, for KIRK's build).
+    bool wide_ok = false;
+    if (KHP_WIDE && n_dnodes > 0) {
+        HIPCHK(c->wide.ensure((size_t)n_dnodes * 8 * sizeof(float4)));
+        HIPCHK(c->wide_bad.ensure(sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(c->wide_bad.p, 0, sizeof(uint32_t), c->stream));
+        hipLaunchKernelGGL(k_wide_records, dim3((n_dnodes + 255) / 256), dim3(256), 0, c->stream,
+                           c->nodes.as<DevNode>(), n_dnodes, c->wide.as<float4>(), c->wide_bad.as<uint32_t>());
+        HIPCHK(hipGetLastError());
+        uint32_t bad = 1;
+        HIPCHK(hipMemcpyAsync(&bad, c->wide_bad.p, sizeof(bad), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        wide_ok = bad == 0;
+    }
+    if (!wide_ok) c->wide.release();
     HIPCHK(c->trislot.ensure(4 * (size_t)std::max(hs.n_tris, 1u)));
     if (hs.n_tris > 0 && n_slots > 0)
         hipLaunchKernelGGL(k_tri_slots, dim3((n_slots + 255) / 256), dim3(256), 0, c->stream, c->prims.as<float4>(),
@@ -2012,6 +2108,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     S.tri_nrm = host_build ? c->trinrm.as<float>() : c->obj.tri_nrm.as<float>();
     S.tri_frame = host_build ? c->trifrm.as<float>() : c->obj.tri_frame.as<float>();
     S.nodes = c->nodes.as<DevNode>();
+    S.wide = wide_ok ? c->wide.as<float4>() : nullptr;
     S.mats = c->mats.as<khp_material>();
     S.lights = c->lights.as<DevLight>();
     S.n_lights = (int32_t)hs.lights.size();
@@ -2034,7 +2131,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     c->st.n_leaves = (c->st.n_nodes + 1) / 2;
     c->st.bvh_depth = hs.depth;
     c->st.max_leaf_size = hs.max_leaf;
-    c->st.device_bytes = c->prims.bytes + c->aux.bytes + c->trinrm.bytes + c->trifrm.bytes + c->nodes.bytes + c->mats.bytes +
+    c->st.device_bytes = c->prims.bytes + c->aux.bytes + c->trinrm.bytes + c->trifrm.bytes + c->nodes.bytes + c->wide.bytes + c->mats.bytes +
                          c->lights.bytes;
     // persistent grid sizes
     int nb = 0;
@@ -2043,6 +2140,12 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     else
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false>, TRAV_BLOCK, EXT_LDS_BYTES));
     c->grid_ext = std::max(1, nb) * c->n_cu;
+    nb = 0;
+    if (c->flags & KHP_CTX_STATS)
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<true, false, true>, TRAV_BLOCK, EXT_LDS_BYTES));
+    else
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false, false, true>, TRAV_BLOCK, EXT_LDS_BYTES));
+    c->grid_ext_w = std::min(c->grid_ext, std::max(1, nb) * c->n_cu);  // the spill columns are sized by grid_ext
     nb = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, TRAV_BLOCK, LDS_BYTES));
     c->grid_sh = std::max(1, nb) * c->n_cu;
@@ -2062,8 +2165,6 @@ static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap, size_t sh_per_
         for (int k = 0; k < 7; ++k) HIPCHK(w.qbuf[q][k].ensure(cap * 4));
     HIPCHK(w.ht.ensure(cap * 4));
     HIPCHK(w.hslot.ensure(cap * 4));
-    HIPCHK(w.hu.ensure(cap * 4));
-    HIPCHK(w.hv.ensure(cap * 4));
     for (int q = 0; q < 2; ++q) {
         HIPCHK(w.TFq[q].ensure(cap * sizeof(float4)));
         HIPCHK(w.CKq[q].ensure(cap * sizeof(float4)));
@@ -2104,8 +2205,6 @@ static Wave wave_view(const khp_ctx* c, PathSet& w) {
     }
     Wv.ht = w.ht.as<float>();
     Wv.hslot = w.hslot.as<int32_t>();
-    Wv.hu = w.hu.as<float>();
-    Wv.hv = w.hv.as<float>();
     for (int q = 0; q < 2; ++q) {
         Wv.TFq[q] = w.TFq[q].as<float4>();
         Wv.CKq[q] = w.CKq[q].as<float4>();
@@ -2400,6 +2499,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     f.nf = nf;
     const int G = async ? F : 1;
     const int grid_ext = std::max(1, c->grid_ext / G), grid_sh = std::max(1, c->grid_sh / G);
+    const int grid_ext_w = std::max(1, c->grid_ext_w / G);
     // Chunks: the owned pixels x samples (x fused frames) are cut into chunks
     // of at most chunk_paths() paths, pixel-major; a fused chunk carries all
     // samples of all frames of its pixels.
@@ -2591,14 +2691,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
                 timed(c, f, 0, true, sA);
                 const bool cam = b == 0 && Wv.cam0;
-                if (stats && cam)
-                    hipLaunchKernelGGL((k_extend<true, true>), dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
-                else if (stats)
-                    hipLaunchKernelGGL(k_extend<true>, dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
-                else if (cam)
-                    hipLaunchKernelGGL((k_extend<false, true>), dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
-                else
-                    hipLaunchKernelGGL(k_extend<false>, dim3(grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, sA, c->S, Wb, cur, sp_ext);
+                const bool wide = c->S.wide != nullptr && b >= c->prm.wide_from;
+                launch_extend(stats, cam, wide, wide ? grid_ext_w : grid_ext, sA, c->S, Wb, cur, sp_ext);
                 timed(c, f, 0, false, sA);
                 if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
                 timed(c, f, 1, true, sA);
@@ -3216,8 +3310,18 @@ __global__ void k_store_hits(DevScene S, uint32_t n, Wave Wv, float* t, int32_t*
     int32_t sl = Wv.hslot[i];
     t[i] = Wv.ht[i];
     obj[i] = sl >= 0 ? (int32_t)S.aux[sl].obj : -1;
-    uv[2 * i] = Wv.hu[i];
-    uv[2 * i + 1] = Wv.hv[i];
+    float u = 0.0f, v = 0.0f;  // the traversal keeps t and slot; barycentrics of a triangle hit from the ray
+    if (sl >= 0) {
+        const float4* p = S.prims + 4 * (size_t)sl;
+        if (is_tri(p[0])) {
+            Ray r;
+            r.o = mk(Wv.qo[0][0][i], Wv.qo[0][1][i], Wv.qo[0][2][i]);
+            r.d = mk(Wv.qd[0][0][i], Wv.qd[0][1][i], Wv.qd[0][2][i]);
+            tri_uv(p[0], p[1], p[2], r, u, v);
+        }
+    }
+    uv[2 * i] = u;
+    uv[2 * i + 1] = v;
 }
 
 // prm.trace_kernels -- 0: one-ray-per-thread kernels; 1: instrumented
@@ -3252,8 +3356,8 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
         HIPCHK(hipMemcpyAsync(hit_out, Wv.vis, n, hipMemcpyDeviceToHost, c->stream));
     } else {
         SpillArea sp{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
-        if (prod) hipLaunchKernelGGL(k_extend<false>, dim3(c->grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, c->stream, c->S, Wv, 0, sp);
-        else hipLaunchKernelGGL(k_extend<true>, dim3(c->grid_ext), dim3(TRAV_BLOCK), EXT_LDS_BYTES, c->stream, c->S, Wv, 0, sp);
+        const bool wide = c->S.wide != nullptr && c->prm.wide_from == 0;  // the two-level loop ray by ray
+        launch_extend(!prod, false, wide, wide ? c->grid_ext_w : c->grid_ext, c->stream, c->S, Wv, 0, sp);
         (void)hipEventRecord(e1, c->stream);
         HIPCHK(t.ensure(4 * (size_t)n));
         HIPCHK(ob.ensure(4 * (size_t)n));

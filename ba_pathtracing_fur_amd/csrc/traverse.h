@@ -312,6 +312,21 @@ __device__ __forceinline__ void leaf_step_closest(const DevScene& S, const TravR
     cur_next(stk, c);
 }
 
+// leaf_candidate without the barycentrics (the production closest-hit loops):
+// the leaf's best t is its shrunk window tMax whenever a candidate was
+// accepted (sl >= 0), and u, v are recomputed from the hit (tri_uv).
+__device__ __forceinline__ void leaf_candidate_t(float4 p0, float4 p1, float4 p2, float4 p3, int32_t slot,
+                                                 const Ray& r, float& tMax, int32_t& sl) {
+    float t, u, v;
+    bool ok;
+    if (is_tri(p0)) ok = tri_test(p0, p1, p2, r, 0.0f, tMax, t, u, v);
+    else ok = cone_closest(p0, p1, p2, p3, r, 0.0f, tMax, t);
+    if (ok) {
+        sl = slot;
+        tMax = t;
+    }
+}
+
 __device__ __forceinline__ bool any_candidate(float4 p0, float4 p1, float4 p2, float4 p3, const Ray& r,
                                               float tMaxRay) {
     if (is_tri(p0)) {
@@ -490,16 +505,14 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
                 return true;
             }
         } else {
-            leaf_candidate(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.tl, lf.sl, lf.lu, lf.lv);
+            leaf_candidate_t(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.sl);
         }
         ++lf.slot;
         --lf.left;
         if (lf.left == 0u) {
-            if (!ANY && lf.sl >= 0 && lf.tl < h.t) {
-                h.t = lf.tl;
+            if (!ANY && lf.sl >= 0 && lf.tmax < h.t) {  // the leaf's best t is its window (leaf_candidate_t)
+                h.t = lf.tmax;
                 h.slot = lf.sl;
-                h.u = lf.lu;
-                h.v = lf.lv;
             }
             need_pop = true;
         }
@@ -539,6 +552,187 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
         stk.pop(eref, et0, et1);
         const float tlimit = ANY ? tmax_any : h.t;
         if (et1 < 0.0f || et0 > tlimit) {
+            if (STATS) st.pruned++;
+            mode = M_POP;
+        } else {
+            have = true;
+        }
+    }
+    if (have) take_entry<STATS>(S, eref, et0, et1, mode, c, lf, st);
+    return false;
+}
+
+// ---- two-level node records (k_extend) ----------------------------------------------------
+// The wide record of interior node X (one 128-B line, `DevScene::wide`, same
+// index as X's 64-B record) holds, for each child C of X, either the boxes and
+// refs of C's two children (C interior) or C's own box (C a leaf):
+//   [0..2]  g0, g1 boxes   (child 1's children, or child 1's box in g0)
+//   [3..5]  g2, g3 boxes   (the same for child 2)
+//   [6]     ref c1, ref c2, ref g0, ref g1      [7] ref g2, ref g3, 0, 0
+// Box k is (mn.xyz, mx.xyz) packed like DevNode's left/right pair.  C's own
+// box is not stored: KIRK's node box is the union (std::min / std::max) of its
+// objects' bounds (CPU_BVH.cpp:113-118), so it equals the union of its two
+// children's boxes bit for bit -- checked for every node when the records are
+// built (k_wide_records); a scene where it fails keeps the 64-B loop.  For a ray
+// with finite origin and inverse direction, every per-axis plane distance
+// (b - o) * inv is monotone in b, so C's per-axis entry / exit are exactly the
+// min / max of its children's (both boxes ordered, mn <= mx, also checked), and
+// slab_fast on C's box follows without C's bounds.
+//
+// One fetch then does the work of two of KIRK's levels on the near path: X's
+// two child boxes (prune, near-first order), and if the near child N is
+// interior, N's two child boxes as KIRK would test them on entering N (same
+// h.t: nothing between those tests can change it).  The far child is pushed
+// below N's far child, so the pops come in KIRK's order; every entry is still
+// prune-tested when KIRK would pop it, and KIRK's visit counts are kept (N
+// counts as a visit in the iteration that expands it).
+struct WBox {
+    float e0, e1, e2, x0, x1, x2;  // per-axis entry / exit (fast slab form)
+};
+__device__ __forceinline__ WBox wbox_fast(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                          const TravRay& tr) {
+    const float ax = (mnx - tr.r.o.x) * tr.inv.x, bx = (mxx - tr.r.o.x) * tr.inv.x;
+    const float ay = (mny - tr.r.o.y) * tr.inv.y, by = (mxy - tr.r.o.y) * tr.inv.y;
+    const float az = (mnz - tr.r.o.z) * tr.inv.z, bz = (mxz - tr.r.o.z) * tr.inv.z;
+    return WBox{fminf(ax, bx), fminf(ay, by), fminf(az, bz), fmaxf(ax, bx), fmaxf(ay, by), fmaxf(az, bz)};
+}
+__device__ __forceinline__ WBox wbox_union(const WBox& a, const WBox& b) {
+    return WBox{fminf(a.e0, b.e0), fminf(a.e1, b.e1), fminf(a.e2, b.e2),
+                fmaxf(a.x0, b.x0), fmaxf(a.x1, b.x1), fmaxf(a.x2, b.x2)};
+}
+__device__ __forceinline__ bool wbox_t(const WBox& w, float& t0, float& t1) {
+    t0 = fmaxf(fmaxf(w.e0, w.e1), w.e2);
+    t1 = fminf(fminf(w.x0, w.x1), w.x2);
+    return t0 <= t1;
+}
+__device__ __forceinline__ float wmin(float a, float b) { return (b < a) ? b : a; }  // std::min, as the build
+__device__ __forceinline__ float wmax(float a, float b) { return (a < b) ? b : a; }  // std::max
+
+// One wave iteration of one lane over wide records (closest hit only; the
+// leaf branch is iter2's).  Returns true when the ray is finished.
+template <bool STATS, class Stack>
+__device__ __forceinline__ bool iterw(const DevScene& S, const TravRay& tr, Hit& h, Stack& stk, uint32_t& mode,
+                                      Cur& c, LeafCur& lf, TravStats& st) {
+    // A wave with a ray whose origin or inverse direction is not finite on
+    // every axis (an exactly axis-parallel direction) runs this iteration as
+    // the one-level step on the 64-B records (same entries, same stack): the
+    // composed slab needs the fast form's monotone plane distances.
+    if (__ballot(!tr.fin) != 0ull) {
+        bool occ_unused;
+        return iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused);
+    }
+    const bool in_leaf = mode == M_LEAF;
+    const bool node = mode == M_NODE;
+    const bool fetch = in_leaf || node;
+    const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : S.wide + 8 * (size_t)c.ref;
+    float4 q0, q1, q2, q3, q4, q5, q6, q7;
+    if (fetch) {
+        q0 = p[0];
+        q1 = p[1];
+        q2 = p[2];
+        q3 = p[3];
+    }
+    if (node) {
+        q4 = p[4];
+        q5 = p[5];
+        q6 = p[6];
+        q7 = p[7];
+    }
+    if (fetch) {
+        pin(q0); pin(q1); pin(q2); pin(q3);
+    }
+    if (node) {
+        pin(q4); pin(q5); pin(q6); pin(q7);
+    }
+    bool need_pop = mode == M_POP;
+    bool have = false;
+    uint32_t eref = 0u;
+    float et0 = 0.0f, et1 = 0.0f;
+    bool push1 = false, push2 = false;
+    uint32_t p1ref = 0u, p2ref = 0u;
+    float p1t0 = 0.0f, p1t1 = 0.0f, p2t0 = 0.0f, p2t1 = 0.0f;
+    if (in_leaf) {
+        if (STATS) st.prims++;
+        leaf_candidate_t(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.sl);
+        ++lf.slot;
+        --lf.left;
+        if (lf.left == 0u) {
+            if (lf.sl >= 0 && lf.tmax < h.t) {
+                h.t = lf.tmax;
+                h.slot = lf.sl;
+            }
+            need_pop = true;
+        }
+    } else if (node) {
+        if (STATS) st.nodes++;
+        const float tlimit = h.t;
+        const uint32_t c1 = __float_as_uint(q6.x), c2 = __float_as_uint(q6.y);
+        const bool i1 = !ref_leaf(c1), i2 = !ref_leaf(c2);
+        float gt0[4], gt1[4], At0, At1, Bt0, Bt1;
+        bool gh[4], hA, hB;
+        {
+            const WBox w0 = wbox_fast(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, tr);
+            const WBox w1 = wbox_fast(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, tr);
+            const WBox w2 = wbox_fast(q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, tr);
+            const WBox w3 = wbox_fast(q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, tr);
+            gh[0] = wbox_t(w0, gt0[0], gt1[0]);
+            gh[1] = wbox_t(w1, gt0[1], gt1[1]);
+            gh[2] = wbox_t(w2, gt0[2], gt1[2]);
+            gh[3] = wbox_t(w3, gt0[3], gt1[3]);
+            const WBox wa = wbox_union(w0, w1), wb = wbox_union(w2, w3);
+            float ua0, ua1, ub0, ub1;
+            const bool ua = wbox_t(wa, ua0, ua1), ub = wbox_t(wb, ub0, ub1);
+            hA = i1 ? ua : gh[0];
+            At0 = i1 ? ua0 : gt0[0];
+            At1 = i1 ? ua1 : gt1[0];
+            hB = i2 ? ub : gh[2];
+            Bt0 = i2 ? ub0 : gt0[2];
+            Bt1 = i2 ? ub1 : gt1[2];
+        }
+        hA = hA && !(At1 < 0.0f || At0 > tlimit);
+        hB = hB && !(Bt1 < 0.0f || Bt0 > tlimit);
+        const bool nearA = hA && (!hB || At0 < Bt0);  // KIRK: left first iff l0 < r0 (ties: right)
+        const bool have_near = hA || hB;
+        const uint32_t nref = nearA ? c1 : c2;
+        const bool nint = have_near && !ref_leaf(nref);
+        const bool fhit = hA && hB;
+        const uint32_t fref = nearA ? c2 : c1;
+        const float f0 = nearA ? Bt0 : At0, f1 = nearA ? Bt1 : At1;
+        // the near child's children (tested as KIRK enters it, with the same h.t)
+        const uint32_t glref = __float_as_uint(nearA ? q6.z : q7.x), grref = __float_as_uint(nearA ? q6.w : q7.y);
+        const float gl0 = nearA ? gt0[0] : gt0[2], gl1 = nearA ? gt1[0] : gt1[2];
+        const float gr0 = nearA ? gt0[1] : gt0[3], gr1 = nearA ? gt1[1] : gt1[3];
+        const bool hl = nint && (nearA ? gh[0] : gh[2]) && !(gl1 < 0.0f || gl0 > tlimit);
+        const bool hr = nint && (nearA ? gh[1] : gh[3]) && !(gr1 < 0.0f || gr0 > tlimit);
+        const bool gnl = hl && (!hr || gl0 < gr0);
+        const bool have_g = hl || hr;
+        if (STATS && nint) st.nodes++;  // KIRK's visit of the near child
+        const uint32_t gref = gnl ? glref : grref;
+        const float g0 = gnl ? gl0 : gr0, g1 = gnl ? gl1 : gr1;
+        // next entry: the near child (a leaf), else its near child, else the far child
+        eref = !nint ? nref : (have_g ? gref : fref);
+        et0 = !nint ? (nearA ? At0 : Bt0) : (have_g ? g0 : f0);
+        et1 = !nint ? (nearA ? At1 : Bt1) : (have_g ? g1 : f1);
+        have = have_near && (!nint || have_g || fhit);
+        need_pop = !have;
+        push1 = fhit && (!nint || have_g);
+        p1ref = fref;
+        p1t0 = f0;
+        p1t1 = f1;
+        push2 = hl && hr;
+        p2ref = gnl ? grref : glref;
+        p2t0 = gnl ? gr0 : gl0;
+        p2t1 = gnl ? gr1 : gl1;
+    }
+    if (push1) stk.push(p1ref, p1t0, p1t1);
+    if (push2) stk.push(p2ref, p2t0, p2t1);
+    if (need_pop) {
+        if (stk.empty()) {
+            mode = M_IDLE;
+            return true;
+        }
+        stk.pop(eref, et0, et1);
+        if (et1 < 0.0f || et0 > h.t) {
             if (STATS) st.pruned++;
             mode = M_POP;
         } else {

@@ -121,7 +121,8 @@ class CtxParams(ctypes.Structure):
     """khp_ctx_params (ABI 7): scheduling knobs of a context; no value changes any result."""
     _fields_ = [("fuse_frames", c_uint32), ("frames_in_flight", c_uint32), ("chunk_paths", c_uint64),
                 ("heavy_iters", c_uint32), ("dump_bounce", c_int32), ("trace_kernels", c_uint32),
-                ("shade_order", c_uint32), ("serial_stages", c_uint32), ("path_order", c_uint32)]
+                ("shade_order", c_uint32), ("serial_stages", c_uint32), ("path_order", c_uint32),
+                ("wide_from", c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

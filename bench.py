@@ -94,6 +94,8 @@ def parse():
     ap.add_argument("--shade-order", type=int, default=None, help="khp_ctx_params.shade_order (1: hits sorted by shading class)")
     ap.add_argument("--path-order", type=int, default=None,
                     help="khp_ctx_params.path_order (0: frame-major fused chunks, 1: pixel-major)")
+    ap.add_argument("--wide-from", type=int, default=None,
+                    help="khp_ctx_params.wide_from (first bounce on two-level node records; >= depth: never)")
     ap.add_argument("--heavy-iters", type=int, default=None,
                     help="khp_ctx_params.heavy_iters (longest-first queue threshold, traversal iterations)")
     ap.add_argument("--bdpt", default=None, metavar="PATHS,VERTICES",
@@ -293,7 +295,8 @@ def main():
     frame = ShardedFrame(ctx, rank, world, dist, tile=args.tile)
     knobs = {k: v for k, v in (("fuse_frames", args.fuse), ("chunk_paths", args.chunk_paths),
                                ("frames_in_flight", args.frames_in_flight), ("shade_order", args.shade_order),
-                               ("heavy_iters", args.heavy_iters), ("path_order", args.path_order))
+                               ("heavy_iters", args.heavy_iters), ("path_order", args.path_order),
+                               ("wide_from", args.wide_from))
              if v is not None}
     if knobs:
         ctx.set_params(**knobs)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 9
+#define KHP_ABI_VERSION 10
 
 typedef struct khp_ctx khp_ctx;
 
@@ -294,6 +294,11 @@ typedef struct {
                                     pixels x samples form one block); 1 (default): pixel-major (all fused
                                     frames' samples of one pixel are adjacent paths, so a wave traces one
                                     pixel of 8 frames at 8 spp).  Measured in DESIGN.md §5a            */
+    uint32_t wide_from;          /* ABI 10: the first bounce whose closest-hit traversal runs on two-level
+                                    node records (one 128-B record per step: a node's child boxes and the
+                                    near child's own, KIRK's order and counts kept); earlier bounces use the
+                                    64-B records.  Default 2 (measured); >= depth: never.
+                                    Batch queries with trace_kernels use them iff wide_from == 0      */
 } khp_ctx_params;
 
 /* ---- context --------------------------------------------------------------- */

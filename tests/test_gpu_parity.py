@@ -521,13 +521,16 @@ def test_cpp_host_program_matches(hip_ctx, tmp_path):
     assert np.array_equal(img.view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.parametrize("wide", ["0", "2"])
 @pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("name,kw", [("config2", dict(n_strands=3000)), ("config5", dict(n_strands=2000,
                                                                                           torus_grid=30))])
-def test_production_traversal_kernels_ray_by_ray(hip_ctx, mode, name, kw):
+def test_production_traversal_kernels_ray_by_ray(hip_ctx, mode, name, kw, wide):
     """khp_ctx_params.trace_kernels routes the batch queries through the renderer's own
     persistent kernels: 1 = instrumented (KIRK's node/candidate visit counts must
-    match the oracle's), 2 = the production build used in timed frames."""
+    match the oracle's), 2 = the production build used in timed frames.  wide_from
+    0: the closest-hit queries run on the two-level node records (traverse.h
+    iterw), 2: on the 64-B records; axis-parallel rays take the one-level step."""
     sd = S.build_config(name, width=32, height=32, **kw)
     hip_ctx.set_scene(sd)
     hip_ctx.build_accel()
@@ -547,9 +550,15 @@ def test_production_traversal_kernels_ray_by_ray(hip_ctx, mode, name, kw):
     orig[120:140, 0] = np.nan   # the any-hit x-slab class (any_hit_x_nan): NaN origin x, finite direction
     orig[140:150, 1] = np.nan
     tmax[150:170] = np.nan
+    # axis-parallel rays (infinite inverse direction components: the slab_sel path)
+    d[170:200] = np.float32([0, 0, 1])
+    d[200:230] = np.float32([0, -1, 0])
+    d[230:260, 0] = 0.0
+    d[230:260] /= np.linalg.norm(d[230:260], axis=1, keepdims=True)
+    d[260:290] = np.float32([-1, 0, 0])
     t0, obj0, uv0, nodes, prims = o.trace_closest(orig, d)
     any0 = o.trace_any(orig, d, tmax)
-    old = hip_ctx.set_params(trace_kernels=int(mode))
+    old = hip_ctx.set_params(trace_kernels=int(mode), wide_from=int(wide))
     try:
         t, obj, uv = hip_ctx.trace_closest(orig, d)
         st = hip_ctx.stats()
@@ -562,3 +571,27 @@ def test_production_traversal_kernels_ray_by_ray(hip_ctx, mode, name, kw):
     assert np.array_equal(a, any0)
     if mode == "1":
         assert (st["node_visits"], st["prim_tests"]) == (nodes, prims)
+
+
+@pytest.mark.parametrize("name,kw,w,h,spp,depth", [CASES[1], CASES[4], CASES[5], CASES[8]],
+                         ids=["config2", "config5", "zoo", "textured"])
+def test_wide_records_frames(hip_ctx, name, kw, w, h, spp, depth):
+    """khp_ctx_params.wide_from: frames whose closest-hit traversal runs on the
+    two-level node records from bounce 0, 1 or never are the oracle's, bit for
+    bit, synchronous and instrumented; KIRK's visit counts do not change."""
+    sd = S.build_config(name, width=w, height=h, **kw)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    want = oracle_ffi.Oracle(sd).render(w, h, spp, depth, threads=16)
+    counts = set()
+    old = hip_ctx.params()
+    try:
+        for wf in (0, 1, 64):
+            hip_ctx.set_params(wide_from=wf)
+            assert_parity(hip_ctx.render(w, h, spp, depth), want, exact=True)
+            assert_parity(hip_ctx.render(w, h, spp, depth, stats=True), want, exact=True)
+            st = hip_ctx.stats()
+            counts.add((st["node_visits"], st["prim_tests"]))
+    finally:
+        hip_ctx.set_params(**old)
+    assert len(counts) == 1
