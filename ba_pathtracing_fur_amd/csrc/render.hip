@@ -262,10 +262,22 @@ constexpr int EXT_WAVES_W = KHP_EXT_WAVES_W;  // k_extend over the two-level rec
 constexpr int EXT_REFILL = KHP_EXT_REFILL;  // k_extend's refill threshold
 constexpr size_t LDS_BYTES = 3 * RING * TRAV_BLOCK * sizeof(uint32_t);
 constexpr size_t EXT_LDS_BYTES = 3 * EXT_RING * TRAV_BLOCK * sizeof(uint32_t);
+// Bounce 0 (camera rays computed in place, k_extend<., true, .>): cache-served and
+// latency-bound, so the 64-B loop (59 VGPRs) runs 8 waves per SIMD there, with
+// 6-entry rings so 32 one-wave blocks fit a CU's LDS.
+#ifndef KHP_CAM_RING
+#define KHP_CAM_RING 6
+#endif
+#ifndef KHP_CAM_WAVES
+#define KHP_CAM_WAVES 8
+#endif
+constexpr int CAM_RING = KHP_CAM_RING;
+constexpr int CAM_WAVES = KHP_CAM_WAVES;
+constexpr size_t CAM_LDS_BYTES = 3 * CAM_RING * TRAV_BLOCK * sizeof(uint32_t);
 template <bool STATS>
 using TravStack = LdsStack<RING, STATS>;
-template <bool STATS>
-using ExtStack = LdsStack<EXT_RING, STATS>;
+template <bool STATS, bool CAM = false>
+using ExtStack = LdsStack<CAM ? CAM_RING : EXT_RING, STATS>;
 
 struct SpillArea {
     int4* base;
@@ -411,10 +423,10 @@ __device__ __forceinline__ void flush_stats(const TravStats& st, const Stack& st
 // the camera ray, computed here instead of loaded.
 // WIDE: the two-level records (S.wide, traverse.h iterw) instead of the 64-B loop.
 template <bool STATS, bool CAM = false, bool WIDE = false>
-__global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : EXT_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
+__global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : CAM ? CAM_WAVES : EXT_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t nf = Wv.cnt->nq[cur], nb = Wv.cnt->nqb[cur];
-    ExtStack<STATS> stk;
+    ExtStack<STATS, CAM> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0, 0};
     TravRay tr;
@@ -494,7 +506,8 @@ __global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : EXT_WAVES) void k_
 static void launch_extend(bool stats, bool cam, bool wide, int grid, hipStream_t s, const DevScene& S, const Wave& W,
                           int cur, SpillArea sp) {
     const dim3 g(grid), b(TRAV_BLOCK);
-#define KHP_EXT(ST, CA, WI) hipLaunchKernelGGL((k_extend<ST, CA, WI>), g, b, EXT_LDS_BYTES, s, S, W, cur, sp)
+#define KHP_EXT(ST, CA, WI) \
+    hipLaunchKernelGGL((k_extend<ST, CA, WI>), g, b, CA ? CAM_LDS_BYTES : EXT_LDS_BYTES, s, S, W, cur, sp)
     if (wide) {
         if (stats) { if (cam) KHP_EXT(true, true, true); else KHP_EXT(true, false, true); }
         else { if (cam) KHP_EXT(false, true, true); else KHP_EXT(false, false, true); }
@@ -1595,8 +1608,8 @@ struct PathSet {
     hipStream_t sA = nullptr, sB = nullptr;
 };
 // Device bytes per path of a PathSet (ensure_wave): 2 x 7 queue columns, hit
-// t/slot/u/v, TF + CK records, heavy flag, 2 x (occlusion flag + 96-B shadow record).
-constexpr size_t PATH_BYTES = 2 * 7 * 4 + 4 * 4 + 5 * 16 + 1 + 2 * (1 + 6 * 16) + 4 + 1;
+// t/slot, TF + CK records, heavy flag, 2 x (occlusion flag + 96-B shadow record).
+constexpr size_t PATH_BYTES = 2 * 7 * 4 + 2 * 4 + 5 * 16 + 1 + 2 * (1 + 6 * 16) + 4 + 1;
 
 #ifndef KHP_MAX_INFLIGHT
 #define KHP_MAX_INFLIGHT 3
@@ -1689,7 +1702,8 @@ struct khp_ctx {
     std::vector<hipEvent_t> ev_pool;
     size_t ev_next = 0;
     std::vector<TimedLaunch> launches;
-    int grid_ext = 0, grid_ext_w = 0, grid_sh = 0, grid_shade = 0;  // grid_ext_w: k_extend on wide records
+    int grid_ext = 0, grid_ext_w = 0, grid_ext_cam = 0, grid_sh = 0, grid_shade = 0;  // k_extend: 64-B, wide, bounce 0
+    int grid_ext_max = 0;  // the k_extend spill columns are sized for the largest grid
     khp_stats st{};
     // rccl gather: pixel lists cached per (W, H, tile, nranks, rank, root)
     uint32_t gather_key[6] = {0, 0, 0, 0, 0, 0};
@@ -2145,7 +2159,14 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<true, false, true>, TRAV_BLOCK, EXT_LDS_BYTES));
     else
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false, false, true>, TRAV_BLOCK, EXT_LDS_BYTES));
-    c->grid_ext_w = std::min(c->grid_ext, std::max(1, nb) * c->n_cu);  // the spill columns are sized by grid_ext
+    c->grid_ext_w = std::max(1, nb) * c->n_cu;
+    nb = 0;
+    if (c->flags & KHP_CTX_STATS)
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<true, true>, TRAV_BLOCK, CAM_LDS_BYTES));
+    else
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_extend<false, true>, TRAV_BLOCK, CAM_LDS_BYTES));
+    c->grid_ext_cam = std::max(1, nb) * c->n_cu;
+    c->grid_ext_max = std::max(c->grid_ext, std::max(c->grid_ext_w, c->grid_ext_cam));
     nb = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, TRAV_BLOCK, LDS_BYTES));
     c->grid_sh = std::max(1, nb) * c->n_cu;
@@ -2183,7 +2204,7 @@ static khp_status ensure_wave(khp_ctx* c, PathSet& w, size_t cap, size_t sh_per_
     HIPCHK(w.cnt.ensure(sizeof(Counters)));
     // traversal-stack spill columns: one per resident lane, STACK_MAX entries deep
     // separate spill columns: k_extend and k_shadow may run at the same time
-    HIPCHK(w.spill.ensure((size_t)c->grid_ext * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
+    HIPCHK(w.spill.ensure((size_t)c->grid_ext_max * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
     HIPCHK(w.spill_sh.ensure((size_t)c->grid_sh * TRAV_BLOCK * STACK_MAX * sizeof(int4)));
     if (!w.sA) {
         HIPCHK(hipStreamCreateWithFlags(&w.sA, hipStreamNonBlocking));
@@ -2499,7 +2520,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     f.nf = nf;
     const int G = async ? F : 1;
     const int grid_ext = std::max(1, c->grid_ext / G), grid_sh = std::max(1, c->grid_sh / G);
-    const int grid_ext_w = std::max(1, c->grid_ext_w / G);
+    const int grid_ext_w = std::max(1, c->grid_ext_w / G), grid_ext_cam = std::max(1, c->grid_ext_cam / G);
     // Chunks: the owned pixels x samples (x fused frames) are cut into chunks
     // of at most chunk_paths() paths, pixel-major; a fused chunk carries all
     // samples of all frames of its pixels.
@@ -2626,7 +2647,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     Wv.bd = BdptDev{bdm ? 1u : 0u, c->bd.light_paths, (uint32_t)c->S.n_lights, c->bd.vertices, c->bd.bias,
                     c->bd.bounce_bias, c->bd.min_pdf, c->bd.image_plane,
                     bdm ? w.lvb.as<float4>() : nullptr};
-    SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
+    SpillArea sp_ext{w.spill.as<int4>(), (uint32_t)c->grid_ext_max * TRAV_BLOCK};
     SpillArea sp_sh{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
     for (uint32_t p0 = 0; p0 < P_all; p0 += P_chunk) {
         const uint32_t P = std::min(P_chunk, P_all - p0);
@@ -2692,7 +2713,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 timed(c, f, 0, true, sA);
                 const bool cam = b == 0 && Wv.cam0;
                 const bool wide = c->S.wide != nullptr && b >= c->prm.wide_from;
-                launch_extend(stats, cam, wide, wide ? grid_ext_w : grid_ext, sA, c->S, Wb, cur, sp_ext);
+                launch_extend(stats, cam, wide, wide ? grid_ext_w : cam ? grid_ext_cam : grid_ext, sA, c->S, Wb, cur,
+                              sp_ext);
                 timed(c, f, 0, false, sA);
                 if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
                 timed(c, f, 1, true, sA);
@@ -3355,7 +3377,7 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(hit_out, Wv.vis, n, hipMemcpyDeviceToHost, c->stream));
     } else {
-        SpillArea sp{w.spill.as<int4>(), (uint32_t)c->grid_ext * TRAV_BLOCK};
+        SpillArea sp{w.spill.as<int4>(), (uint32_t)c->grid_ext_max * TRAV_BLOCK};
         const bool wide = c->S.wide != nullptr && c->prm.wide_from == 0;  // the two-level loop ray by ray
         launch_extend(!prod, false, wide, wide ? c->grid_ext_w : c->grid_ext, c->stream, c->S, Wv, 0, sp);
         (void)hipEventRecord(e1, c->stream);
