@@ -258,7 +258,7 @@ constexpr int EXT_WAVES = KHP_EXT_WAVES;
 #ifndef KHP_EXT_WAVES_W
 #define KHP_EXT_WAVES_W 6
 #endif
-constexpr int EXT_WAVES_W = KHP_EXT_WAVES_W;  // k_extend over the two-level records (32 B more per record in flight)
+constexpr int EXT_WAVES_W = KHP_EXT_WAVES_W;  // k_extend over the two-level records (80 VGPRs: 6 waves)
 constexpr int EXT_REFILL = KHP_EXT_REFILL;  // k_extend's refill threshold
 constexpr size_t LDS_BYTES = 3 * RING * TRAV_BLOCK * sizeof(uint32_t);
 constexpr size_t EXT_LDS_BYTES = 3 * EXT_RING * TRAV_BLOCK * sizeof(uint32_t);
@@ -307,10 +307,10 @@ static_assert(NSEG <= KHP_MAX_SEG, "claim cursors");
 #endif
 // Two-level node records for k_extend (traverse.h iterw); 0: the 64-B loop only.
 // KHP_WIDE_FROM: the default first bounce that uses them (khp_ctx_params.wide_from,
-// ABI 10).  The camera and first
-// secondary bounces are cache-served and issue-bound, where the two-level step
-// (more VALU per iteration, 5 instead of 6 waves per SIMD) loses; the deep
-// bounces are bound by line fetches, which it cuts by a third.
+// ABI 10).  The camera and first secondary bounces are cache-served and
+// issue-bound, where the two-level step (4 boxes per step, 80 VGPRs) loses;
+// from bounce 2 line fetches bound the loop, and it takes a third fewer steps
+// (DESIGN.md §4).
 #ifndef KHP_WIDE
 #define KHP_WIDE 1
 #endif

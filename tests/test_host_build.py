@@ -117,3 +117,37 @@ def test_camera_setup_validates():
     rc = lib.khp_camera_setup(N.fptr(p), N.fptr(np.float32([0, 0, -1])), N.fptr(up), 0.036, 0.024, 0.0415, 0, 16,
                               cam)
     assert rc == N.KHP_EINVAL
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("config2", dict(width=32, height=32, n_strands=2000)),
+    ("config3", dict(width=32, height=32, n_strands=3000)),
+    ("config5", dict(width=32, height=32, n_strands=1500, torus_grid=20, glass_subdiv=2)),
+    ("zoo", dict(width=32, height=32, n_strands=300)),
+])
+def test_node_boxes_are_child_unions(name, kw):
+    """The premise of k_extend's two-level records (traverse.h iterw): in KIRK's
+    build (the oracle's restatement of CPU_BVH.cpp) every interior node's box is
+    the std::min / std::max union of its two children's boxes, bit for bit, and
+    every box is ordered (min <= max), so a child's slab follows from its own
+    children's plane distances.  The device checks the same per node when it
+    builds the records (k_wide_records)."""
+    sd = S.build_config(name, **kw)
+    boxes, first, count, ids, depth = oracle_ffi.Oracle(sd).bvh()
+    boxes = np.ascontiguousarray(boxes, np.float32)
+    n = len(count)
+    assert np.all(boxes[:, :3] <= boxes[:, 3:])
+    # preorder: an interior node's left child follows it, its right child follows the left subtree
+    size = np.ones(n, np.int64)
+    right = np.full(n, -1, np.int64)
+    for i in range(n - 1, -1, -1):
+        if count[i] == 0:
+            r = i + 1 + size[i + 1]
+            right[i] = r
+            size[i] = 1 + size[i + 1] + size[r]
+    interior = np.nonzero(count == 0)[0]
+    L, R = boxes[interior + 1], boxes[right[interior]]
+    union = np.concatenate([np.where(R[:, :3] < L[:, :3], R[:, :3], L[:, :3]),
+                            np.where(L[:, 3:] < R[:, 3:], R[:, 3:], L[:, 3:])], axis=1)
+    assert len(interior) > 0
+    assert _same_bits(union, boxes[interior])
