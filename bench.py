@@ -482,7 +482,7 @@ def main():
         "isolated": isolated,
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_extend (closest-hit BVH2 traversal)",
+            "kernel": "k_extend (closest-hit traversal: bounce-0, 64-B and two-level instances together)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",

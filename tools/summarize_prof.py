@@ -16,9 +16,18 @@ lines = [f"# rocprofv3 summary {tag}", ""]
 stats = os.path.join(src, "trace", "run_kernel_stats.csv")
 if os.path.exists(stats):
     lines += ["## kernel trace (--kernel-trace --stats)", "", "| kernel | calls | total ms | avg ms | % |", "|---|---|---|---|---|"]
+    ext_calls, ext_ns = 0, 0.0
     for r in csv.DictReader(open(stats)):
         lines.append(f"| {r['Name'][:60]} | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.2f} | "
                      f"{float(r['AverageNs'])/1e6:.3f} | {float(r['Percentage']):.1f} |")
+        if r["Name"].startswith("void k_extend<false"):
+            ext_calls += int(r["Calls"])
+            ext_ns += float(r["TotalDurationNs"])
+    if ext_calls:
+        # round 3: k_extend<STATS, CAM, WIDE> -- bounce 0 (camera rays in place), the 64-B loop
+        # and the two-level loop are separate instances of one kernel; their launches together
+        lines.append(f"| k_extend<false, *, *> (all uninstrumented instances) | {ext_calls} | {ext_ns/1e6:.2f} | "
+                     f"{ext_ns/1e6/ext_calls:.3f} | |")
     lines.append("")
 pmc = collections.defaultdict(dict)
 for p in ["fetch", "write", "sq", "tcc", "lat", "ea", "l1"]:
@@ -26,7 +35,10 @@ for p in ["fetch", "write", "sq", "tcc", "lat", "ea", "l1"]:
     if not os.path.exists(f):
         continue
     for r in csv.DictReader(open(f)):
-        key = (r["Kernel_Name"].split("(")[0].replace("void ", ""), p, int(r["Dispatch_Id"]))
+        kn = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        if kn.startswith("k_extend<false"):  # every uninstrumented instance (bounce 0, 64-B, two-level)
+            kn = "k_extend<false>"
+        key = (kn, p, int(r["Dispatch_Id"]))
         pmc[key][r["Counter_Name"]] = float(r["Counter_Value"])
         pmc[key]["dur_ms"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         pmc[key]["scratch"] = r.get("Scratch_Size"); pmc[key]["vgpr"] = r.get("VGPR_Count"); pmc[key]["lds"] = r.get("LDS_Block_Size")
