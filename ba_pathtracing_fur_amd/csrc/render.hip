@@ -250,9 +250,15 @@ __global__ void k_prep(Counters* c, ShadowQ* q, int cur) {
 #ifndef KHP_EXT_REFILL
 #define KHP_EXT_REFILL 24
 #endif
-constexpr int RING = 8;        // LDS ring entries per lane (3 x 4 B each), k_shadow
-constexpr int REFILL = 24;     // refill when >= REFILL lanes are idle
-constexpr int TRAV_WAVES = 6;  // __launch_bounds__ waves per SIMD, k_shadow
+#ifndef KHP_SH_RING
+#define KHP_SH_RING 8
+#endif
+#ifndef KHP_SH_WAVES
+#define KHP_SH_WAVES 6
+#endif
+constexpr int RING = KHP_SH_RING;         // LDS ring entries per lane (3 x 4 B each), k_shadow
+constexpr int REFILL = 24;                // refill when >= REFILL lanes are idle
+constexpr int TRAV_WAVES = KHP_SH_WAVES;  // __launch_bounds__ waves per SIMD, k_shadow
 constexpr int EXT_RING = KHP_EXT_RING;    // the same for k_extend
 constexpr int EXT_WAVES = KHP_EXT_WAVES;
 #ifndef KHP_EXT_WAVES_W
