@@ -265,7 +265,17 @@ constexpr int EXT_WAVES = KHP_EXT_WAVES;
 #define KHP_EXT_WAVES_W 6
 #endif
 constexpr int EXT_WAVES_W = KHP_EXT_WAVES_W;  // k_extend over the two-level records (80 VGPRs: 6 waves)
-constexpr int EXT_REFILL = KHP_EXT_REFILL;  // k_extend's refill threshold
+// k_extend's refill threshold per instance (bounce 0 / 64-B loop / two-level
+// loop), default KHP_EXT_REFILL for each; 16 and 32 measured for each
+#ifndef KHP_REFILL_CAM
+#define KHP_REFILL_CAM KHP_EXT_REFILL
+#endif
+#ifndef KHP_REFILL_NARROW
+#define KHP_REFILL_NARROW KHP_EXT_REFILL
+#endif
+#ifndef KHP_REFILL_WIDE
+#define KHP_REFILL_WIDE KHP_EXT_REFILL
+#endif
 constexpr size_t LDS_BYTES = 3 * RING * TRAV_BLOCK * sizeof(uint32_t);
 constexpr size_t EXT_LDS_BYTES = 3 * EXT_RING * TRAV_BLOCK * sizeof(uint32_t);
 // Bounce 0 (camera rays computed in place, k_extend<., true, .>): cache-served and
@@ -445,9 +455,10 @@ __global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : CAM ? CAM_WAVES : 
     uint32_t it = 0;  // this lane's iterations on its current ray (longest-first queues)
     Claimer cl;
     cl.init(Wv.cnt->fetch_ext, nf, nb, Wv.cap);
+    constexpr int refill = WIDE ? KHP_REFILL_WIDE : CAM ? KHP_REFILL_CAM : KHP_REFILL_NARROW;
     for (;;) {
         unsigned long long idle = __ballot(!has);
-        if (!exhausted && __popcll(idle) >= EXT_REFILL) {
+        if (!exhausted && __popcll(idle) >= refill) {
             uint32_t my;
             const bool got = cl.claim(idle, my, exhausted);
             if (!has && got && cl.phys(my, idx)) {
@@ -500,7 +511,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : CAM ? CAM_WAVES : 
                 }
             }
             act = __ballot(has);
-            if (act == 0 || (!exhausted && 64 - __popcll(act) >= EXT_REFILL)) break;
+            if (act == 0 || (!exhausted && 64 - __popcll(act) >= refill)) break;
         }
     }
     if (STATS)
@@ -869,8 +880,11 @@ __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3,
 
 // TEX: the scene has textured materials or an environment map (a separate
 // instantiation, so untextured scenes keep k_shade's registers).
+#ifndef KHP_SHADE_WAVES
+#define KHP_SHADE_WAVES 1   // min waves per SIMD for k_shade's register budget (1: unconstrained)
+#endif
 template <bool TEX, bool BD>
-__global__ __launch_bounds__(256) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
+__global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
     const uint32_t nf = Wv.cnt->nq[cur], n = nf + Wv.cnt->nqb[cur];
     const int nxt = cur ^ 1;
     const bool last = bounce + 1 >= Wv.depth;
