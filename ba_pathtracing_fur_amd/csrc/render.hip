@@ -333,6 +333,10 @@ static_assert(NSEG <= KHP_MAX_SEG, "claim cursors");
 #ifndef KHP_WIDE_FROM
 #define KHP_WIDE_FROM 2   // default of khp_ctx_params.wide_from
 #endif
+// The shadow stage (any hit) of bounce b uses them from max(wide_from, this).
+#ifndef KHP_WIDE_SH_FROM
+#define KHP_WIDE_SH_FROM 2
+#endif
 constexpr uint32_t CB_LOG = KHP_CLAIM_BLOCK_LOG2;
 constexpr uint32_t CB_MASK = (1u << CB_LOG) - 1u;
 struct Claimer {
@@ -498,7 +502,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : CAM ? CAM_WAVES : 
             if (has) {
                 bool occ_unused;
                 ++it;
-                const bool fin = WIDE ? iterw<STATS>(S, tr, h, stk, mode, c, lf, st)
+                const bool fin = WIDE ? iterw<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused)
                                       : iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused);
                 if (fin) {
                     // the output addresses are formed here, not kept live through the loop
@@ -1226,7 +1230,8 @@ __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv, int 
     }
 }
 
-template <bool STATS>
+// WIDE: the two-level records (traverse.h iterw) instead of the 64-B loop.
+template <bool STATS, bool WIDE = false>
 __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t nf = Wv.shq->nsh, nb = Wv.shq->nshb;
@@ -1280,7 +1285,9 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, W
             if (has) {
                 bool occ = false;
                 Hit hu_{0.0f, -1, 0.0f, 0.0f};
-                if (iter2<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ)) {
+                const bool fin = WIDE ? iterw<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ)
+                                      : iter2<true, STATS>(S, tr, hu_, tmax, stk, mode, c, lf, st, occ);
+                if (fin) {
                     Wv.vis[idx] = occ ? 1 : 0;
                     has = false;
                 }
@@ -1292,6 +1299,18 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, W
     if (STATS)
         flush_stats(st, stk, wit, wbusy, &Wv.cnt->sh_node_visits, &Wv.cnt->sh_prim_tests, &Wv.cnt->sh_pruned,
                     &Wv.cnt->sh_iters, &Wv.cnt->sh_lanes_busy, &Wv.cnt->spills);
+}
+
+// Host-side launch of the k_shadow instance for (stats, wide records).
+static void launch_shadow(bool stats, bool wide, int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp) {
+    const dim3 g(grid), b(TRAV_BLOCK);
+    if (wide) {
+        if (stats) hipLaunchKernelGGL((k_shadow<true, true>), g, b, LDS_BYTES, s, S, W, sp);
+        else hipLaunchKernelGGL((k_shadow<false, true>), g, b, LDS_BYTES, s, S, W, sp);
+    } else {
+        if (stats) hipLaunchKernelGGL((k_shadow<true, false>), g, b, LDS_BYTES, s, S, W, sp);
+        else hipLaunchKernelGGL((k_shadow<false, false>), g, b, LDS_BYTES, s, S, W, sp);
+    }
 }
 
 // ---- accumulate: PathTracer::drawTexture running mean (CPU_PathTracer.cpp:61-90) -------
@@ -1723,6 +1742,7 @@ struct khp_ctx {
     size_t ev_next = 0;
     std::vector<TimedLaunch> launches;
     int grid_ext = 0, grid_ext_w = 0, grid_ext_cam = 0, grid_sh = 0, grid_shade = 0;  // k_extend: 64-B, wide, bounce 0
+    int grid_sh_w = 0;     // k_shadow on the two-level records
     int grid_ext_max = 0;  // the k_extend spill columns are sized for the largest grid
     khp_stats st{};
     // rccl gather: pixel lists cached per (W, H, tile, nranks, rank, root)
@@ -2191,6 +2211,9 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false>, TRAV_BLOCK, LDS_BYTES));
     c->grid_sh = std::max(1, nb) * c->n_cu;
     nb = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false, true>, TRAV_BLOCK, LDS_BYTES));
+    c->grid_sh_w = std::min(c->grid_sh, std::max(1, nb) * c->n_cu);  // the spill columns are sized by grid_sh
+    nb = 0;
     if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<true, false>), 256, 0));
     else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false>), 256, 0));
     c->grid_shade = std::max(1, nb) * c->n_cu;
@@ -2540,6 +2563,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     f.nf = nf;
     const int G = async ? F : 1;
     const int grid_ext = std::max(1, c->grid_ext / G), grid_sh = std::max(1, c->grid_sh / G);
+    const int grid_sh_w = std::max(1, c->grid_sh_w / G);
     const int grid_ext_w = std::max(1, c->grid_ext_w / G), grid_ext_cam = std::max(1, c->grid_ext_cam / G);
     // Chunks: the owned pixels x samples (x fused frames) are cut into chunks
     // of at most chunk_paths() paths, pixel-major; a fused chunk carries all
@@ -2698,10 +2722,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 HIPCHK(hipMemsetAsync(Wi.shq, 0, sizeof(ShadowQ), sA));
                 hipLaunchKernelGGL(k_img_connect, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wi);
                 timed(c, f, 2, true, sA);
-                if (stats)
-                    hipLaunchKernelGGL(k_shadow<true>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wi, sp_sh);
-                else
-                    hipLaunchKernelGGL(k_shadow<false>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sA, c->S, Wi, sp_sh);
+                launch_shadow(stats, false, grid_sh, sA, c->S, Wi, sp_sh);
                 timed(c, f, 2, false, sA);
                 timed(c, f, 4, true, sA);
                 hipLaunchKernelGGL(k_shadow_finish<true>, dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wi, 0);
@@ -2775,10 +2796,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     }
                 }
                 timed(c, f, 2, true, sB);
-                if (stats)
-                    hipLaunchKernelGGL(k_shadow<true>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sB, c->S, Wb, sp_sh);
-                else
-                    hipLaunchKernelGGL(k_shadow<false>, dim3(grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, sB, c->S, Wb, sp_sh);
+                const bool wide_sh = c->S.wide != nullptr && b >= std::max(c->prm.wide_from, (uint32_t)KHP_WIDE_SH_FROM);
+                launch_shadow(stats, wide_sh, wide_sh ? grid_sh_w : grid_sh, sB, c->S, Wb, sp_sh);
                 timed(c, f, 2, false, sB);
                 timed(c, f, 4, true, sB);   // shadow stage = any-hit traversal + finish
                 if (bdm) hipLaunchKernelGGL(k_shadow_finish<true>, dim3(c->grid_shade), dim3(256), 0, sB, c->S, Wb, cur ^ 1);
@@ -3391,8 +3410,8 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
     (void)hipEventRecord(e0, c->stream);
     if (shadow) {
         SpillArea sp{w.spill_sh.as<int4>(), (uint32_t)c->grid_sh * TRAV_BLOCK};
-        if (prod) hipLaunchKernelGGL(k_shadow<false>, dim3(c->grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, c->stream, c->S, Wv, sp);
-        else hipLaunchKernelGGL(k_shadow<true>, dim3(c->grid_sh), dim3(TRAV_BLOCK), LDS_BYTES, c->stream, c->S, Wv, sp);
+        const bool wide = c->S.wide != nullptr && c->prm.wide_from == 0;  // the two-level any-hit loop ray by ray
+        launch_shadow(!prod, wide, wide ? c->grid_sh_w : c->grid_sh, c->stream, c->S, Wv, sp);
         (void)hipEventRecord(e1, c->stream);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(hit_out, Wv.vis, n, hipMemcpyDeviceToHost, c->stream));

@@ -608,19 +608,19 @@ __device__ __forceinline__ bool wbox_t(const WBox& w, float& t0, float& t1) {
 __device__ __forceinline__ float wmin(float a, float b) { return (b < a) ? b : a; }  // std::min, as the build
 __device__ __forceinline__ float wmax(float a, float b) { return (a < b) ? b : a; }  // std::max
 
-// One wave iteration of one lane over wide records (closest hit only; the
-// leaf branch is iter2's).  Returns true when the ray is finished.
-template <bool STATS, class Stack>
-__device__ __forceinline__ bool iterw(const DevScene& S, const TravRay& tr, Hit& h, Stack& stk, uint32_t& mode,
-                                      Cur& c, LeafCur& lf, TravStats& st) {
+// One wave iteration of one lane over wide records; the leaf branch is
+// iter2's.  ANY: any hit with the fixed limit tmax_any (the ray's tMax; KIRK's
+// any-hit walk has the same near-first order and prune test,
+// CPU_BVH.cpp:211-265), else closest hit with tlimit = h.t.  Returns true when
+// the ray is finished; for ANY, `occluded` tells the result.
+template <bool ANY, bool STATS, class Stack>
+__device__ __forceinline__ bool iterw(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
+                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
     // A wave with a ray whose origin or inverse direction is not finite on
     // every axis (an exactly axis-parallel direction) runs this iteration as
     // the one-level step on the 64-B records (same entries, same stack): the
     // composed slab needs the fast form's monotone plane distances.
-    if (__ballot(!tr.fin) != 0ull) {
-        bool occ_unused;
-        return iter2<false, STATS>(S, tr, h, 0.0f, stk, mode, c, lf, st, occ_unused);
-    }
+    if (__ballot(!tr.fin) != 0ull) return iter2<ANY, STATS>(S, tr, h, tmax_any, stk, mode, c, lf, st, occluded);
     const bool in_leaf = mode == M_LEAF;
     const bool node = mode == M_NODE;
     const bool fetch = in_leaf || node;
@@ -653,11 +653,18 @@ __device__ __forceinline__ bool iterw(const DevScene& S, const TravRay& tr, Hit&
     float p1t0 = 0.0f, p1t1 = 0.0f, p2t0 = 0.0f, p2t1 = 0.0f;
     if (in_leaf) {
         if (STATS) st.prims++;
-        leaf_candidate_t(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.sl);
+        if (ANY) {
+            if (any_candidate(q0, q1, q2, q3, tr.r, tmax_any)) {
+                occluded = true;
+                return true;
+            }
+        } else {
+            leaf_candidate_t(q0, q1, q2, q3, (int32_t)lf.slot, tr.r, lf.tmax, lf.sl);
+        }
         ++lf.slot;
         --lf.left;
         if (lf.left == 0u) {
-            if (lf.sl >= 0 && lf.tmax < h.t) {
+            if (!ANY && lf.sl >= 0 && lf.tmax < h.t) {
                 h.t = lf.tmax;
                 h.slot = lf.sl;
             }
@@ -665,7 +672,7 @@ __device__ __forceinline__ bool iterw(const DevScene& S, const TravRay& tr, Hit&
         }
     } else if (node) {
         if (STATS) st.nodes++;
-        const float tlimit = h.t;
+        const float tlimit = ANY ? tmax_any : h.t;
         const uint32_t c1 = __float_as_uint(q6.x), c2 = __float_as_uint(q6.y);
         const bool i1 = !ref_leaf(c1), i2 = !ref_leaf(c2);
         float gt0[4], gt1[4], At0, At1, Bt0, Bt1;
@@ -729,10 +736,11 @@ __device__ __forceinline__ bool iterw(const DevScene& S, const TravRay& tr, Hit&
     if (need_pop) {
         if (stk.empty()) {
             mode = M_IDLE;
+            occluded = false;
             return true;
         }
         stk.pop(eref, et0, et1);
-        if (et1 < 0.0f || et0 > h.t) {
+        if (et1 < 0.0f || et0 > (ANY ? tmax_any : h.t)) {
             if (STATS) st.pruned++;
             mode = M_POP;
         } else {

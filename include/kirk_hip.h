@@ -298,7 +298,8 @@ typedef struct {
                                     node records (one 128-B record per step: a node's child boxes and the
                                     near child's own, KIRK's order and counts kept); earlier bounces use the
                                     64-B records.  Default 2 (measured); >= depth: never.
-                                    Batch queries with trace_kernels use them iff wide_from == 0      */
+                                    The shadow stage (any hit) of bounce b uses them when b >= max(wide_from,
+                                    2).  Batch queries with trace_kernels use them iff wide_from == 0   */
 } khp_ctx_params;
 
 /* ---- context --------------------------------------------------------------- */
