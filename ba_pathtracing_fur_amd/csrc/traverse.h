@@ -562,7 +562,7 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
     return false;
 }
 
-// ---- two-level node records (k_extend) ----------------------------------------------------
+// ---- two-level node records (k_extend from bounce wide_from; k_shadow from bounce 2) -------
 // The wide record of interior node X (one 128-B line, `DevScene::wide`, same
 // index as X's 64-B record) holds, for each child C of X, either the boxes and
 // refs of C's two children (C interior) or C's own box (C a leaf):
