@@ -1628,6 +1628,12 @@ __global__ void k_unpack(float* fb, const uint32_t* pix, uint32_t P, const float
         if (e_ != hipSuccess) return fail(KHP_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+#define KHPCHK(expr)                \
+    do {                            \
+        khp_status s_ = (expr);     \
+        if (s_ != KHP_OK) return s_; \
+    } while (0)
+
 struct TimedLaunch {
     int kind;  // 0 extend, 1 shade, 2 shadow (any hit), 3 other, 4 shadow finish
     int bounce;
@@ -1750,17 +1756,96 @@ struct khp_ctx {
     std::vector<uint64_t> gather_counts; // khp_gather_plan counts: root: per sender; sender: its own
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // ABI 11: while a comm is active (or after it was aborted) every device wait
+    // polls with this bound and ncclCommGetAsyncError instead of blocking
+    uint32_t comm_timeout_ms = 120000;
+    std::string comm_dead;   // why the comm was aborted ("" while alive or never created)
     // ABI 8 in-process group (khp_comm_init_local): the gather's transport between
     // contexts of one process instead of RCCL; a sender's k-th gather packs into
-    // ring slot k % LG_SLOTS, the root's k-th gather copies every sender's slot k
+    // ring slot k % LG_SLOTS, the root's k-th gather copies every sender's slot k.
+    // Sender-side slot state: lg_evts[k] = end of the pack, lg_copied[k] = end of
+    // the root's copy (recorded by the root on its stream), lg_stamp[k] = seq + 1
+    // of the gather packed there (0: never), lg_taken[k] = the root has enqueued
+    // that copy, lg_count[k] = pixels packed.
     std::shared_ptr<std::vector<khp_ctx*>> lgroup;
     DevMem lg_slots[64];
-    hipEvent_t lg_evts[64] = {};
+    hipEvent_t lg_evts[64] = {}, lg_copied[64] = {};
+    uint64_t lg_stamp[64] = {}, lg_count[64] = {};
+    bool lg_taken[64] = {};
     uint64_t lg_seq = 0;
 };
 constexpr size_t LG_SLOTS = 64;
 
 static khp_status drain(khp_ctx* c);
+static void comm_release(khp_ctx* c);
+
+// ---- bounded device waits (ABI 11) ------------------------------------------------------------
+// Without a communicator a wait blocks (hipEventSynchronize / hipStreamSynchronize).
+// With one, the context's stream can hold RCCL sends/receives that only finish when
+// the peers post theirs, so a lost or mismatched peer would hang the caller: the
+// wait then polls, checks ncclCommGetAsyncError, and after comm_timeout_ms aborts
+// the communicator (ncclCommAbort releases its kernels) and fails naming this rank
+// and its peers.  KIRK has no multi-device path; its only failure mode is the loud
+// exit of CPU_PathTracer.cpp:236-240, which this mirrors as a status.
+static std::string comm_who(const khp_ctx* c) {
+    return "rank " + std::to_string(c->rank) + " of " + std::to_string(c->nranks);
+}
+static khp_status comm_abort(khp_ctx* c, const std::string& why) {
+    if (c->comm) {
+        (void)ncclCommAbort(c->comm);
+        c->comm = nullptr;
+    }
+    c->comm_dead = why;
+    return fail(KHP_EDEVICE, why);
+}
+static bool bounded_waits(const khp_ctx* c) { return c->comm != nullptr || !c->comm_dead.empty(); }
+
+template <typename Query>
+static khp_status poll_wait(khp_ctx* c, Query query, const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spins = 0;; ++spins) {
+        const hipError_t q = query();
+        if (q == hipSuccess) return KHP_OK;
+        if (q != hipErrorNotReady) return fail(KHP_EDEVICE, std::string(what) + ": " + hipGetErrorString(q));
+        if (c->comm) {
+            ncclResult_t ae = ncclSuccess;
+            const ncclResult_t r = ncclCommGetAsyncError(c->comm, &ae);
+            if (r != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress))
+                return comm_abort(c, comm_who(c) + ": RCCL error while waiting for " + what + ": " +
+                                         ncclGetErrorString(r != ncclSuccess ? r : ae) + "; communicator aborted");
+        }
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (ms > c->comm_timeout_ms) {
+            if (!c->comm)
+                return fail(KHP_EDEVICE, comm_who(c) + ": " + what + " still running " +
+                                             std::to_string(c->comm_timeout_ms) + " ms after the communicator abort (" +
+                                             c->comm_dead + ")");
+            std::string peers;
+            for (int r = 0; r < c->nranks; ++r)
+                if (r != c->rank) peers += (peers.empty() ? "" : ",") + std::to_string(r);
+            return comm_abort(c, comm_who(c) + ": " + what + " not complete after " +
+                                     std::to_string(c->comm_timeout_ms) + " ms; a framebuffer gather with peer(s) " +
+                                     peers + " is not progressing (a peer lost or its gathers mismatched); "
+                                     "communicator aborted");
+        }
+        if (spins < 256) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+static khp_status wait_event(khp_ctx* c, hipEvent_t e, const char* what) {
+    if (!bounded_waits(c)) {
+        HIPCHK(hipEventSynchronize(e));
+        return KHP_OK;
+    }
+    return poll_wait(c, [e] { return hipEventQuery(e); }, what);
+}
+static khp_status wait_stream(khp_ctx* c, hipStream_t s, const char* what) {
+    if (!bounded_waits(c)) {
+        HIPCHK(hipStreamSynchronize(s));
+        return KHP_OK;
+    }
+    return poll_wait(c, [s] { return hipStreamQuery(s); }, what);
+}
 
 static hipEvent_t next_event(khp_ctx* c) {
     if (c->ev_next == c->ev_pool.size()) {
@@ -1881,20 +1966,20 @@ extern "C" void khp_destroy(khp_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)drain(c);
+    if (c->stream) (void)wait_stream(c, c->stream, "the context stream at khp_destroy");
     if (c->gather_evt) (void)hipEventDestroy(c->gather_evt);
     if (c->snap_evt) (void)hipEventDestroy(c->snap_evt);
     if (c->report_ref) (void)hipEventDestroy(c->report_ref);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->comm) ncclCommDestroy(c->comm);
     if (c->lgroup)
         for (auto& m : *c->lgroup)
             if (m == c) m = nullptr;
-    for (auto e : c->lg_evts)
-        if (e) (void)hipEventDestroy(e);
+    for (auto* ev : {c->lg_evts, c->lg_copied})
+        for (size_t k = 0; k < 64; ++k)
+            if (ev[k]) (void)hipEventDestroy(ev[k]);
     for (auto& w : c->ps) {
         for (hipStream_t s : {w.sA, w.sB}) {
             if (!s) continue;
-            (void)hipStreamSynchronize(s);
+            (void)wait_stream(c, s, "a frame stream at khp_destroy");
             (void)hipStreamDestroy(s);
         }
     }
@@ -1910,6 +1995,7 @@ extern "C" void khp_destroy(khp_ctx* c) {
             if (sn->done) (void)hipEventDestroy(sn->done);
             delete sn;
         }
+    comm_release(c);   // after every wait above: those still poll while the comm is alive
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -2395,7 +2481,7 @@ static khp_status harvest(khp_ctx* c, int slot) {
     FrameSlot& f = c->fs[slot];
     if (!f.inflight) return KHP_OK;
     f.inflight = false;
-    HIPCHK(hipEventSynchronize(f.done));
+    KHPCHK(wait_event(c, f.done, "a batch of frames"));
     if (!c->report_open) report_begin(c);
     float ms = 0.0f;
     if (hipEventElapsedTime(&ms, f.ev_start, f.done_t) == hipSuccess) c->st.render_ms += ms;
@@ -2479,7 +2565,7 @@ static khp_status drain(khp_ctx* c) {
         khp_status r = harvest(c, s);
         if (r != KHP_OK) return r;
     }
-    if (c->stream) HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->stream) KHPCHK(wait_stream(c, c->stream, "the context stream"));
     return KHP_OK;
 }
 
@@ -2873,7 +2959,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     }
     s = harvest(c, slot);
     if (s != KHP_OK) return s;
-    HIPCHK(hipStreamSynchronize(c->stream));
+    KHPCHK(wait_stream(c, c->stream, "a synchronous frame"));
     c->report_open = false;
     return KHP_OK;
 }
@@ -3065,11 +3151,21 @@ static khp_status deliver_snapshots(khp_ctx* c, uint64_t upto, bool wait) {
         if (!sn->enqueued) {
             if (!wait) return KHP_OK;
             khp_status s = flush(c);
+            if (!sn->enqueued) {
+                // its conversion never reached the device (an error inside the flush
+                // above or an earlier one): drop this ticket only, so later snapshots
+                // and syncs still work
+                c->snaps.erase(c->snaps.begin());
+                sn->out = nullptr;
+                c->snap_free.push_back(sn);
+                return s != KHP_OK ? s
+                                   : fail(KHP_EDEVICE, "snapshot " + std::to_string(sn->id) +
+                                                           " was not enqueued (an earlier call failed); dropped");
+            }
             if (s != KHP_OK) return s;
-            if (!sn->enqueued) return fail(KHP_EDEVICE, "snapshot was not enqueued");
         }
         if (wait) {
-            HIPCHK(hipEventSynchronize(sn->done));
+            KHPCHK(wait_event(c, sn->done, "an 8-bit snapshot"));
         } else {
             const hipError_t q = hipEventQuery(sn->done);
             if (q == hipErrorNotReady) return KHP_OK;
@@ -3121,7 +3217,13 @@ extern "C" khp_status khp_read_rgba8_async(khp_ctx* c, uint8_t* out_rgba, uint64
         c->pend.push_back(o);
         return KHP_OK;
     }
-    return snapshot_now(c, sn->id);
+    const khp_status st = snapshot_now(c, sn->id);
+    if (st != KHP_OK) {  // not enqueued: the ticket is void, the buffer goes back to the free list
+        c->snaps.pop_back();
+        sn->out = nullptr;
+        c->snap_free.push_back(sn);
+    }
+    return st;
 }
 
 extern "C" khp_status khp_snapshot_wait(khp_ctx* c, uint64_t ticket, int wait) {
@@ -3508,57 +3610,118 @@ extern "C" khp_status khp_get_stats(khp_ctx* c, khp_stats* out) {
 }
 
 // ---- RCCL ---------------------------------------------------------------------------------
-#define NCCLCHK(expr)                                                                                       \
-    do {                                                                                                    \
-        ncclResult_t r_ = (expr);                                                                           \
-        if (r_ != ncclSuccess) return fail(KHP_EDEVICE, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
-    } while (0)
+// The communicator is non-blocking (ncclConfig_t.blocking = 0, ABI 11): an RCCL call
+// may return ncclInProgress while RCCL finishes it in the background, and the
+// communicator must not be used, nor anything enqueued behind the call on its
+// stream, until ncclCommGetAsyncError reports ncclSuccess.  comm_settle does
+// that poll with the context's bound, so no init, send, receive or group end can
+// hang the caller: a timeout or an error aborts the communicator (ncclCommAbort)
+// and returns KHP_EDEVICE naming this rank and its peers.
+static khp_status comm_settle(khp_ctx* c, ncclResult_t r, const std::string& what) {
+    if (!c->comm) return fail(KHP_EDEVICE, comm_who(c) + ": " + what + ": no communicator");
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spins = 0; r == ncclInProgress; ++spins) {
+        ncclResult_t ae = ncclInProgress;
+        const ncclResult_t q = ncclCommGetAsyncError(c->comm, &ae);
+        r = q != ncclSuccess ? q : ae;
+        if (r != ncclInProgress) break;
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (ms > c->comm_timeout_ms)
+            return comm_abort(c, comm_who(c) + ": " + what + " did not complete within " +
+                                     std::to_string(c->comm_timeout_ms) + " ms (peers not joined or not progressing); "
+                                     "communicator aborted");
+        if (spins < 256) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    if (r != ncclSuccess)
+        return comm_abort(c, comm_who(c) + ": " + what + ": " + ncclGetErrorString(r) + "; communicator aborted");
+    return KHP_OK;
+}
+
+// Frees the communicator: finalize (flushes issued operations; bounded), then
+// destroy; a finalize that does not settle aborts instead.
+static void comm_release(khp_ctx* c) {
+    if (!c->comm) return;
+    if (comm_settle(c, ncclCommFinalize(c->comm), "ncclCommFinalize") == KHP_OK && c->comm)
+        (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+    c->comm_dead.clear();
+}
 
 extern "C" khp_status khp_comm_unique_id(uint8_t out_id[128]) {
     if (!out_id) return fail(KHP_EINVAL, "null argument");
     ncclUniqueId id;
-    NCCLCHK(ncclGetUniqueId(&id));
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(KHP_EDEVICE, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
     static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
     memcpy(out_id, &id, 128);
     return KHP_OK;
 }
 
-extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint8_t id[128]) {
-    if (c) {  // complete asynchronous frames first
-        khp_status dr = drain(c);
-        if (dr != KHP_OK) return dr;
+extern "C" khp_status khp_comm_set_timeout(khp_ctx* c, uint32_t timeout_ms) {
+    if (!c || timeout_ms == 0) return fail(KHP_EINVAL, "khp_comm_set_timeout: null context or zero timeout");
+    c->comm_timeout_ms = timeout_ms;
+    return KHP_OK;
+}
+
+static void leave_local_group(khp_ctx* c) {
+    if (c->lgroup)
+        for (auto& m : *c->lgroup)
+            if (m == c) m = nullptr;
+    c->lgroup.reset();
+    c->lg_seq = 0;
+    for (size_t k = 0; k < LG_SLOTS; ++k) {
+        c->lg_stamp[k] = 0;
+        c->lg_taken[k] = false;
+        c->lg_count[k] = 0;
     }
+}
+
+extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint8_t id[128]) {
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(KHP_EINVAL, "bad comm arguments");
     HIPCHK(hipSetDevice(c->device));
-    ncclUniqueId uid;
-    memcpy(&uid, id, 128);
-    if (c->comm) {
-        ncclCommDestroy(c->comm);
-        c->comm = nullptr;
-    }
-    NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+    KHPCHK(drain(c));   // complete asynchronous frames (and gathers) first
+    comm_release(c);
+    leave_local_group(c);
+    memset(c->gather_key, 0, sizeof(c->gather_key));
     c->nranks = nranks;
     c->rank = rank;
-    return KHP_OK;
+    ncclUniqueId uid;
+    memcpy(&uid, id, 128);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;   // every RCCL call is then polled with the context's bound (comm_settle)
+    const ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, uid, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+        c->comm = nullptr;
+        return fail(KHP_EDEVICE, comm_who(c) + ": ncclCommInitRankConfig: " + ncclGetErrorString(r));
+    }
+    const khp_status s = comm_settle(c, r, "RCCL communicator init");
+    if (s != KHP_OK) c->comm_dead.clear();   // nothing was enqueued on the comm: the context stays usable
+    return s;
 }
 
 extern "C" khp_status khp_comm_init_local(khp_ctx* const* ctxs, int nranks) {
     if (!ctxs || nranks < 1) return fail(KHP_EINVAL, "bad local group");
-    for (int r = 0; r < nranks; ++r)
+    for (int r = 0; r < nranks; ++r) {
         if (!ctxs[r]) return fail(KHP_EINVAL, "null context in local group");
+        if (ctxs[r]->device != ctxs[0]->device)
+            return fail(KHP_EINVAL, "local group: every context must be on the same device");
+        for (int q = 0; q < r; ++q)
+            if (ctxs[q] == ctxs[r]) return fail(KHP_EINVAL, "local group: a context appears twice");
+    }
+    for (int r = 0; r < nranks; ++r) {
+        khp_ctx* c = ctxs[r];
+        HIPCHK(hipSetDevice(c->device));
+        KHPCHK(drain(c));
+    }
     auto g = std::make_shared<std::vector<khp_ctx*>>(ctxs, ctxs + nranks);
     for (int r = 0; r < nranks; ++r) {
         khp_ctx* c = ctxs[r];
-        khp_status dr = drain(c);
-        if (dr != KHP_OK) return dr;
-        if (c->comm) {
-            ncclCommDestroy(c->comm);
-            c->comm = nullptr;
-        }
+        comm_release(c);
+        leave_local_group(c);   // stamps cleared: nothing packed for an earlier group is ever copied
         c->lgroup = g;
         c->nranks = nranks;
         c->rank = r;
-        c->lg_seq = 0;
         memset(c->gather_key, 0, sizeof(c->gather_key));
     }
     return KHP_OK;
@@ -3567,7 +3730,10 @@ extern "C" khp_status khp_comm_init_local(khp_ctx* const* ctxs, int nranks) {
 extern "C" khp_status khp_gather_framebuffer(khp_ctx* c, const khp_render_params* p, int root) {
     khp_status s = check_params(c, p);
     if (s != KHP_OK) return s;
-    if (!c->comm && !c->lgroup) return fail(KHP_ENOTREADY, "khp_comm_init first");
+    if (!c->comm && !c->lgroup)
+        return fail(KHP_ENOTREADY, c->comm_dead.empty() ? std::string("khp_comm_init first")
+                                                        : "the communicator was aborted (" + c->comm_dead +
+                                                              "); khp_comm_init again");
     if (root < 0 || root >= c->nranks) return fail(KHP_EINVAL, "bad root");
     if (p->tile_nranks != (uint32_t)c->nranks) return fail(KHP_EINVAL, "tile_nranks must equal the comm size");
     if (!c->pend.empty()) {  // behind asynchronous renders waiting for fusion: keep the call order
@@ -3577,10 +3743,103 @@ extern "C" khp_status khp_gather_framebuffer(khp_ctx* c, const khp_render_params
     return gather_now(c, p, root);
 }
 
+// In-process group transport (khp_comm_init_local).  Sender: pack into slot
+// seq % LG_SLOTS once the root has taken the slot's previous content, stamp it
+// with seq.  Root: every sender's slot must carry this gather's stamp (else
+// KHP_ENOTREADY, nothing enqueued, the root's sequence unchanged); copy each,
+// and record the sender's "copied" event behind the copy so the sender's next
+// pack into that slot waits for it.
+static khp_status local_send(khp_ctx* c, uint32_t P) {
+    const uint64_t seq = c->lg_seq;
+    const size_t k = seq % LG_SLOTS;
+    if (c->lg_stamp[k] && !c->lg_taken[k])
+        return fail(KHP_ENOTREADY, "local group: " + comm_who(c) + " is " + std::to_string(LG_SLOTS) +
+                                       " gathers ahead of the root (gather " + std::to_string(c->lg_stamp[k] - 1) +
+                                       " in ring slot " + std::to_string(k) + " not taken yet)");
+    HIPCHK(c->lg_slots[k].ensure((size_t)P * 3 * sizeof(float) + 16));
+    if (!c->lg_evts[k]) HIPCHK(hipEventCreateWithFlags(&c->lg_evts[k], hipEventDisableTiming));
+    if (!c->lg_copied[k]) HIPCHK(hipEventCreateWithFlags(&c->lg_copied[k], hipEventDisableTiming));
+    if (c->lg_stamp[k]) HIPCHK(hipStreamWaitEvent(c->stream, c->lg_copied[k], 0));  // the root's copy of the old content
+    if (P) hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
+                              c->stage_pix.as<uint32_t>(), P, c->lg_slots[k].as<float>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->lg_evts[k], c->stream));
+    c->lg_stamp[k] = seq + 1;
+    c->lg_taken[k] = false;
+    c->lg_count[k] = P;
+    c->lg_seq = seq + 1;
+    return KHP_OK;
+}
+
+static khp_status local_receive(khp_ctx* c, int root, size_t* total) {
+    const uint64_t seq = c->lg_seq;
+    const size_t k = seq % LG_SLOTS;
+    for (int r = 0; r < c->nranks; ++r) {   // every sender ready before anything is enqueued
+        if (r == root) continue;
+        khp_ctx* sc = (*c->lgroup)[r];
+        if (!sc) return fail(KHP_ENOTREADY, "local group: rank " + std::to_string(r) + " was destroyed");
+        if (sc->lg_stamp[k] != seq + 1 || sc->lg_taken[k])
+            return fail(KHP_ENOTREADY, "local group: rank " + std::to_string(r) + " has not enqueued gather " +
+                                           std::to_string(seq) + " yet");
+        if (sc->lg_count[k] != c->gather_counts[r])
+            return fail(KHP_EINVAL, "local group: rank " + std::to_string(r) + " packed " +
+                                        std::to_string(sc->lg_count[k]) + " pixels, the root's plan expects " +
+                                        std::to_string(c->gather_counts[r]) + " (different frame geometry?)");
+    }
+    *total = 0;
+    for (int r = 0; r < c->nranks; ++r) {
+        if (r == root) continue;
+        khp_ctx* sc = (*c->lgroup)[r];
+        HIPCHK(hipStreamWaitEvent(c->stream, sc->lg_evts[k], 0));
+        const size_t n = c->gather_counts[r];
+        if (n)
+            HIPCHK(hipMemcpyAsync(c->stage.as<float>() + *total * 3, sc->lg_slots[k].p, n * 3 * sizeof(float),
+                                  hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipEventRecord(sc->lg_copied[k], c->stream));
+        sc->lg_taken[k] = true;
+        *total += n;
+    }
+    c->lg_seq = seq + 1;
+    return KHP_OK;
+}
+
+// RCCL transport: one ncclSend per sender; the root posts one receive per sender
+// in ONE group.  The group is closed on every path, also when a receive fails.
+static khp_status rccl_send(khp_ctx* c, uint32_t P, int root) {
+    if (P) hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
+                              c->stage_pix.as<uint32_t>(), P, c->stage.as<float>());
+    HIPCHK(hipGetLastError());
+    return comm_settle(c, ncclSend(c->stage.p, (size_t)P * 3, ncclFloat32, root, c->comm, c->stream),
+                       "ncclSend of " + std::to_string(P) + " pixels to root " + std::to_string(root));
+}
+
+static khp_status rccl_receive(khp_ctx* c, int root, size_t* total) {
+    *total = 0;
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) return comm_settle(c, r, "ncclGroupStart");
+    std::string failed;
+    for (int q = 0; q < c->nranks && failed.empty(); ++q) {
+        if (q == root) continue;
+        r = ncclRecv(c->stage.as<float>() + *total * 3, c->gather_counts[q] * 3, ncclFloat32, q, c->comm, c->stream);
+        if (r != ncclSuccess && r != ncclInProgress)
+            failed = "ncclRecv from rank " + std::to_string(q) + ": " + ncclGetErrorString(r);
+        *total += c->gather_counts[q];
+    }
+    const ncclResult_t e = ncclGroupEnd();   // closes the group on every path
+    if (!failed.empty()) {
+        (void)comm_settle(c, e, "ncclGroupEnd");
+        return comm_abort(c, comm_who(c) + ": " + failed + "; communicator aborted");
+    }
+    return comm_settle(c, e, "the gather's ncclGroupEnd (receives from every sender)");
+}
+
 static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root) {
     khp_status s = check_params(c, p);
     if (s != KHP_OK) return s;
-    if (!c->comm && !c->lgroup) return fail(KHP_ENOTREADY, "khp_comm_init first");
+    if (!c->comm && !c->lgroup)
+        return fail(KHP_ENOTREADY, c->comm_dead.empty() ? std::string("khp_comm_init first")
+                                                        : "the communicator was aborted (" + c->comm_dead +
+                                                              "); khp_comm_init again");
     if (!c->fb.p || c->fbW != p->width || c->fbH != p->height) return fail(KHP_ENOTREADY, "render first");
     if (root < 0 || root >= c->nranks) return fail(KHP_EINVAL, "bad root");
     if (p->tile_nranks != (uint32_t)c->nranks) return fail(KHP_EINVAL, "tile_nranks must equal the comm size");
@@ -3594,7 +3853,7 @@ static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root) {
         if (!e.empty()) return fail(KHP_EINVAL, "khp_gather_framebuffer: " + e);
         HIPCHK(upload(c->stage_pix, flat.data(), flat.size(), c->stream));
         HIPCHK(c->stage.ensure(flat.size() * 3 * sizeof(float) + 16));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        KHPCHK(wait_stream(c, c->stream, "the gather plan upload"));
         memcpy(c->gather_key, key, sizeof(key));
     }
     // Enqueued on the context stream, which already carries the last frame's
@@ -3603,57 +3862,17 @@ static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root) {
     if (!c->gather_evt) HIPCHK(hipEventCreateWithFlags(&c->gather_evt, hipEventDisableTiming));
     if (c->fb_evt) HIPCHK(hipStreamWaitEvent(c->stream, c->fb_evt, 0));
     if (c->rank != root) {
-        uint32_t P = (uint32_t)c->gather_counts[c->rank];
-        if (c->lgroup) {  // in-process group: pack into this gather's ring slot, the root copies it
-            const size_t k = c->lg_seq++ % LG_SLOTS;
-            HIPCHK(c->lg_slots[k].ensure((size_t)P * 3 * sizeof(float) + 16));
-            if (!c->lg_evts[k]) HIPCHK(hipEventCreateWithFlags(&c->lg_evts[k], hipEventDisableTiming));
-            if (P) hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
-                                      c->stage_pix.as<uint32_t>(), P, c->lg_slots[k].as<float>());
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(c->lg_evts[k], c->stream));
-            HIPCHK(hipEventRecord(c->gather_evt, c->stream));
-            c->fb_evt = c->gather_evt;
-            return KHP_OK;
-        }
-        if (P) hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
-                                  c->stage_pix.as<uint32_t>(), P, c->stage.as<float>());
-        NCCLCHK(ncclSend(c->stage.p, (size_t)P * 3, ncclFloat32, root, c->comm, c->stream));
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c->gather_evt, c->stream));
-        c->fb_evt = c->gather_evt;
-        return KHP_OK;
-    }
-    // root: receive every other rank's pixels (one grouped recv), then scatter them into the framebuffer
-    size_t total = 0;
-    if (c->lgroup) {  // in-process group: the senders' slot k of this gather (their k-th gather)
-        const size_t k = c->lg_seq++ % LG_SLOTS;
-        for (int r = 0; r < c->nranks; ++r) {
-            if (r == root) continue;
-            khp_ctx* sc = (*c->lgroup)[r];
-            if (!sc || !sc->lg_evts[k])
-                return fail(KHP_ENOTREADY, "local group: a sender has not enqueued this gather yet");
-            HIPCHK(hipStreamWaitEvent(c->stream, sc->lg_evts[k], 0));
-            const size_t n = c->gather_counts[r];
-            if (n)
-                HIPCHK(hipMemcpyAsync(c->stage.as<float>() + total * 3, sc->lg_slots[k].p, n * 3 * sizeof(float),
-                                      hipMemcpyDeviceToDevice, c->stream));
-            total += n;
-        }
+        const uint32_t P = (uint32_t)c->gather_counts[c->rank];
+        KHPCHK(c->lgroup ? local_send(c, P) : rccl_send(c, P, root));
     } else {
-        NCCLCHK(ncclGroupStart());
-        for (int r = 0; r < c->nranks; ++r) {
-            if (r == root) continue;
-            NCCLCHK(ncclRecv(c->stage.as<float>() + total * 3, c->gather_counts[r] * 3, ncclFloat32, r, c->comm,
-                             c->stream));
-            total += c->gather_counts[r];
-        }
-        NCCLCHK(ncclGroupEnd());
+        // root: receive every other rank's pixels, then scatter them into the framebuffer
+        size_t total = 0;
+        KHPCHK(c->lgroup ? local_receive(c, root, &total) : rccl_receive(c, root, &total));
+        if (total)
+            hipLaunchKernelGGL(k_unpack, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, c->stream,
+                               c->fb.as<float>(), c->stage_pix.as<uint32_t>(), (uint32_t)total, c->stage.as<float>());
+        HIPCHK(hipGetLastError());
     }
-    if (total)
-        hipLaunchKernelGGL(k_unpack, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, c->stream,
-                           c->fb.as<float>(), c->stage_pix.as<uint32_t>(), (uint32_t)total, c->stage.as<float>());
-    HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->gather_evt, c->stream));
     c->fb_evt = c->gather_evt;
     return KHP_OK;

@@ -118,7 +118,8 @@ class Stats(ctypes.Structure):
 
 
 class CtxParams(ctypes.Structure):
-    """khp_ctx_params (ABI 7): scheduling knobs of a context; no value changes any result."""
+    """khp_ctx_params (ABI 10 layout, 48 bytes; path_order since ABI 9, wide_from since
+    ABI 10): scheduling knobs of a context; no value changes any result."""
     _fields_ = [("fuse_frames", c_uint32), ("frames_in_flight", c_uint32), ("chunk_paths", c_uint64),
                 ("heavy_iters", c_uint32), ("dump_bounce", c_int32), ("trace_kernels", c_uint32),
                 ("shade_order", c_uint32), ("serial_stages", c_uint32), ("path_order", c_uint32),
@@ -165,7 +166,10 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device",
             "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params", "khp_debug_shadow_queue",
             "khp_bdpt_params_defaults", "khp_set_bdpt", "khp_get_bdpt", "khp_gather_plan",
-            "khp_read_rgba8_async", "khp_snapshot_wait", "khp_comm_init_local"]
+            "khp_read_rgba8_async", "khp_snapshot_wait", "khp_comm_init_local", "khp_comm_set_timeout"]
+
+# the include/kirk_hip.h this module mirrors (load_library refuses another)
+ABI_VERSION = 11
 
 _lib = None
 
@@ -230,6 +234,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_get_stats": (c_int, [c_void_p, P(Stats)]),
         "khp_comm_unique_id": (c_int, [P(c_uint8)]),
         "khp_comm_init": (c_int, [c_void_p, c_int, c_int, P(c_uint8)]),
+        "khp_comm_set_timeout": (c_int, [c_void_p, c_uint32]),
         "khp_gather_framebuffer": (c_int, [c_void_p, P(RenderParams), c_int]),
         "khp_comm_init_local": (c_int, [P(c_void_p), c_int]),
         "khp_gather_plan": (c_int, [c_uint32, c_uint32, c_uint32, c_int, c_int, c_int, P(c_uint64), P(c_uint32),
@@ -249,6 +254,11 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_host_build": (c_int, [P(SceneDesc), P(c_uint32), P(c_uint32), P(c_float), P(c_int32), P(c_int32),
                                    P(c_int32), P(c_float), P(c_float)]),
     }
+    lib.khp_abi_version.restype = c_int
+    lib.khp_abi_version.argtypes = []
+    abi = lib.khp_abi_version()
+    if abi != ABI_VERSION:   # the structs above would be read with the wrong layout
+        raise RuntimeError(f"{p}: ABI {abi}, this package needs ABI {ABI_VERSION} (rebuild: __graft_entry__.build())")
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -320,9 +320,16 @@ class HipContext:
         return s.as_dict()
 
     # --- multi-GPU --------------------------------------------------------------
-    def comm_init(self, nranks: int, rank: int, uid: bytes):
+    def comm_init(self, nranks: int, rank: int, uid: bytes, timeout_ms: int | None = None):
+        """khp_comm_init; timeout_ms (khp_comm_set_timeout, ABI 11) bounds the init and
+        every later wait of this context while the communicator exists."""
+        if timeout_ms is not None:
+            self.comm_set_timeout(timeout_ms)
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         N.check(self.lib, self.lib.khp_comm_init(self.ptr, nranks, rank, buf), "khp_comm_init")
+
+    def comm_set_timeout(self, timeout_ms: int):
+        N.check(self.lib, self.lib.khp_comm_set_timeout(self.ptr, int(timeout_ms)), "khp_comm_set_timeout")
 
     def gather_framebuffer(self, width, height, spp, depth, tile_size, nranks, rank, root=0):
         p = N.RenderParams(width, height, spp, depth, 0, 0, tile_size, rank, nranks, 0)

@@ -56,7 +56,10 @@ class ShardedFrame:
     """
 
     def __init__(self, ctx, rank: int, world: int, dist=None, tile: int = TILE, root: int = 0,
-                 unique_id=None):
+                 unique_id=None, comm_timeout_ms: int | None = None):
+        """comm_timeout_ms: khp_comm_set_timeout (ABI 11) -- the RCCL init and every
+        later wait of the context fail with KHP_EDEVICE instead of hanging when a
+        peer is lost or a gather has no counterpart (library default 120 s)."""
         if world > 1 and dist is None:
             raise ValueError("world_size > 1 needs an initialised torch.distributed")
         self.ctx, self.rank, self.world, self.dist, self.tile, self.root = ctx, rank, world, dist, tile, root
@@ -65,7 +68,10 @@ class ShardedFrame:
                 from .pathtracer import comm_unique_id as unique_id
             obj = [unique_id() if rank == root else None]
             dist.broadcast_object_list(obj, src=root)
-            ctx.comm_init(world, rank, obj[0])
+            if comm_timeout_ms is None:
+                ctx.comm_init(world, rank, obj[0])
+            else:
+                ctx.comm_init(world, rank, obj[0], timeout_ms=comm_timeout_ms)
 
     def render(self, width, height, spp, depth, seed=0x4B49524B, first_sample=0, stats=False, gather=True,
                async_=False):

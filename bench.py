@@ -104,6 +104,18 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-scene", action="store_true",
                     help="generate + flatten + build on the host (the pre-(f)1/(f)2 path) instead of in HBM")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="--gpus N without torchrun: seconds the N ranks may take before they are killed "
+                         "(exit status 124)")
+    ap.add_argument("--comm-timeout-ms", type=int, default=60000,
+                    help="N > 1: khp_comm_set_timeout -- a lost peer or a gather without its counterpart fails "
+                         "the rank (KHP_EDEVICE) after this long instead of hanging")
+    ap.add_argument("--no-gather-check", action="store_true",
+                    help="N > 1: skip rank 0's re-render of the untiled frame compared with the gathered one")
+    ap.add_argument("--ctx-factory", default=None, metavar="FILE.py:CALLABLE",
+                    help="test hook: build each rank's context with CALLABLE(device=, host_build=) from FILE.py "
+                         "instead of libkirk_hip.so (tests/_bench_standin.py runs the multi-rank orchestration "
+                         "on a CPU); the line is then marked as a stand-in run and measures nothing")
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
     for k in ("steps", "warmup", "strands", "width", "height", "spp"):
@@ -118,7 +130,11 @@ def log(*a):
 
 def launch_ranks(args) -> int:
     """`bench.py --gpus N` without torchrun: run N ranks as a child process group
-    (no GPU has been touched in this process) and return their exit status."""
+    (no GPU has been touched in this process) and return their exit status.
+    torch.distributed.run ends every rank when one fails; if the ranks together
+    take longer than --launch-timeout, the whole group is killed and the status
+    is 124 (a hang never outlives the bench)."""
+    import signal
     import socket
 
     with socket.socket() as s:
@@ -127,7 +143,72 @@ def launch_ranks(args) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     log("bench: launching", " ".join(cmd))
-    return subprocess.call(cmd)
+    proc = subprocess.Popen(cmd, start_new_session=True)
+    try:
+        rc = proc.wait(timeout=args.launch_timeout)
+    except subprocess.TimeoutExpired:
+        log(f"bench: the {args.gpus} ranks did not finish within {args.launch_timeout:.0f} s; killing them")
+        for sig, grace in ((signal.SIGTERM, 15), (signal.SIGKILL, 15)):
+            try:
+                os.killpg(proc.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                proc.wait(timeout=grace)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        return 124
+    if rc != 0:
+        log(f"bench: the ranks exited with status {rc}")
+    return rc if rc >= 0 else 128 - rc
+
+
+def make_context(args, local_rank):
+    """The rank's khp_ctx (pathtracer.HipContext on GPU local_rank), or the
+    --ctx-factory stand-in."""
+    if args.ctx_factory is None:
+        from ba_pathtracing_fur_amd import HipContext
+        return HipContext(device=local_rank, host_build=args.host_scene)
+    import importlib.util
+    path, name = args.ctx_factory.rsplit(":", 1)
+    path = path if os.path.isabs(path) else os.path.join(HERE, path)
+    spec = importlib.util.spec_from_file_location("bench_ctx_factory", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return getattr(mod, name)(device=local_rank, host_build=args.host_scene)
+
+
+def gather_check(args, passes, gathered, scenes):
+    """N > 1, rank 0: re-render the same `passes` progressive passes of the whole
+    (untiled) frame on a second context of this GPU and compare them with the
+    frame the ranks' tiles and RCCL gathers assembled.  Bit for bit: the counter
+    RNG is keyed by pixel and sample, so tile ownership must not change a value
+    (SURVEY §8(e), config 4)."""
+    W, H, spp, depth = args.width, args.height, args.spp, args.depth
+    t0 = time.perf_counter()
+    ref_ctx = make_context(args, int(os.environ.get("LOCAL_RANK", "0")))
+    try:
+        build_scene(ref_ctx, args, scenes)
+        ref_ctx.build_accel()
+        for k in range(passes):
+            ref_ctx.render(W, H, spp, depth, first_sample=k * spp, readback=False, async_=True)
+        ref_ctx.sync()
+        ref = ref_ctx.read_framebuffer(W, H)
+    finally:
+        ref_ctx.close()
+    import numpy as np
+    a, b = gathered.view(np.uint32), ref.view(np.uint32)
+    bad = np.any(a != b, axis=-1)
+    out = {"passes": passes, "pixels": W * H, "bit_exact": bool(not bad.any()), "mismatched_pixels": int(bad.sum()),
+           "ms": round((time.perf_counter() - t0) * 1e3, 1),
+           "def": "rank 0's gathered frame (every rank's tiles, one gather per pass) vs the same passes of the "
+                  "untiled frame re-rendered on rank 0's GPU; float bits compared"}
+    if bad.any():
+        ys, xs = np.nonzero(bad)
+        out["first_mismatch"] = {"x": int(xs[0]), "y": int(ys[0]), "gathered": gathered[ys[0], xs[0]].tolist(),
+                                 "untiled": ref[ys[0], xs[0]].tolist()}
+    return out
 
 
 def available_cores() -> tuple[int, str]:
@@ -273,10 +354,10 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo")   # bootstrap only: the framebuffer moves over RCCL
-    from ba_pathtracing_fur_amd import HipContext, scenes
+    from ba_pathtracing_fur_amd import scenes
 
     W, H, spp, depth = args.width, args.height, args.spp, args.depth
-    ctx = HipContext(device=local_rank, host_build=args.host_scene)
+    ctx = make_context(args, local_rank)
     t0 = time.time()
     sd, path = build_scene(ctx, args, scenes)
     gen_s = time.time() - t0
@@ -292,7 +373,8 @@ def main():
     if rank == 0:
         log(f"scene: {n_objects} objects, gen+flatten {gen_s:.3f}s, BVH+layout {build_s:.3f}s "
             f"({setup}), depth {st0['bvh_depth']}, nodes {st0['n_nodes']}, HBM {st0['device_bytes'] / 1e9:.2f} GB")
-    frame = ShardedFrame(ctx, rank, world, dist, tile=args.tile)
+    frame = ShardedFrame(ctx, rank, world, dist, tile=args.tile, unique_id=getattr(ctx, "comm_unique_id", None),
+                         comm_timeout_ms=args.comm_timeout_ms if world > 1 else None)
     knobs = {k: v for k, v in (("fuse_frames", args.fuse), ("chunk_paths", args.chunk_paths),
                                ("frames_in_flight", args.frames_in_flight), ("shade_order", args.shade_order),
                                ("heavy_iters", args.heavy_iters), ("path_order", args.path_order),
@@ -456,6 +538,15 @@ def main():
             (cnt["shadow_node_visits"] + cnt["shadow_prim_tests"]) * nfi / max(1e-9, s_ms * 1e-3), 1)
         isolated["k_extend"]["records_per_s"] = round(
             (cnt["node_visits"] + cnt["prim_tests"]) * nfi / max(1e-9, e_ms * 1e-3), 1)
+    # N > 1: rank 0's gathered frame against the untiled frame of the same passes
+    check = None
+    if world > 1 and not args.no_gather_check:
+        frame.sync()
+        if rank == 0:
+            check = gather_check(args, k, ctx.read_framebuffer(W, H), scenes)
+            log(f"bench: gather check over {k} passes: {'bit-exact' if check['bit_exact'] else 'MISMATCH'} "
+                f"({check['mismatched_pixels']} pixels differ)")
+        frame.barrier()
     cfg = CONFIGS[args.config]
     out = {
         "metric": METRIC if args.config == "metric" else f"Msamples/s, {cfg['what']}, {W}x{H} {spp}spp",
@@ -477,6 +568,7 @@ def main():
             "config": args.config, "width": W, "height": H, "spp": spp, "depth": depth, "strands": args.strands,
             "objects": n_objects, "parallelism": f"tile-sharded {args.tile}px tiles x{world}, RCCL gather",
         },
+        "gather_check": check,
         "sync_steps": sync_line,
         "gui_steps": gui_line,
         "isolated": isolated,
@@ -566,12 +658,18 @@ def main():
             out["cpu_baseline"] = cpu_baseline(host_scene_for_oracle(sd, args, scenes), args, args.cpu_seconds)
         except Exception as e:  # reported, never silently replaced
             out["cpu_baseline"] = {"error": repr(e)}
+    if args.ctx_factory is not None:
+        out["data"] = f"STAND-IN RUN ({args.ctx_factory}): orchestration test, the numbers measure nothing"
+        out["config"]["ctx_factory"] = args.ctx_factory
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         frame.barrier()
         dist.destroy_process_group()
     ctx.close()
+    if check is not None and not check["bit_exact"]:
+        log("bench: the gathered frame differs from the untiled frame; exiting with status 3")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

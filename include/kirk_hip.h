@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 10
+#define KHP_ABI_VERSION 11
 
 typedef struct khp_ctx khp_ctx;
 
@@ -449,20 +449,37 @@ khp_status khp_get_stats(khp_ctx* ctx, khp_stats* out);
 /* ---- multi-GPU: tile sharding + RCCL framebuffer gather -------------------- */
 /* RCCL unique id (128 bytes), created on rank 0 and broadcast by the caller. */
 khp_status khp_comm_unique_id(uint8_t out_id[128]);
+/* Joins the RCCL communicator of nranks ranks (one process per GPU).  ABI 11:
+ * the communicator is non-blocking (ncclConfig_t.blocking = 0) and no call of
+ * this context waits without a bound while it exists: RCCL calls are polled to
+ * completion, and every device wait (khp_sync, synchronous renders, reads,
+ * khp_destroy) polls ncclCommGetAsyncError.  An RCCL error, or no progress
+ * within the context's timeout (khp_comm_set_timeout, default 120 s: e.g. a
+ * peer that never joins or a gather without its counterpart), aborts the
+ * communicator (ncclCommAbort) and returns KHP_EDEVICE with a message naming
+ * this rank and its peers; gathers then return KHP_ENOTREADY until the next
+ * khp_comm_init.  KIRK has no multi-device path; its only failure mode is the
+ * loud exit of CPU_PathTracer.cpp:236-240. */
 khp_status khp_comm_init(khp_ctx* ctx, int nranks, int rank, const uint8_t id[128]);
+/* ABI 11: the bound (ms, > 0) of the waits above, for this context. */
+khp_status khp_comm_set_timeout(khp_ctx* ctx, uint32_t timeout_ms);
 /* Gather every rank's owned tiles (per p->tile_*) into rank root's device
  * framebuffer over RCCL; root may then khp_read_framebuffer. Collective. */
 khp_status khp_gather_framebuffer(khp_ctx* ctx, const khp_render_params* p, int root);
 
-/* ABI 8: an in-process group of contexts (rank = index in ctxs) for
- * khp_gather_framebuffer without RCCL -- RCCL needs one GPU per rank, this
- * transport lets one process (e.g. a single-GPU test box) run every rank's
- * contexts and the product's gather plan, pack and unpack kernels.  A
- * sender's k-th gather packs into ring slot k % 64 and records an event; the
- * root's k-th gather waits for every sender's slot k, so each sender must have
- * ENQUEUED its k-th gather (khp_sync flushes fused frames) before the root's
- * k-th gather is enqueued, and no sender may run 64 gathers ahead.  Destroy
- * the members together. */
+/* ABI 8: an in-process group of contexts (rank = index in ctxs, all on one
+ * device) for khp_gather_framebuffer without RCCL -- RCCL needs one GPU per
+ * rank, this transport lets one process (e.g. a single-GPU test box) run every
+ * rank's contexts and the product's gather plan, pack and unpack kernels.  A
+ * sender's k-th gather packs into ring slot k % 64, stamped with k; the root's
+ * k-th gather copies every sender's slot k, so each sender must have ENQUEUED
+ * its k-th gather (khp_sync flushes fused frames) before the root's k-th gather
+ * is enqueued (else the root's call returns KHP_ENOTREADY and can be repeated),
+ * and a sender 64 gathers ahead of the root gets KHP_ENOTREADY instead of
+ * overwriting a slot the root has not taken (ABI 11: stamps; before, both cases
+ * copied stale pixels silently).  A member's pack into a slot waits for the
+ * root's copy of its previous content.  Re-initialising a member removes it
+ * from its old group. */
 khp_status khp_comm_init_local(khp_ctx* const* ctxs, int nranks);
 
 /* ABI 8: the pixel plan khp_gather_framebuffer moves, as seen from `rank`

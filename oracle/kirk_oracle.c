@@ -2002,6 +2002,9 @@ int ko_trace_closest(ko_ctx* c, uint32_t n, const float* orig, const float* dir,
 int ko_trace_closest_log(ko_ctx* c, uint32_t n, const float* orig, const float* dir, float* t_out, int32_t* log,
                          uint64_t cap, uint64_t* offsets) {
     trav_stats_t st = {0, 0, log, 0, cap, 0};
+    /* a log entry packs the node id into bits 0..24 and the deferred far-child
+     * count into bits 25..31: a larger tree would alias ids and counts */
+    if (c->n_nodes >= (1u << 25)) return KHP_EINVAL;
     for (uint32_t i = 0; i < n; ++i) {
         offsets[i] = st.log_n;
         ray_t r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));

@@ -49,7 +49,16 @@ def test_library_is_gfx950_code_object():
 
 
 def test_abi_version():
-    assert N.load_library().khp_abi_version() >= 1
+    """The library, the header and the ctypes mirror agree (load_library refuses a
+    library of another ABI: its structs would be read with the wrong layout)."""
+    m = re.search(r"#define KHP_ABI_VERSION (\d+)", open(HEADER).read())
+    assert N.load_library().khp_abi_version() == int(m.group(1)) == N.ABI_VERSION
+
+
+def test_comm_timeout_needs_a_context_and_a_bound():
+    lib = N.load_library()
+    assert lib.khp_comm_set_timeout(None, 1000) == N.KHP_EINVAL
+    assert b"timeout" in lib.khp_last_error()
 
 
 def test_bsdf_registry_matches_kirk_factory_names():

@@ -302,19 +302,24 @@ def test_config2_full_size_sampled_rows(hip_ctx):
 def test_config5_full_size_sampled_rows():
     """BASELINE config 5 at its stated size: 1M strands (9M cones, generated in
     HBM) + 500x500x2-triangle torus + subdiv-5 glass icosphere at 3840x2160;
-    2 spp (the path is per-sample independent, so 32 spp is 16 such passes),
-    every 216th row against the oracle on the host-generated scene."""
+    8 spp as 4 fused asynchronous 2-spp passes (the path is per-sample
+    independent, so 32 spp is 16 such passes), every 54th row (40 rows) against
+    the oracle's 8-spp frame on the host-generated scene."""
     ctx = HipContext(0)
     try:
         S.config5_device(ctx, 3840, 2160, n_strands=1_000_000)
         ctx.build_accel()
         assert ctx.stats()["n_objects"] == 500 * 500 * 2 + 20 * 4 ** 5 + 2 + 9_000_000
-        got = ctx.render(3840, 2160, 2, 5)
+        for k in range(4):
+            ctx.render(3840, 2160, 2, 5, first_sample=2 * k, async_=True)
+        ctx.sync()
+        got = ctx.read_framebuffer(3840, 2160)
     finally:
         ctx.close()
     host = S.config5(3840, 2160, n_strands=1_000_000)
-    rows = list(range(11, 2160, 216))
-    want = oracle_ffi.Oracle(host).render(3840, 2160, 2, 5, threads=16, rows=(11, 2160, 216))
+    rows = list(range(11, 2160, 54))
+    assert len(rows) == 40
+    want = oracle_ffi.Oracle(host).render(3840, 2160, 8, 5, threads=16, rows=(11, 2160, 54))
     assert_parity(got[rows], want[rows], exact=True)
 
 
@@ -423,11 +428,20 @@ def test_fused_full_size_matches_passes():
         ctx.close()
 
 
-def test_driver_batch_chunks():
+@pytest.fixture(scope="module")
+def metric_oracle():
+    """The oracle on the host-generated metric scene (config 3: 1M strands,
+    9,000,002 objects); its BVH build takes ~15 s, so the tests below share it."""
+    return oracle_ffi.Oracle(S.config3(1920, 1080, n_strands=1_000_000))
+
+
+def test_driver_batch_chunks(metric_oracle):
     """The driver's bench command: 20 fused 8-spp passes at the metric size
-    (332M paths).  The automatic chunk size makes 2 chunks of 166M paths (within
-    5/4 of the 2^27 cap) instead of 3; an explicit chunk_paths is a hard cap
-    (2^27: 3 chunks, 2^26: 5).  All give the same framebuffer, bit for bit."""
+    (332M paths), default parameters.  The automatic chunk size makes 2 chunks of
+    166M paths (within 5/4 of the 2^27 cap) instead of 3; an explicit chunk_paths
+    is a hard cap (2^27: 3 chunks, 2^26: 5).  All give the same framebuffer, bit
+    for bit, and the default batch -- exactly what the timed region renders -- is
+    the oracle's 160-spp frame on every 20th row (54 rows x 1920 px x 160 spp)."""
     ctx = HipContext(0)
     try:
         S.config3_device(ctx, 1920, 1080, n_strands=1_000_000)
@@ -446,6 +460,26 @@ def test_driver_batch_chunks():
             assert np.array_equal(got[cap][1].view(np.uint32), got[0][1].view(np.uint32)), cap
     finally:
         ctx.close()
+    rows = list(range(3, 1080, 20))
+    assert len(rows) == 54
+    want = metric_oracle.render(1920, 1080, 160, 5, threads=16, rows=(3, 1080, 20))
+    assert_parity(got[0][1][rows], want[rows], exact=True)
+
+
+def test_config3_stated_spp_rows(metric_oracle):
+    """BASELINE config 3 at its stated 16 spp (one synchronous render of the
+    1M-strand scene generated in HBM): every 20th row against the oracle."""
+    ctx = HipContext(0)
+    try:
+        S.config3_device(ctx, 1920, 1080, n_strands=1_000_000)
+        ctx.build_accel()
+        got = ctx.render(1920, 1080, 16, 5)
+    finally:
+        ctx.close()
+    rows = list(range(11, 1080, 20))
+    assert len(rows) >= 54
+    want = metric_oracle.render(1920, 1080, 16, 5, threads=16, rows=(11, 1080, 20))
+    assert_parity(got[rows], want[rows], exact=True)
 
 
 @pytest.mark.parametrize("max_paths", ["14000", "4096"])

@@ -122,3 +122,111 @@ def test_local_group_driver_batch_two_ranks():
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_rccl_single_rank_gather_on_one_gpu():
+    """The RCCL path on a one-GPU box: a non-blocking communicator of one rank
+    (khp_comm_init, ABI 11), rank 0's gather posting an empty receive group
+    (ncclGroupStart/End), frames fused around it.  The frame is the untiled one."""
+    from ba_pathtracing_fur_amd.pathtracer import HipContext, comm_unique_id
+    W, H, SPP = 64, 48, 2
+    sd = S.config2(W, H, n_strands=800)
+    want = oracle_ffi.Oracle(sd).render(W, H, 2 * SPP, 5, threads=16)
+    ctx = HipContext(0)
+    try:
+        ctx.set_scene(sd)
+        ctx.build_accel()
+        ctx.comm_init(1, 0, comm_unique_id(), timeout_ms=30000)
+        for k in range(2):
+            ctx.render(W, H, SPP, 5, first_sample=k * SPP, tile_size=16, tile_rank=0, tile_nranks=1, readback=False,
+                       async_=True)
+            ctx.gather_framebuffer(W, H, SPP, 5, 16, 1, 0, 0)
+        ctx.sync()
+        assert_parity(ctx.read_framebuffer(W, H), want, exact=True)
+    finally:
+        ctx.close()
+
+
+_NO_PEER = r"""
+import sys, time
+sys.path.insert(0, %(root)r)
+from ba_pathtracing_fur_amd import native as N, scenes as S
+from ba_pathtracing_fur_amd.pathtracer import HipContext, comm_unique_id
+ctx = HipContext(0)
+sd = S.config2(32, 24, n_strands=100)
+ctx.set_scene(sd); ctx.build_accel()
+t0 = time.time()
+try:
+    ctx.comm_init(2, 0, comm_unique_id(), timeout_ms=3000)   # rank 1 never joins
+    print("UNEXPECTED: init succeeded"); sys.exit(1)
+except N.KhpError as e:
+    dt = time.time() - t0
+    assert e.status == N.KHP_EDEVICE, e
+    assert "rank 0 of 2" in str(e) and "3000 ms" in str(e), e
+    assert dt < 30, dt
+try:
+    ctx.gather_framebuffer(32, 24, 1, 5, 16, 2, 0, 0)
+    print("UNEXPECTED: gather without a communicator"); sys.exit(1)
+except N.KhpError as e:
+    assert e.status in (N.KHP_ENOTREADY, N.KHP_EINVAL), e
+img = ctx.render(32, 24, 1, 5)          # the context is still usable
+assert img.shape == (24, 32, 3)
+ctx.close()
+print("NO_PEER_OK %%.1f s" %% dt)
+"""
+
+
+def test_rccl_init_without_peer_fails_with_a_status():
+    """A forced RCCL failure: rank 0 of 2 initialises while rank 1 never joins.
+    The non-blocking init is polled against the context's timeout and returns
+    KHP_EDEVICE naming the rank (it used to block in ncclCommInitRank forever).
+    Run in a child process with its own time limit, so a regression cannot
+    hang the test run."""
+    r = subprocess.run([sys.executable, "-c", _NO_PEER % {"root": ROOT}], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "NO_PEER_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+def test_local_group_refuses_out_of_order_gathers():
+    """khp_comm_init_local's stamped ring slots (ABI 11): a root gather enqueued
+    before its sender's returns KHP_ENOTREADY and can be repeated; a sender 64
+    gathers ahead of its root gets KHP_ENOTREADY instead of overwriting a slot
+    the root has not copied (both used to copy stale pixels silently); the
+    frame after the repeated gathers is still the oracle's."""
+    from ba_pathtracing_fur_amd import native as N
+    from ba_pathtracing_fur_amd.pathtracer import HipContext, comm_init_local
+    W, H, SPP, TILE = 48, 32, 1, 16
+    sd = S.config2(W, H, n_strands=600)
+    want = oracle_ffi.Oracle(sd).render(W, H, SPP, 5, threads=16)
+    ctxs = [HipContext(0) for _ in range(2)]
+    try:
+        for c in ctxs:
+            c.set_scene(sd)
+            c.build_accel()
+        comm_init_local(ctxs)
+        for r in (0, 1):
+            ctxs[r].render(W, H, SPP, 5, tile_size=TILE, tile_rank=r, tile_nranks=2, readback=False)
+        with pytest.raises(N.KhpError) as e:       # root first: its sender has not packed gather 0
+            ctxs[0].gather_framebuffer(W, H, SPP, 5, TILE, 2, 0, 0)
+        assert e.value.status == N.KHP_ENOTREADY
+        ctxs[1].gather_framebuffer(W, H, SPP, 5, TILE, 2, 1, 0)
+        ctxs[0].gather_framebuffer(W, H, SPP, 5, TILE, 2, 0, 0)   # repeated: now it finds gather 0
+        ctxs[0].sync()
+        assert_parity(ctxs[0].read_framebuffer(W, H), want, exact=True)
+        for _ in range(64):                        # gathers 1..64 fill the ring; the root takes none
+            ctxs[1].gather_framebuffer(W, H, SPP, 5, TILE, 2, 1, 0)
+        with pytest.raises(N.KhpError) as e:       # gather 65 would overwrite gather 1's slot
+            ctxs[1].gather_framebuffer(W, H, SPP, 5, TILE, 2, 1, 0)
+        assert e.value.status == N.KHP_ENOTREADY
+        ctxs[0].gather_framebuffer(W, H, SPP, 5, TILE, 2, 0, 0)   # the root takes gather 1
+        ctxs[1].gather_framebuffer(W, H, SPP, 5, TILE, 2, 1, 0)   # and slot 1 is free again
+        ctxs[1].sync()
+        ctxs[0].sync()
+        comm_init_local(ctxs)                      # a new group starts from gather 0 on both
+        ctxs[1].gather_framebuffer(W, H, SPP, 5, TILE, 2, 1, 0)
+        ctxs[0].gather_framebuffer(W, H, SPP, 5, TILE, 2, 0, 0)
+        ctxs[0].sync()
+        assert_parity(ctxs[0].read_framebuffer(W, H), want, exact=True)
+    finally:
+        for c in ctxs:
+            c.close()

@@ -1,0 +1,7 @@
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r04b
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
