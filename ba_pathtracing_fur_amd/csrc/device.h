@@ -206,15 +206,24 @@ __device__ __forceinline__ void tri_uv(float4 r0, float4 r1, float4 r2, const Ra
     v = dot(wu, r.d) * inv;
 }
 
-// Cylinder::closestIntersection (Common/Cylinder.cpp:73-156), open cone frustum.
-__device__ __forceinline__ bool cone_closest(float4 c0, float4 c1, float4 c2, float4 c3, const Ray& r, float tMin,
-                                             float tMax, float& t) {
+// Cylinder::closestIntersection (Common/Cylinder.cpp:73-156) and
+// Cylinder::isIntersection (:158-228), open cone frustum.  The two differ only
+// in the quadratic's leading coefficient -- a = 1 - Dy^2 (1 + s^2) for the
+// closest hit, a = Dx^2 + Dz^2 - s^2 Dy^2 for the any hit -- and in the any
+// hit's fixed tMin = 0; everything after a is the same sequence.  any_form
+// selects a (a compile-time constant in cone_closest / cone_any; a per-lane
+// value in the path kernel's mixed closest/any traversal, where both
+// coefficients are computed by their own expressions and one is selected).
+__device__ __forceinline__ bool cone_quadratic(float4 c0, float4 c1, float4 c2, float4 c3, const Ray& r, bool any_form,
+                                               float tMin, float tMax, float& t) {
     v3 base = mk(c0.x, c0.y, c0.z), U = mk(c1.x, c1.y, c1.z), Vv = mk(c2.x, c2.y, c2.z), W = mk(c3.x, c3.y, c3.z);
     float r0 = c0.w, slope = c1.w, min_d = c2.w, max_d = c3.w;
     v3 P = r.o - base;
     P = mk(dot(P, U), dot(P, Vv), dot(P, W));
     v3 D = mk(dot(r.d, U), dot(r.d, Vv), dot(r.d, W));
-    float a = 1.0f - D.y * D.y * (1.0f + slope * slope);
+    const float a_closest = 1.0f - D.y * D.y * (1.0f + slope * slope);
+    const float a_any = D.x * D.x + D.z * D.z - slope * slope * D.y * D.y;
+    float a = any_form ? a_any : a_closest;
     float b = P.x * D.x + P.z * D.z + r0 * slope * D.y - slope * slope * P.y * D.y;
     float c = r0 - slope * P.y;
     c = P.x * P.x + P.z * P.z - c * c;
@@ -238,33 +247,15 @@ __device__ __forceinline__ bool cone_closest(float4 c0, float4 c1, float4 c2, fl
     return false;
 }
 
+__device__ __forceinline__ bool cone_closest(float4 c0, float4 c1, float4 c2, float4 c3, const Ray& r, float tMin,
+                                             float tMax, float& t) {
+    return cone_quadratic(c0, c1, c2, c3, r, false, tMin, tMax, t);
+}
+
 // Cylinder::isIntersection (Common/Cylinder.cpp:158-228): note a = Dx^2+Dz^2-s^2 Dy^2.
 __device__ __forceinline__ bool cone_any(float4 c0, float4 c1, float4 c2, float4 c3, const Ray& r, float tMax) {
-    v3 base = mk(c0.x, c0.y, c0.z), U = mk(c1.x, c1.y, c1.z), Vv = mk(c2.x, c2.y, c2.z), W = mk(c3.x, c3.y, c3.z);
-    float r0 = c0.w, slope = c1.w, min_d = c2.w, max_d = c3.w;
-    v3 P = r.o - base;
-    P = mk(dot(P, U), dot(P, Vv), dot(P, W));
-    v3 D = mk(dot(r.d, U), dot(r.d, Vv), dot(r.d, W));
-    float a = D.x * D.x + D.z * D.z - slope * slope * D.y * D.y;
-    float b = P.x * D.x + P.z * D.z + r0 * slope * D.y - slope * slope * P.y * D.y;
-    float c = r0 - slope * P.y;
-    c = P.x * P.x + P.z * P.z - c * c;
-    float disc = b * b - a * c;
-    if (disc < 0.0f) return false;
-    disc = sqrtf(disc);
-    float t1 = (-b - disc) / a;
-    float t2 = (-b + disc) / a;
-    if ((t2 < 0.0f) || (t1 > tMax)) return false;
-    if (t1 < RAY_EPS_D) {
-        if ((t2 > tMax) || (t2 < 0.0f)) return false;
-        float d = dot(Vv, follow(r, t2));
-        return d >= min_d && d <= max_d;
-    }
-    if ((t1 < 0.0f) && (t2 > tMax)) return false;
-    float d = dot(Vv, follow(r, t1));
-    if (d >= min_d && d <= max_d) return true;
-    d = dot(Vv, follow(r, t2));
-    return d >= min_d && d <= max_d;
+    float t;
+    return cone_quadratic(c0, c1, c2, c3, r, true, 0.0f, tMax, t);
 }
 
 #include "traverse.h"

@@ -1313,6 +1313,361 @@ static void launch_shadow(bool stats, bool wide, int grid, hipStream_t s, const 
     }
 }
 
+// ---- path kernel: every bounce of a path in one persistent launch (khp_ctx_params.path_kernel) ----
+// KIRK's loop runs every pixel's path to its end, bounce after bounce
+// (PathTracer::traceRays, CPU_PathTracer.cpp:129-168).  The wavefront above makes
+// each bounce's stages persistent launches, and a launch ends with its slowest
+// ray: a synchronous frame pays depth x (extension tail + shadow tail) whatever
+// its size -- 11 of the 14.8 ms of a 1-spp 1080p call (profiles/
+// r04a_sync_breakdown.md).  k_path carries every path of a chunk through all its
+// bounces in ONE persistent launch: a lane traces its path's extension ray,
+// shades the hit, traces the shadow ray in the same loop (iter2k<2>: the lane's
+// query kind is a per-lane value), adds the colour, continues with the next
+// bounce, and claims the next camera path when its path ends.  Only the longest
+// path remains a tail.  Shading waits until REFILL lanes of the wave have
+// finished their traversals (fewer once every path is claimed), so the shading
+// code runs with most lanes active.  A lane's path state (T, C, key, the next
+// ray and the deferred NEE terms) lives in global columns (PathLanes, one entry
+// per resident lane) while it traverses, so the loop carries traversal
+// registers only.  The per-hit arithmetic is k_shade's (the !BD path), the
+// any-hit walk k_shadow's and the colour add k_shadow_finish's: frames are
+// bit-identical to the wavefront's and the oracle's.
+#ifndef KHP_PATH_WAVES
+#define KHP_PATH_WAVES 4
+#endif
+#ifndef KHP_PATH_RING
+#define KHP_PATH_RING 8
+#endif
+constexpr int PATH_WAVES = KHP_PATH_WAVES;
+constexpr int PATH_RING = KHP_PATH_RING;
+constexpr size_t PATH_LDS_BYTES = 3 * PATH_RING * TRAV_BLOCK * sizeof(uint32_t);
+
+struct PathLanes {
+    // [column][grid lane]: 0 T.xyz | flags   1 C.xyz | key   2 next ray o.xyz | path id
+    // 3 next ray d.xyz | bounce (bit 31: the path continues after the pending shadow ray)
+    // 4 lc.xyz | has_emit   5 Told.xyz   6 AT.xyz   7 ET.xyz  (the deferred NEE terms, k_shade's shadow record)
+    float4* col[8];
+};
+
+// k_shade's per-hit operations without the light-path variant (KIRK's traceRay
+// light test, EnvironmentShader / LightShader / SimpleShader /
+// MarschnerHairShader): the path state after bounce `bounce` and, when the NEE
+// colour is nonzero, the shadow ray whose any-hit result decides the deferred
+// colour add (shadow_finish_one).
+struct ShadeOut {
+    v3 T, C;
+    int flags;
+    Ray nr;           // the next extension ray
+    bool emit_ray;    // the path continues with nr
+    bool emit_sh;     // a shadow ray to trace; the colour add is deferred to its finish
+    Ray shr;
+    float sh_tmax;
+    v3 lc, Told, AT, ET;
+    bool has_emit;
+};
+template <bool TEX>
+__device__ __forceinline__ void shade_core(const DevScene& S, const Ray& r, float lambda, int32_t slot, v3 T, v3 C,
+                                           int flags, uint32_t key, uint32_t bounce, bool last, ShadeOut& o) {
+    o.nr.o = o.nr.d = mk(0, 0, 0);
+    o.shr.o = o.shr.d = mk(0, 0, 0);
+    o.sh_tmax = 0.0f;
+    o.lc = o.Told = o.AT = o.ET = mk(0, 0, 0);
+    o.has_emit = false;
+    o.emit_sh = false;
+    float t_lights = FLT_MAX_;
+    int t_index = -1;
+    for (int li = 0; li < S.n_lights; ++li) {
+        float t = FLT_MAX_;
+        if (light_isect(S.lights[li], r, t)) {
+            t_lights = gmin(t_lights, t);
+            t_index = (t == t_lights) ? li : t_index;
+        }
+    }
+    bool light_hit = false;
+    if (t_lights < lambda) {
+        lambda = t_lights;
+        light_hit = true;
+    }
+    if (lambda == FLT_MAX_) {
+        C = C + (TEX ? env_color(S, r.d) : mk(S.env.color[0], S.env.color[1], S.env.color[2])) * T;
+        T = mk(0, 0, 0);
+    } else if (light_hit) {
+        C = C + light_emit(S.lights[t_index], r.d) * T;
+        T = mk(0, 0, 0);
+    } else {
+        ShadeCtx s;
+        khp_material mres;
+        const Hit hh{lambda, slot, 0.0f, 0.0f};
+        const v3 nrm = surface_at<TEX>(S, r, hh, s, mres);
+        const v3 loc = follow(r, lambda);
+        const khp_material* m = s.m;
+        float h0 = draw_u01(key, dim_of(bounce, P_HAIR_ALPHA)), h1 = draw_u01(key, dim_of(bounce, P_HAIR_BETA));
+        v3 counter = -normalize(r.d);
+        bool need_shadow = false;
+        if (S.n_lights > 0) {
+            int li = (int)((double)draw_u01(key, dim_of(bounce, P_LIGHT_SEL)) * (double)S.n_lights);
+            const DevLight& L = S.lights[li];
+            float att;
+            Ray h2l = light_dir(L, loc, draw_u01(key, dim_of(bounce, P_LIGHT_0)),
+                                draw_u01(key, dim_of(bounce, P_LIGHT_1)), att);
+            v3 lightpos = h2l.o + h2l.d;
+            h2l.o = h2l.o + faceforward(nrm, h2l.o - lightpos, nrm) * 1e-4f;
+            h2l.d = normalize(h2l.d);
+            if (L.color[0] > 0.0f || L.color[1] > 0.0f || L.color[2] > 0.0f) {
+                v3 f = bsdf_eval(s, h2l.d, -r.d);
+                float ad = fabsf(dot(h2l.d, nrm));
+                o.lc = mk(L.color[0] * ((att * f.x) * ad), L.color[1] * ((att * f.y) * ad),
+                          L.color[2] * ((att * f.z) * ad));
+                o.sh_tmax = length(lightpos - h2l.o);
+                o.shr = h2l;
+                need_shadow = true;
+            }
+        }
+        v3 ev = bsdf_eval(s, nrm, nrm);
+        v3 amb = mk(S.env.ambient[0], S.env.ambient[1], S.env.ambient[2]) * (ev * ONE_OVER_PI);
+        o.Told = T;
+        o.AT = amb * T;
+        bool add_now = true;
+        if (m->shader == KHP_SHADER_MARSCHNER_HAIR) {
+            float smp[2] = {0.0f, 0.0f};
+            v3 out;
+            float pdf = 0.0f;
+            bool valid;
+            v3 refl = bsdf_sample(s, counter, nrm, smp, h0, h1, out, pdf, flags, valid);
+            v3 off = out * 1e-4f;
+            if (!(flags & F_SPECULAR)) off = faceforward(-(nrm * 1e-4f), nrm, out);
+            o.nr = make_ray(loc + off, out);
+            if ((flags & F_CYL_T) || (flags & F_CYL_TR)) {
+                need_shadow = false;
+                add_now = false;
+            } else {
+                if (is_zero(refl) || pdf <= 1E-4f || gmax(T.x, gmax(T.y, T.z)) < 0.01f) T = mk(0, 0, 0);
+                else T = T * ((refl * 3.0f) * fabsf(k_cosf(smp[0])));
+            }
+        } else {
+            float smp[2] = {draw_u01(key, dim_of(bounce, P_BSDF_0)), draw_u01(key, dim_of(bounce, P_BSDF_1))};
+            v3 out;
+            float pdf = 0.0f;
+            int fl = 0;
+            bool valid;
+            v3 refl = bsdf_sample(s, counter, nrm, smp, h0, h1, out, pdf, fl, valid);
+            if (is_zero(refl) || pdf <= 1E-4f || gmax(T.x, gmax(T.y, T.z)) < 0.01f) {
+                T = mk(0, 0, 0);
+            } else if ((fl & F_EMISSIVE) == F_EMISSIVE) {
+                o.has_emit = true;
+                o.ET = mk(m->emission[0], m->emission[1], m->emission[2]) * T;
+                T = mk(0, 0, 0);
+            } else {
+                float ad = fabsf(dot(out, nrm));
+                T = T * ((refl * ad) / pdf);
+                flags = fl;
+                v3 off = out * 1e-4f;
+                if ((fl & F_SPECULAR) != F_SPECULAR) off = faceforward(-(nrm * 1e-4f), nrm, out);
+                o.nr = make_ray(loc + off, out);
+            }
+        }
+        if (add_now) {
+            const v3 lc = o.lc;
+            if (need_shadow && !(lc.x == 0.0f && lc.y == 0.0f && lc.z == 0.0f)) {
+                o.emit_sh = true;  // the colour add waits for the shadow ray
+            } else if (need_shadow) {  // zero light colour: the finish's operations, without the ray (k_shade)
+                v3 dl = mk(0, 0, 0) + lc * 1.0f;
+                v3 acc = (mk(0, 0, 0) + dl * o.Told) + o.AT;
+                if (o.has_emit) acc = acc + o.ET;
+                C = C + acc;
+            } else {
+                v3 acc = (mk(0, 0, 0) + mk(0, 0, 0) * o.Told) + o.AT;
+                if (o.has_emit) acc = acc + o.ET;
+                C = C + acc;
+            }
+        }
+    }
+    o.T = T;
+    o.C = C;
+    o.flags = flags;
+    o.emit_ray = !last && !is_zero(T) && !is_zero(o.nr.d);
+}
+
+// shadow_finish_one's colour term for a traced shadow ray.
+__device__ __forceinline__ v3 finish_acc(const DevScene& S, const Ray& r, float tmax, bool occ, v3 lc, v3 Told, v3 AT,
+                                         bool has_emit, v3 ET) {
+    if (!occ) {
+        for (int li = 0; li < S.n_lights; ++li) {
+            float t;
+            if (light_isect(S.lights[li], r, t) && (t < tmax)) {
+                occ = true;
+                break;
+            }
+        }
+    }
+    v3 l = lc * (occ ? 0.0f : 1.0f);
+    v3 dl = mk(0, 0, 0) + l;
+    v3 acc = (mk(0, 0, 0) + dl * Told) + AT;
+    if (has_emit) acc = acc + ET;
+    return acc;
+}
+
+enum : uint32_t { PS_TRAV = 0u, PS_FIN = 1u, PS_NEW = 2u, PS_BEGIN = 3u, PS_DONE = 4u };
+
+template <bool TEX, bool WIDE>
+__global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wave Wv, SpillArea spill, PathLanes L) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t npaths = Wv.P * Wv.n_samples * Wv.n_frames;
+    const uint32_t g = blockIdx.x * TRAV_BLOCK + threadIdx.x;
+    LdsStack<PATH_RING, false> stk;
+    stk.init(lds, spill.base, spill.stride);
+    TravStats st{0, 0, 0};
+    TravRay tr;
+    tr.r.o = tr.r.d = tr.inv = mk(0, 0, 0);
+    tr.fin = true;
+    Hit h{FLT_MAX_, -1, 0.0f, 0.0f};
+    Cur c{0u, 0.0f, 0.0f, false};
+    LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
+    uint32_t mode = 0u, state = PS_NEW, n_ext = 0, n_sh = 0;
+    bool any = false, occ = false, exhausted = false;
+    float tmax_any = 0.0f;
+    Claimer cl;
+    cl.init(Wv.cnt->fetch_ext, npaths, 0u, npaths);
+    for (;;) {
+        // ---- service: shade finished extension rays, finish shadow rays, claim camera
+        //      paths, start traversals -- until every lane traverses or has no work left
+        for (;;) {
+            if (state == PS_FIN && !any) {  // k_shade
+                const float4 f0 = L.col[0][g], f1 = L.col[1][g], f2 = L.col[2][g], f3 = L.col[3][g];
+                const uint32_t bounce = bits_from_f(f3.w) & 0xFFFFu;
+                ShadeOut o;
+                shade_core<TEX>(S, tr.r, h.t, h.slot, mk(f0.x, f0.y, f0.z), mk(f1.x, f1.y, f1.z),
+                                (int)bits_from_f(f0.w), bits_from_f(f1.w), bounce, bounce + 1 >= Wv.depth, o);
+                ++n_ext;
+                const float4 tfo = make_float4(o.T.x, o.T.y, o.T.z, f_from_bits((uint32_t)o.flags));
+                const float4 cko = make_float4(o.C.x, o.C.y, o.C.z, f1.w);
+                if (o.emit_sh) {
+                    L.col[0][g] = tfo;
+                    L.col[1][g] = cko;
+                    L.col[2][g] = make_float4(o.nr.o.x, o.nr.o.y, o.nr.o.z, f2.w);
+                    L.col[3][g] = make_float4(o.nr.d.x, o.nr.d.y, o.nr.d.z,
+                                              f_from_bits(bounce | (o.emit_ray ? 0x80000000u : 0u)));
+                    L.col[4][g] = make_float4(o.lc.x, o.lc.y, o.lc.z, o.has_emit ? 1.0f : 0.0f);
+                    L.col[5][g] = make_float4(o.Told.x, o.Told.y, o.Told.z, 0.0f);
+                    L.col[6][g] = make_float4(o.AT.x, o.AT.y, o.AT.z, 0.0f);
+                    L.col[7][g] = make_float4(o.ET.x, o.ET.y, o.ET.z, 0.0f);
+                    trav_setup(tr, o.shr);
+                    tmax_any = o.sh_tmax;
+                    any = true;
+                    state = PS_BEGIN;
+                } else if (o.emit_ray) {
+                    L.col[0][g] = tfo;
+                    L.col[1][g] = cko;
+                    L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(bounce + 1u));
+                    trav_setup(tr, o.nr);
+                    any = false;
+                    state = PS_BEGIN;
+                } else {
+                    Wv.CK[bits_from_f(f2.w)] = cko;
+                    state = PS_NEW;
+                }
+            } else if (state == PS_FIN) {  // k_shadow_finish
+                const float4 f1 = L.col[1][g], f2 = L.col[2][g], f3 = L.col[3][g], f4 = L.col[4][g];
+                const float4 f5 = L.col[5][g], f6 = L.col[6][g], f7 = L.col[7][g];
+                const v3 acc = finish_acc(S, tr.r, tmax_any, occ, mk(f4.x, f4.y, f4.z), mk(f5.x, f5.y, f5.z),
+                                          mk(f6.x, f6.y, f6.z), f4.w != 0.0f, mk(f7.x, f7.y, f7.z));
+                ++n_sh;
+                const float4 cko = make_float4(f1.x + acc.x, f1.y + acc.y, f1.z + acc.z, f1.w);
+                const uint32_t b3 = bits_from_f(f3.w);
+                if (b3 & 0x80000000u) {
+                    L.col[1][g] = cko;
+                    L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits((b3 & 0xFFFFu) + 1u));
+                    Ray nr;
+                    nr.o = mk(f2.x, f2.y, f2.z);
+                    nr.d = mk(f3.x, f3.y, f3.z);
+                    trav_setup(tr, nr);
+                    any = false;
+                    state = PS_BEGIN;
+                } else {
+                    Wv.CK[bits_from_f(f2.w)] = cko;
+                    state = PS_NEW;
+                }
+            }
+            const unsigned long long want = __ballot(state == PS_NEW);
+            if (want != 0ull) {  // wave-uniform: claim camera paths for the lanes whose path ended
+                uint32_t my = 0, pid = 0;
+                bool got = false;
+                if (!exhausted) got = cl.claim(want, my, exhausted);
+                if (state == PS_NEW) {
+                    if (got && cl.phys(my, pid)) {
+                        uint32_t key;
+                        const Ray r = camera_path(S, Wv, pid, key);
+                        L.col[0][g] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));
+                        L.col[1][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));
+                        L.col[2][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(pid));
+                        L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(0u));
+                        trav_setup(tr, r);
+                        any = false;
+                        state = PS_BEGIN;
+                    } else if (exhausted) {
+                        state = PS_DONE;
+                    }
+                }
+            }
+            if (state == PS_BEGIN) {
+                lf.left = 0;
+                if (!any) {  // k_extend's ray start (a NaN ray: no hit)
+                    h.t = FLT_MAX_;
+                    h.slot = -1;
+                    const bool go = !ray_has_nan(tr.r) && trav2_begin<false>(S, tr, h.t, stk, mode, c, lf, st);
+                    state = go ? PS_TRAV : PS_FIN;
+                } else {  // k_shadow's
+                    occ = false;
+                    if (x_slab_nan(tr)) {
+                        occ = any_hit_x_nan(S, tr.r);
+                        state = PS_FIN;
+                    } else {
+                        state = trav2_begin<false>(S, tr, tmax_any, stk, mode, c, lf, st) ? PS_TRAV : PS_FIN;
+                    }
+                }
+            }
+            if (__ballot(state == PS_FIN || state == PS_BEGIN || state == PS_NEW) == 0ull) break;
+        }
+        if (__ballot(state == PS_TRAV) == 0ull) break;  // every lane done: no path left
+        // ---- traversal: one record per lane per iteration, closest or any hit per lane
+        for (;;) {
+            if (state == PS_TRAV) {
+                bool o2 = false;
+                const bool f = WIDE ? iterwk<2, false>(S, tr, h, tmax_any, stk, mode, c, lf, st, o2, any)
+                                    : iter2k<2, false>(S, tr, h, tmax_any, stk, mode, c, lf, st, o2, any);
+                if (f) {
+                    state = PS_FIN;
+                    occ = o2;
+                }
+            }
+            const uint32_t ntrav = (uint32_t)__popcll(__ballot(state == PS_TRAV));
+            const uint32_t nfin = (uint32_t)__popcll(__ballot(state == PS_FIN));
+            // refill at REFILL finished lanes; once every path is claimed, as soon as
+            // the finished lanes are as many as those still traversing (the tail)
+            const uint32_t thr = exhausted ? (ntrav < (uint32_t)REFILL ? (ntrav > 0u ? ntrav : 1u) : (uint32_t)REFILL)
+                                           : (uint32_t)REFILL;
+            if (ntrav == 0u || nfin >= thr) break;
+        }
+    }
+    const unsigned long long se = wave_sum((unsigned long long)n_ext), ss = wave_sum((unsigned long long)n_sh);
+    if (lane_id() == 0) {
+        atomicAdd(&Wv.cnt->ext_rays, se);
+        atomicAdd(&Wv.cnt->sh_rays, ss);
+    }
+}
+
+static void launch_path(bool tex, bool wide, int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp,
+                        const PathLanes& L) {
+    const dim3 g(grid), b(TRAV_BLOCK);
+    if (tex) {
+        if (wide) hipLaunchKernelGGL((k_path<true, true>), g, b, PATH_LDS_BYTES, s, S, W, sp, L);
+        else hipLaunchKernelGGL((k_path<true, false>), g, b, PATH_LDS_BYTES, s, S, W, sp, L);
+    } else {
+        if (wide) hipLaunchKernelGGL((k_path<false, true>), g, b, PATH_LDS_BYTES, s, S, W, sp, L);
+        else hipLaunchKernelGGL((k_path<false, false>), g, b, PATH_LDS_BYTES, s, S, W, sp, L);
+    }
+}
+
 // ---- accumulate: PathTracer::drawTexture running mean (CPU_PathTracer.cpp:61-90) -------
 
 // Fused frames are accumulated one frame per launch (fr), in call order.
@@ -1649,6 +2004,7 @@ struct PathSet {
     DevMem heavyb;
     DevMem permb, hkeyb, hclsb;   // shade_order 1
     DevMem lvb;                   // light-path variant: subpath vertices of a chunk's sample slots
+    DevMem plane, pspill;         // k_path: per-lane path state columns, traversal-stack spill columns
     size_t sh_cap = 0;            // shadow-record capacity per parity (cap x connections per path)
     hipStream_t sA = nullptr, sB = nullptr;
 };
@@ -1749,6 +2105,7 @@ struct khp_ctx {
     std::vector<TimedLaunch> launches;
     int grid_ext = 0, grid_ext_w = 0, grid_ext_cam = 0, grid_sh = 0, grid_shade = 0;  // k_extend: 64-B, wide, bounce 0
     int grid_sh_w = 0;     // k_shadow on the two-level records
+    int grid_path = 0, grid_path_w = 0;   // k_path (64-B / two-level records)
     int grid_ext_max = 0;  // the k_extend spill columns are sized for the largest grid
     khp_stats st{};
     // rccl gather: pixel lists cached per (W, H, tile, nranks, rank, root)
@@ -1882,6 +2239,7 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->serial_stages = 0;
     out->path_order = 1;       // pixel-major fused chunks, +5-7%
     out->wide_from = KHP_WIDE_FROM;  // two-level records from bounce 2
+    out->path_kernel = 0;       // automatic: k_path for synchronous renders
 }
 
 extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {
@@ -1901,6 +2259,7 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     if (prm->shade_order > 1) return fail(KHP_EINVAL, "shade_order must be 0 or 1");
     if (prm->serial_stages > 1) return fail(KHP_EINVAL, "serial_stages must be 0 or 1");
     if (prm->path_order > 1) return fail(KHP_EINVAL, "path_order must be 0 or 1");
+    if (prm->path_kernel > 2) return fail(KHP_EINVAL, "path_kernel must be 0, 1 or 2");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
     if (dr != KHP_OK) return dr;
@@ -2303,6 +2662,14 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<true, false>), 256, 0));
     else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false>), 256, 0));
     c->grid_shade = std::max(1, nb) * c->n_cu;
+    nb = 0;
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, false>), TRAV_BLOCK, PATH_LDS_BYTES));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, false>), TRAV_BLOCK, PATH_LDS_BYTES));
+    c->grid_path = std::max(1, nb) * c->n_cu;
+    nb = 0;
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, true>), TRAV_BLOCK, PATH_LDS_BYTES));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, true>), TRAV_BLOCK, PATH_LDS_BYTES));
+    c->grid_path_w = std::min(c->grid_path, std::max(1, nb) * c->n_cu);   // the columns are sized by grid_path
     c->built = true;
     return KHP_OK;
 }
@@ -2727,6 +3094,20 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         HIPCHK(w.lvb.ensure(lv_bytes));
     }
     const int dump_b = (!async && !ops) ? c->prm.dump_bounce : -1;
+    // the path kernel (khp_ctx_params.path_kernel): automatic for synchronous renders
+    const bool path_ok = !stats && !bdm && c->prm.shade_order == 0 && dump_b < 0;
+    const bool use_path = path_ok && (c->prm.path_kernel == 2 || (c->prm.path_kernel == 0 && !async));
+    const bool path_wide = use_path && c->S.wide != nullptr && c->prm.wide_from == 0;
+    PathLanes PL{};
+    SpillArea sp_path{nullptr, 0};
+    if (use_path) {
+        const size_t lanes = (size_t)c->grid_path * TRAV_BLOCK;
+        HIPCHK(w.plane.ensure(lanes * 8 * sizeof(float4)));
+        HIPCHK(w.pspill.ensure(lanes * STACK_MAX * sizeof(int4)));
+        for (int k = 0; k < 8; ++k) PL.col[k] = w.plane.as<float4>() + (size_t)k * lanes;
+        sp_path = SpillArea{w.pspill.as<int4>(), (uint32_t)lanes};
+    }
+    const int grid_path = std::max(1, (path_wide ? c->grid_path_w : c->grid_path) / G);
     if (stats) {
         const size_t chunks = (size_t)((P_all + P_chunk - 1) / P_chunk) * ((p->spp + S_chunk - 1) / S_chunk);
         HIPCHK(c->snap.ensure(std::max<size_t>(1, chunks * p->depth) * sizeof(Counters)));
@@ -2790,8 +3171,16 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
             Wv.n_frames = nf;
             for (uint32_t q = 0; q < nf; ++q) Wv.fsample0[q] = fs0[q] + s0;
             const uint32_t npaths = P * ns * nf;
+            if (use_path) {  // every bounce of the chunk's paths in one launch; then the accumulate below
+                HIPCHK(hipMemsetAsync(reinterpret_cast<char*>(Wv.cnt) + offsetof(Counters, fetch_ext), 0,
+                                      sizeof(Counters::fetch_ext), sA));
+                timed(c, f, 3, true, sA);
+                launch_path(c->S.textured != 0, path_wide, grid_path, sA, c->S, Wv, sp_path, PL);
+                timed(c, f, 3, false, sA);
+            }
             timed(c, f, 3, true, sA);
-            if (Wv.cam0) hipLaunchKernelGGL(k_start, dim3(1), dim3(1), 0, sA, Wv.cnt, npaths);
+            if (use_path) {
+            } else if (Wv.cam0) hipLaunchKernelGGL(k_start, dim3(1), dim3(1), 0, sA, Wv.cnt, npaths);
             else hipLaunchKernelGGL(k_generate, dim3((npaths + 255) / 256), dim3(256), 0, sA, c->S, Wv);
             if (bdm) {  // the light subpaths of this chunk's sample slots (frames x samples)
                 const uint32_t nsub = nf * ns * c->bd.light_paths * (uint32_t)c->S.n_lights;
@@ -2815,7 +3204,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 timed(c, f, 4, false, sA);
             }
             hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
-            for (uint32_t b = 0; b < p->depth; ++b) {
+            for (uint32_t b = 0; b < (use_path ? 0u : p->depth); ++b) {
                 const int cur = b & 1;
                 c->cur_bounce = (int)b;
                 Wave Wb = Wv;

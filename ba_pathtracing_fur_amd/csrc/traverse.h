@@ -473,12 +473,28 @@ __device__ __forceinline__ bool trav2_begin(const DevScene& S, const TravRay& tr
     return true;
 }
 
-// One wave iteration of one lane (mode != M_IDLE).  ANY: any-hit with the
-// fixed limit tlimit = the ray's tMax; else closest hit, tlimit = h.t.
-// Returns true when the ray is finished; for ANY, `occluded` tells the result.
-template <bool ANY, bool STATS, class Stack>
-__device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
-                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
+// A candidate of a leaf for a lane whose query kind is a per-lane value (the
+// path kernel traces closest-hit and any-hit rays in one loop): the same test
+// as leaf_candidate_t (any = false, window tMax = the leaf's) or any_candidate
+// (any = true, tMax = the ray's), with one instruction stream for both.
+__device__ __forceinline__ bool candidate_rt(float4 p0, float4 p1, float4 p2, float4 p3, const Ray& r, bool any,
+                                             float tMax, float& t) {
+    if (is_tri(p0)) {
+        float u, v;
+        return tri_test(p0, p1, p2, r, 0.0f, tMax, t, u, v);
+    }
+    return cone_quadratic(p0, p1, p2, p3, r, any, 0.0f, tMax, t);
+}
+
+// One wave iteration of one lane (mode != M_IDLE).  KIND 1: any-hit with the
+// fixed limit tlimit = the ray's tMax; KIND 0: closest hit, tlimit = h.t;
+// KIND 2: the lane's any_rt decides (the path kernel).  Returns true when the
+// ray is finished; for an any-hit query, `occluded` tells the result.
+template <int KIND, bool STATS, class Stack>
+__device__ __forceinline__ bool iter2k(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
+                                       uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded,
+                                       bool any_rt) {
+    const bool ANY = KIND == 2 ? any_rt : KIND == 1;
     const bool in_leaf = mode == M_LEAF;
     const bool fetch = in_leaf || mode == M_NODE;
     const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
@@ -499,7 +515,18 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
     float pt0 = 0.0f, pt1 = 0.0f;
     if (in_leaf) {
         if (STATS) st.prims++;
-        if (ANY) {
+        if (KIND == 2) {
+            float t = 0.0f;
+            const bool ok = candidate_rt(q0, q1, q2, q3, tr.r, ANY, ANY ? tmax_any : lf.tmax, t);
+            if (ok && ANY) {
+                occluded = true;
+                return true;
+            }
+            if (ok) {
+                lf.sl = (int32_t)lf.slot;
+                lf.tmax = t;
+            }
+        } else if (ANY) {
             if (any_candidate(q0, q1, q2, q3, tr.r, tmax_any)) {
                 occluded = true;
                 return true;
@@ -562,6 +589,12 @@ __device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit&
     return false;
 }
 
+template <bool ANY, bool STATS, class Stack>
+__device__ __forceinline__ bool iter2(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
+                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
+    return iter2k<ANY ? 1 : 0, STATS>(S, tr, h, tmax_any, stk, mode, c, lf, st, occluded, ANY);
+}
+
 // ---- two-level node records (k_extend from bounce wide_from; k_shadow from bounce 2) -------
 // The wide record of interior node X (one 128-B line, `DevScene::wide`, same
 // index as X's 64-B record) holds, for each child C of X, either the boxes and
@@ -612,15 +645,18 @@ __device__ __forceinline__ float wmax(float a, float b) { return (a < b) ? b : a
 // iter2's.  ANY: any hit with the fixed limit tmax_any (the ray's tMax; KIRK's
 // any-hit walk has the same near-first order and prune test,
 // CPU_BVH.cpp:211-265), else closest hit with tlimit = h.t.  Returns true when
-// the ray is finished; for ANY, `occluded` tells the result.
-template <bool ANY, bool STATS, class Stack>
-__device__ __forceinline__ bool iterw(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
-                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
+// the ray is finished; for ANY, `occluded` tells the result.  KIND as iter2k.
+template <int KIND, bool STATS, class Stack>
+__device__ __forceinline__ bool iterwk(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
+                                       uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded,
+                                       bool any_rt) {
+    const bool ANY = KIND == 2 ? any_rt : KIND == 1;
     // A wave with a ray whose origin or inverse direction is not finite on
     // every axis (an exactly axis-parallel direction) runs this iteration as
     // the one-level step on the 64-B records (same entries, same stack): the
     // composed slab needs the fast form's monotone plane distances.
-    if (__ballot(!tr.fin) != 0ull) return iter2<ANY, STATS>(S, tr, h, tmax_any, stk, mode, c, lf, st, occluded);
+    if (__ballot(!tr.fin) != 0ull)
+        return iter2k<KIND, STATS>(S, tr, h, tmax_any, stk, mode, c, lf, st, occluded, any_rt);
     const bool in_leaf = mode == M_LEAF;
     const bool node = mode == M_NODE;
     const bool fetch = in_leaf || node;
@@ -653,7 +689,18 @@ __device__ __forceinline__ bool iterw(const DevScene& S, const TravRay& tr, Hit&
     float p1t0 = 0.0f, p1t1 = 0.0f, p2t0 = 0.0f, p2t1 = 0.0f;
     if (in_leaf) {
         if (STATS) st.prims++;
-        if (ANY) {
+        if (KIND == 2) {
+            float t = 0.0f;
+            const bool ok = candidate_rt(q0, q1, q2, q3, tr.r, ANY, ANY ? tmax_any : lf.tmax, t);
+            if (ok && ANY) {
+                occluded = true;
+                return true;
+            }
+            if (ok) {
+                lf.sl = (int32_t)lf.slot;
+                lf.tmax = t;
+            }
+        } else if (ANY) {
             if (any_candidate(q0, q1, q2, q3, tr.r, tmax_any)) {
                 occluded = true;
                 return true;
@@ -749,6 +796,12 @@ __device__ __forceinline__ bool iterw(const DevScene& S, const TravRay& tr, Hit&
     }
     if (have) take_entry<STATS>(S, eref, et0, et1, mode, c, lf, st);
     return false;
+}
+
+template <bool ANY, bool STATS, class Stack>
+__device__ __forceinline__ bool iterw(const DevScene& S, const TravRay& tr, Hit& h, float tmax_any, Stack& stk,
+                                      uint32_t& mode, Cur& c, LeafCur& lf, TravStats& st, bool& occluded) {
+    return iterwk<ANY ? 1 : 0, STATS>(S, tr, h, tmax_any, stk, mode, c, lf, st, occluded, ANY);
 }
 
 // Whole-ray forms (batch query kernels).

@@ -300,6 +300,13 @@ typedef struct {
                                     64-B records.  Default 2 (measured); >= depth: never.
                                     The shadow stage (any hit) of bounce b uses them when b >= max(wide_from,
                                     2).  Batch queries with trace_kernels use them iff wide_from == 0   */
+    uint32_t path_kernel;        /* ABI 11: 0 (default) automatic, 1 never, 2 whenever supported: run a chunk's
+                                    paths through all their bounces in ONE persistent launch (k_path: a lane
+                                    traces, shades, traces the shadow ray and continues with the next bounce)
+                                    instead of the per-bounce wavefront, whose every launch ends with its
+                                    slowest ray.  Automatic: synchronous renders (KIRK's own one-call-per-pass
+                                    use).  Not with the light-path variant, hit sorting, instrumented renders
+                                    or queue dumps (those always run the wavefront).  Measured in DESIGN.md */
 } khp_ctx_params;
 
 /* ---- context --------------------------------------------------------------- */

@@ -629,3 +629,52 @@ def test_wide_records_frames(hip_ctx, name, kw, w, h, spp, depth):
     finally:
         hip_ctx.set_params(**old)
     assert len(counts) == 1
+
+
+PK_CASES = [CASES[0], CASES[1], CASES[2], CASES[3], CASES[4], CASES[5], CASES[8]]
+
+
+@pytest.mark.parametrize("name,kw,w,h,spp,depth", PK_CASES,
+                         ids=[f"{c[0]}-{c[1].get('bsdf', '')}{c[1].get('env', '')}{c[1].get('n_strands', '')}"
+                              for c in PK_CASES])
+def test_path_kernel_frames(name, kw, w, h, spp, depth):
+    """khp_ctx_params.path_kernel (ABI 11): k_path, every bounce of a path in one
+    persistent launch, on the 64-B and the two-level records, synchronous and
+    fused asynchronous passes, gives the oracle's frame bit for bit -- the same
+    frame the per-bounce wavefront (path_kernel 1) gives."""
+    sd = S.build_config(name, width=w, height=h, **kw)
+    want = oracle_ffi.Oracle(sd).render(w, h, 2 * spp, depth, threads=16)
+    ctx = HipContext(0)
+    try:
+        ctx.set_scene(sd)
+        ctx.build_accel()
+        for pk, wide in ((1, 2), (2, 2), (2, 0), (0, 2)):
+            ctx.set_params(path_kernel=pk, wide_from=wide)
+            ctx.render(w, h, spp, depth, readback=False)                     # synchronous pass
+            ctx.render(w, h, spp, depth, first_sample=spp, readback=False)
+            assert_parity(ctx.read_framebuffer(w, h), want, exact=True)
+            for k in range(2):                                                # fused asynchronous passes
+                ctx.render(w, h, spp, depth, first_sample=k * spp, async_=True)
+            ctx.sync()
+            assert_parity(ctx.read_framebuffer(w, h), want, exact=True)
+    finally:
+        ctx.close()
+
+
+def test_path_kernel_full_size(metric_oracle):
+    """The metric scene (1M strands, 1080p) through k_path: one synchronous 1-spp
+    pass (KIRK's GUI call, path_kernel automatic) equals the wavefront's frame bit
+    for bit, and every 27th row is the oracle's."""
+    ctx = HipContext(0)
+    try:
+        S.config3_device(ctx, 1920, 1080, n_strands=1_000_000)
+        ctx.build_accel()
+        got = ctx.render(1920, 1080, 1, 5)
+        ctx.set_params(path_kernel=1)
+        wf = ctx.render(1920, 1080, 1, 5)
+    finally:
+        ctx.close()
+    assert np.array_equal(got.view(np.uint32), wf.view(np.uint32))
+    rows = list(range(13, 1080, 27))
+    want = metric_oracle.render(1920, 1080, 1, 5, threads=16, rows=(13, 1080, 27))
+    assert_parity(got[rows], want[rows], exact=True)

@@ -2,7 +2,7 @@
 
 Input: the kernel_trace.csv (and memory_copy_trace.csv, if present) of
 tools/sync_trace.py, plus its JSON line.  A call starts at its k_start (or
-k_generate) dispatch.  Per call: the device span (first kernel start to the
+k_generate, or k_path) dispatch.  Per call: the device span (first kernel start to the
 last kernel/copy end), the time some kernel or copy was running (union), the
 idle time inside the span (host waits, launch gaps), and the launches by
 kernel with their summed durations; k_extend / k_shadow durations per bounce.
@@ -47,7 +47,7 @@ def main():
     for r in cps:
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy:" + r.get("Direction", "?")))
     ev.sort()
-    starts = [i for i, e in enumerate(ev) if e[2] in ("k_start", "k_generate")]
+    starts = [i for i, e in enumerate(ev) if e[2] in ("k_start", "k_generate", "k_path")]
     n_calls = len(calls["gui"]) + len(calls["sync"])
     starts = starts[-n_calls:]
     names = ["gui"] * len(calls["gui"]) + ["sync"] * len(calls["sync"])
