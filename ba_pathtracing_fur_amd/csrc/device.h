@@ -521,6 +521,10 @@ __device__ __forceinline__ v3 hair_r(const ShadeCtx& s, v3 in, v3 n, float sampl
 // Inlined into k_shade: measured 2.02 -> 1.66 ms per frame against a real call
 // (whose frame spilled 41 SGPRs and 112 B of scratch), +0.7% at the metric row
 // (profiles/r02p_bsdf_inline.json).
+// KINDS: the BSDF kinds the scene's materials use (bit k = khp_bsdf_kind k), a
+// compile-time set: the other cases are compiled out (their registers with
+// them).  The host instantiates a kernel whose set covers every material.
+template <uint32_t KINDS = 0xFFFFFFFFu>
 __device__ __forceinline__
 v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float h1, v3& out,
                                        float& pdf, int& flags, bool& valid) {
@@ -537,6 +541,7 @@ v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float 
     v3 vol = mk(m->volume[0], m->volume[1], m->volume[2]);
     switch (m->bsdf) {
         case KHP_BSDF_LAMBERTIAN_REFLECTION: {  // :186-195
+            if constexpr (!(KINDS & (1u << KHP_BSDF_LAMBERTIAN_REFLECTION))) __builtin_unreachable();
             bool entering = dot(in, n) > 0.0f;
             v3 h = cosine_hemi(sample[0], sample[1]);
             out = local_to_world_normal(entering ? h : -h, n);
@@ -546,12 +551,14 @@ v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float 
             return diff * ONE_OVER_PI;
         }
         case KHP_BSDF_SPECULAR_REFLECTION: {  // :210-217
+            if constexpr (!(KINDS & (1u << KHP_BSDF_SPECULAR_REFLECTION))) __builtin_unreachable();
             out = reflect(-in, faceforward(n, -in, n));
             pdf = 1.0f;
             flags |= F_SPECULAR;
             return spec / fabsf(dot(out, n));
         }
         case KHP_BSDF_GLOSSY: {  // :227-245
+            if constexpr (!(KINDS & (1u << KHP_BSDF_GLOSSY))) __builtin_unreachable();
             float rad = (180.0f - (1.0f - m->roughness) * 180.0f) * DEG2RAD;
             v3 refl = reflect(-in, faceforward(n, -in, n));
             v3 sp = sample_angle(sample[0], sample[1], rad);
@@ -562,6 +569,7 @@ v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float 
             return spec / fabsf(dot(out, n));
         }
         case KHP_BSDF_SPECULAR_TRANSMISSION: {  // :258-288
+            if constexpr (!(KINDS & (1u << KHP_BSDF_SPECULAR_TRANSMISSION))) __builtin_unreachable();
             bool entering = dot(in, n) > 0.0f;
             float ei = entering ? 1.0f : m->ior, et = entering ? m->ior : 1.0f;
             float F = fresnel_dielectric(fabsf(dot(in, n)), ei, et);
@@ -577,6 +585,7 @@ v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float 
             return zero;
         }
         case KHP_BSDF_LAMBERTIAN_TRANSMISSION: {  // :298-308
+            if constexpr (!(KINDS & (1u << KHP_BSDF_LAMBERTIAN_TRANSMISSION))) __builtin_unreachable();
             bool entering = dot(in, n) > 0.0f;
             v3 h = cosine_hemi(sample[0], sample[1]);
             out = local_to_world_normal(entering ? -h : h, n);
@@ -586,6 +595,7 @@ v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float 
             return vol * ONE_OVER_PI;
         }
         case KHP_BSDF_GLASS: {  // :326-357
+            if constexpr (!(KINDS & (1u << KHP_BSDF_GLASS))) __builtin_unreachable();
             bool entering = dot(in, n) > 0.0f;
             float ei = entering ? 1.0f : m->ior, et = entering ? m->ior : 1.0f;
             float F = fresnel_dielectric(fabsf(dot(normalize(in), n)), ei, et);
@@ -604,6 +614,7 @@ v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float 
             return (spec * F) / fabsf(dot(out, n));
         }
         case KHP_BSDF_MILK_GLASS: {  // :367-416
+            if constexpr (!(KINDS & (1u << KHP_BSDF_MILK_GLASS))) __builtin_unreachable();
             bool entering = dot(in, n) > 0.0f;
             float ei = entering ? 1.0f : m->ior, et = entering ? m->ior : 1.0f;
             v3 nin = normalize(in);
@@ -630,18 +641,22 @@ v3 bsdf_sample(const ShadeCtx& s, v3 in, v3 n, float sample[2], float h0, float 
             return (spec * F) / fabsf(dot(out, n));
         }
         case KHP_BSDF_EMISSION:  // :427-435
+            if constexpr (!(KINDS & (1u << KHP_BSDF_EMISSION))) __builtin_unreachable();
             pdf = 1.0f;
             out = zero;
             flags = F_EMISSIVE;
             return mk(1.0f, 1.0f, 1.0f);
         case KHP_BSDF_TRANSPARENT:  // :445-454
+            if constexpr (!(KINDS & (1u << KHP_BSDF_TRANSPARENT))) __builtin_unreachable();
             out = -in;
             flags = F_TRANSPARENT | F_SPECULAR;
             pdf = 1.0f;
             return vol / fabsf(dot(out, n));
         case KHP_BSDF_MARSCHNER_HAIR:
+            if constexpr (!(KINDS & (1u << KHP_BSDF_MARSCHNER_HAIR))) __builtin_unreachable();
             return hair_r<false>(s, in, n, sample, h0, h1, out, pdf, flags);
         case KHP_BSDF_DEON_HAIR:
+            if constexpr (!(KINDS & (1u << KHP_BSDF_DEON_HAIR))) __builtin_unreachable();
             return hair_r<true>(s, in, n, sample, h0, h1, out, pdf, flags);
         default:
             out = mk(0.0f, 0.0f, 1.0f);

@@ -13,6 +13,7 @@
 // counts stay on the device, so a frame is enqueued without host syncs.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -887,7 +888,7 @@ __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3,
 #ifndef KHP_SHADE_WAVES
 #define KHP_SHADE_WAVES 1   // min waves per SIMD for k_shade's register budget (1: unconstrained)
 #endif
-template <bool TEX, bool BD>
+template <bool TEX, bool BD, uint32_t KINDS = 0xFFFFFFFFu>
 __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
     const uint32_t nf = Wv.cnt->nq[cur], n = nf + Wv.cnt->nqb[cur];
     const int nxt = cur ^ 1;
@@ -996,7 +997,7 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
                     v3 out;
                     float pdf = 0.0f;
                     bool valid;
-                    v3 refl = bsdf_sample(s, counter, nrm, smp, h0, h1, out, pdf, flags, valid);
+                    v3 refl = bsdf_sample<KINDS>(s, counter, nrm, smp, h0, h1, out, pdf, flags, valid);
                     v3 off = out * 1e-4f;
                     if (!(flags & F_SPECULAR)) off = faceforward(-(nrm * 1e-4f), nrm, out);
                     nr = make_ray(loc + off, out);
@@ -1013,7 +1014,7 @@ __global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave
                     float pdf = 0.0f;
                     int fl = 0;
                     bool valid;
-                    v3 refl = bsdf_sample(s, counter, nrm, smp, h0, h1, out, pdf, fl, valid);
+                    v3 refl = bsdf_sample<KINDS>(s, counter, nrm, smp, h0, h1, out, pdf, fl, valid);
                     if (is_zero(refl) || pdf <= 1E-4f || gmax(T.x, gmax(T.y, T.z)) < 0.01f) {
                         T = mk(0, 0, 0);
                     } else if ((fl & F_EMISSIVE) == F_EMISSIVE) {
@@ -1336,9 +1337,13 @@ static void launch_shadow(bool stats, bool wide, int grid, hipStream_t s, const 
 #define KHP_PATH_WAVES 4
 #endif
 #ifndef KHP_PATH_RING
-#define KHP_PATH_RING 8
+#define KHP_PATH_RING 6   // with the parked state (9.5 KB per wave) 16 waves fit a CU's LDS
+#endif
+#ifndef KHP_PATH_REFILL
+#define KHP_PATH_REFILL 24
 #endif
 constexpr int PATH_WAVES = KHP_PATH_WAVES;
+constexpr uint32_t PATH_REFILL = KHP_PATH_REFILL;   // finished lanes that trigger a wave's service
 constexpr int PATH_RING = KHP_PATH_RING;
 constexpr size_t PATH_LDS_BYTES = 3 * PATH_RING * TRAV_BLOCK * sizeof(uint32_t);
 
@@ -1365,7 +1370,7 @@ struct ShadeOut {
     v3 lc, Told, AT, ET;
     bool has_emit;
 };
-template <bool TEX>
+template <bool TEX, uint32_t KINDS>
 __device__ __forceinline__ void shade_core(const DevScene& S, const Ray& r, float lambda, int32_t slot, v3 T, v3 C,
                                            int flags, uint32_t key, uint32_t bounce, bool last, ShadeOut& o) {
     o.nr.o = o.nr.d = mk(0, 0, 0);
@@ -1433,7 +1438,7 @@ __device__ __forceinline__ void shade_core(const DevScene& S, const Ray& r, floa
             v3 out;
             float pdf = 0.0f;
             bool valid;
-            v3 refl = bsdf_sample(s, counter, nrm, smp, h0, h1, out, pdf, flags, valid);
+            v3 refl = bsdf_sample<KINDS>(s, counter, nrm, smp, h0, h1, out, pdf, flags, valid);
             v3 off = out * 1e-4f;
             if (!(flags & F_SPECULAR)) off = faceforward(-(nrm * 1e-4f), nrm, out);
             o.nr = make_ray(loc + off, out);
@@ -1450,7 +1455,7 @@ __device__ __forceinline__ void shade_core(const DevScene& S, const Ray& r, floa
             float pdf = 0.0f;
             int fl = 0;
             bool valid;
-            v3 refl = bsdf_sample(s, counter, nrm, smp, h0, h1, out, pdf, fl, valid);
+            v3 refl = bsdf_sample<KINDS>(s, counter, nrm, smp, h0, h1, out, pdf, fl, valid);
             if (is_zero(refl) || pdf <= 1E-4f || gmax(T.x, gmax(T.y, T.z)) < 0.01f) {
                 T = mk(0, 0, 0);
             } else if ((fl & F_EMISSIVE) == F_EMISSIVE) {
@@ -1509,9 +1514,24 @@ __device__ __forceinline__ v3 finish_acc(const DevScene& S, const Ray& r, float 
 
 enum : uint32_t { PS_TRAV = 0u, PS_FIN = 1u, PS_NEW = 2u, PS_BEGIN = 3u, PS_DONE = 4u };
 
-template <bool TEX, bool WIDE>
+// PARK: while a wave services its finished lanes, every lane's traversal state
+// (20 dwords: ray, hit, cursor, leaf cursor, mode, any-hit limit, flags, stack
+// depth) is parked in LDS, [field][lane], and reloaded after -- so the
+// traversal registers are not live through the shading code, which otherwise
+// holds them for the lanes still traversing (128 VGPRs + scratch without it).
+constexpr int PARK_FIELDS = 20;
+constexpr size_t path_lds_bytes(bool park) {
+    return PATH_LDS_BYTES + (park ? (size_t)PARK_FIELDS * TRAV_BLOCK * sizeof(uint32_t) : 0);
+}
+enum : int { PF_O = 0, PF_D = 3, PF_HT = 6, PF_HSLOT = 7, PF_CREF = 8, PF_CT0 = 9, PF_CT1 = 10, PF_LSLOT = 11,
+             PF_LLEFT = 12, PF_LTMAX = 13, PF_LSL = 14, PF_MODE = 15, PF_TMAX = 16, PF_FLAGS = 17, PF_SP = 18,
+             PF_LO = 19 };
+
+template <bool TEX, bool WIDE, bool PARK, uint32_t KINDS>
 __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wave Wv, SpillArea spill, PathLanes L) {
     extern __shared__ uint32_t lds[];
+    uint32_t* park = lds + 3 * PATH_RING * TRAV_BLOCK;
+    auto pk = [&](int f) -> uint32_t& { return park[f * TRAV_BLOCK + threadIdx.x]; };
     const uint32_t npaths = Wv.P * Wv.n_samples * Wv.n_frames;
     const uint32_t g = blockIdx.x * TRAV_BLOCK + threadIdx.x;
     LdsStack<PATH_RING, false> stk;
@@ -1529,63 +1549,95 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     Claimer cl;
     cl.init(Wv.cnt->fetch_ext, npaths, 0u, npaths);
     for (;;) {
+        if (PARK) {
+            pk(PF_O) = bits_from_f(tr.r.o.x); pk(PF_O + 1) = bits_from_f(tr.r.o.y); pk(PF_O + 2) = bits_from_f(tr.r.o.z);
+            pk(PF_D) = bits_from_f(tr.r.d.x); pk(PF_D + 1) = bits_from_f(tr.r.d.y); pk(PF_D + 2) = bits_from_f(tr.r.d.z);
+            pk(PF_HT) = bits_from_f(h.t); pk(PF_HSLOT) = (uint32_t)h.slot;
+            pk(PF_CREF) = c.ref; pk(PF_CT0) = bits_from_f(c.t0); pk(PF_CT1) = bits_from_f(c.t1);
+            pk(PF_LSLOT) = lf.slot; pk(PF_LLEFT) = lf.left; pk(PF_LTMAX) = bits_from_f(lf.tmax);
+            pk(PF_LSL) = (uint32_t)lf.sl; pk(PF_MODE) = mode; pk(PF_TMAX) = bits_from_f(tmax_any);
+            pk(PF_FLAGS) = (any ? 1u : 0u) | (occ ? 2u : 0u);
+            pk(PF_SP) = (uint32_t)stk.sp; pk(PF_LO) = (uint32_t)stk.lo;
+        }
         // ---- service: shade finished extension rays, finish shadow rays, claim camera
         //      paths, start traversals -- until every lane traverses or has no work left
         for (;;) {
-            if (state == PS_FIN && !any) {  // k_shade
-                const float4 f0 = L.col[0][g], f1 = L.col[1][g], f2 = L.col[2][g], f3 = L.col[3][g];
-                const uint32_t bounce = bits_from_f(f3.w) & 0xFFFFu;
-                ShadeOut o;
-                shade_core<TEX>(S, tr.r, h.t, h.slot, mk(f0.x, f0.y, f0.z), mk(f1.x, f1.y, f1.z),
-                                (int)bits_from_f(f0.w), bits_from_f(f1.w), bounce, bounce + 1 >= Wv.depth, o);
-                ++n_ext;
-                const float4 tfo = make_float4(o.T.x, o.T.y, o.T.z, f_from_bits((uint32_t)o.flags));
-                const float4 cko = make_float4(o.C.x, o.C.y, o.C.z, f1.w);
-                if (o.emit_sh) {
-                    L.col[0][g] = tfo;
-                    L.col[1][g] = cko;
-                    L.col[2][g] = make_float4(o.nr.o.x, o.nr.o.y, o.nr.o.z, f2.w);
-                    L.col[3][g] = make_float4(o.nr.d.x, o.nr.d.y, o.nr.d.z,
-                                              f_from_bits(bounce | (o.emit_ray ? 0x80000000u : 0u)));
-                    L.col[4][g] = make_float4(o.lc.x, o.lc.y, o.lc.z, o.has_emit ? 1.0f : 0.0f);
-                    L.col[5][g] = make_float4(o.Told.x, o.Told.y, o.Told.z, 0.0f);
-                    L.col[6][g] = make_float4(o.AT.x, o.AT.y, o.AT.z, 0.0f);
-                    L.col[7][g] = make_float4(o.ET.x, o.ET.y, o.ET.z, 0.0f);
-                    trav_setup(tr, o.shr);
-                    tmax_any = o.sh_tmax;
-                    any = true;
-                    state = PS_BEGIN;
-                } else if (o.emit_ray) {
-                    L.col[0][g] = tfo;
-                    L.col[1][g] = cko;
-                    L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(bounce + 1u));
-                    trav_setup(tr, o.nr);
-                    any = false;
-                    state = PS_BEGIN;
+            Ray sray;          // the ray a lane starts next (PS_BEGIN)
+            bool sany = false;
+            float stmax = 0.0f;
+            sray.o = sray.d = mk(0, 0, 0);
+            if (state == PS_FIN) {
+                Ray fr;
+                float fht, ftmax;
+                int32_t fslot;
+                bool fany, focc;
+                if (PARK) {
+                    fr.o = mk(f_from_bits(pk(PF_O)), f_from_bits(pk(PF_O + 1)), f_from_bits(pk(PF_O + 2)));
+                    fr.d = mk(f_from_bits(pk(PF_D)), f_from_bits(pk(PF_D + 1)), f_from_bits(pk(PF_D + 2)));
+                    fht = f_from_bits(pk(PF_HT));
+                    fslot = (int32_t)pk(PF_HSLOT);
+                    ftmax = f_from_bits(pk(PF_TMAX));
+                    fany = (pk(PF_FLAGS) & 1u) != 0u;
+                    focc = (pk(PF_FLAGS) & 2u) != 0u;
                 } else {
-                    Wv.CK[bits_from_f(f2.w)] = cko;
-                    state = PS_NEW;
+                    fr = tr.r;
+                    fht = h.t;
+                    fslot = h.slot;
+                    ftmax = tmax_any;
+                    fany = any;
+                    focc = occ;
                 }
-            } else if (state == PS_FIN) {  // k_shadow_finish
-                const float4 f1 = L.col[1][g], f2 = L.col[2][g], f3 = L.col[3][g], f4 = L.col[4][g];
-                const float4 f5 = L.col[5][g], f6 = L.col[6][g], f7 = L.col[7][g];
-                const v3 acc = finish_acc(S, tr.r, tmax_any, occ, mk(f4.x, f4.y, f4.z), mk(f5.x, f5.y, f5.z),
-                                          mk(f6.x, f6.y, f6.z), f4.w != 0.0f, mk(f7.x, f7.y, f7.z));
-                ++n_sh;
-                const float4 cko = make_float4(f1.x + acc.x, f1.y + acc.y, f1.z + acc.z, f1.w);
-                const uint32_t b3 = bits_from_f(f3.w);
-                if (b3 & 0x80000000u) {
-                    L.col[1][g] = cko;
-                    L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits((b3 & 0xFFFFu) + 1u));
-                    Ray nr;
-                    nr.o = mk(f2.x, f2.y, f2.z);
-                    nr.d = mk(f3.x, f3.y, f3.z);
-                    trav_setup(tr, nr);
-                    any = false;
-                    state = PS_BEGIN;
-                } else {
-                    Wv.CK[bits_from_f(f2.w)] = cko;
-                    state = PS_NEW;
+                if (!fany) {  // k_shade
+                    const float4 f0 = L.col[0][g], f1 = L.col[1][g], f2 = L.col[2][g], f3 = L.col[3][g];
+                    const uint32_t bounce = bits_from_f(f3.w) & 0xFFFFu;
+                    ShadeOut o;
+                    shade_core<TEX, KINDS>(S, fr, fht, fslot, mk(f0.x, f0.y, f0.z), mk(f1.x, f1.y, f1.z),
+                                    (int)bits_from_f(f0.w), bits_from_f(f1.w), bounce, bounce + 1 >= Wv.depth, o);
+                    ++n_ext;
+                    const float4 tfo = make_float4(o.T.x, o.T.y, o.T.z, f_from_bits((uint32_t)o.flags));
+                    const float4 cko = make_float4(o.C.x, o.C.y, o.C.z, f1.w);
+                    if (o.emit_sh) {
+                        L.col[0][g] = tfo;
+                        L.col[1][g] = cko;
+                        L.col[2][g] = make_float4(o.nr.o.x, o.nr.o.y, o.nr.o.z, f2.w);
+                        L.col[3][g] = make_float4(o.nr.d.x, o.nr.d.y, o.nr.d.z,
+                                                  f_from_bits(bounce | (o.emit_ray ? 0x80000000u : 0u)));
+                        L.col[4][g] = make_float4(o.lc.x, o.lc.y, o.lc.z, o.has_emit ? 1.0f : 0.0f);
+                        L.col[5][g] = make_float4(o.Told.x, o.Told.y, o.Told.z, 0.0f);
+                        L.col[6][g] = make_float4(o.AT.x, o.AT.y, o.AT.z, 0.0f);
+                        L.col[7][g] = make_float4(o.ET.x, o.ET.y, o.ET.z, 0.0f);
+                        sray = o.shr;
+                        stmax = o.sh_tmax;
+                        sany = true;
+                        state = PS_BEGIN;
+                    } else if (o.emit_ray) {
+                        L.col[0][g] = tfo;
+                        L.col[1][g] = cko;
+                        L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(bounce + 1u));
+                        sray = o.nr;
+                        state = PS_BEGIN;
+                    } else {
+                        Wv.CK[bits_from_f(f2.w)] = cko;
+                        state = PS_NEW;
+                    }
+                } else {  // k_shadow_finish
+                    const float4 f1 = L.col[1][g], f2 = L.col[2][g], f3 = L.col[3][g], f4 = L.col[4][g];
+                    const float4 f5 = L.col[5][g], f6 = L.col[6][g], f7 = L.col[7][g];
+                    const v3 acc = finish_acc(S, fr, ftmax, focc, mk(f4.x, f4.y, f4.z), mk(f5.x, f5.y, f5.z),
+                                              mk(f6.x, f6.y, f6.z), f4.w != 0.0f, mk(f7.x, f7.y, f7.z));
+                    ++n_sh;
+                    const float4 cko = make_float4(f1.x + acc.x, f1.y + acc.y, f1.z + acc.z, f1.w);
+                    const uint32_t b3 = bits_from_f(f3.w);
+                    if (b3 & 0x80000000u) {
+                        L.col[1][g] = cko;
+                        L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits((b3 & 0xFFFFu) + 1u));
+                        sray.o = mk(f2.x, f2.y, f2.z);
+                        sray.d = mk(f3.x, f3.y, f3.z);
+                        state = PS_BEGIN;
+                    } else {
+                        Wv.CK[bits_from_f(f2.w)] = cko;
+                        state = PS_NEW;
+                    }
                 }
             }
             const unsigned long long want = __ballot(state == PS_NEW);
@@ -1596,37 +1648,73 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                 if (state == PS_NEW) {
                     if (got && cl.phys(my, pid)) {
                         uint32_t key;
-                        const Ray r = camera_path(S, Wv, pid, key);
+                        sray = camera_path(S, Wv, pid, key);
                         L.col[0][g] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));
                         L.col[1][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));
                         L.col[2][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(pid));
                         L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(0u));
-                        trav_setup(tr, r);
-                        any = false;
+                        sany = false;
                         state = PS_BEGIN;
                     } else if (exhausted) {
                         state = PS_DONE;
                     }
                 }
             }
-            if (state == PS_BEGIN) {
-                lf.left = 0;
-                if (!any) {  // k_extend's ray start (a NaN ray: no hit)
-                    h.t = FLT_MAX_;
-                    h.slot = -1;
-                    const bool go = !ray_has_nan(tr.r) && trav2_begin<false>(S, tr, h.t, stk, mode, c, lf, st);
-                    state = go ? PS_TRAV : PS_FIN;
-                } else {  // k_shadow's
-                    occ = false;
-                    if (x_slab_nan(tr)) {
-                        occ = any_hit_x_nan(S, tr.r);
-                        state = PS_FIN;
-                    } else {
-                        state = trav2_begin<false>(S, tr, tmax_any, stk, mode, c, lf, st) ? PS_TRAV : PS_FIN;
-                    }
+            if (state == PS_BEGIN) {  // k_extend's / k_shadow's ray start
+                TravRay t2;
+                trav_setup(t2, sray);
+                Hit h2{FLT_MAX_, -1, 0.0f, 0.0f};
+                Cur c2{0u, 0.0f, 0.0f, false};
+                LeafCur l2{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
+                uint32_t m2 = 0u;
+                bool o2 = false, go;
+                if (!sany) {  // a NaN extension ray: no hit
+                    go = !ray_has_nan(sray) && trav2_begin<false>(S, t2, h2.t, stk, m2, c2, l2, st);
+                } else if (x_slab_nan(t2)) {
+                    o2 = any_hit_x_nan(S, sray);
+                    go = false;
+                } else {
+                    go = trav2_begin<false>(S, t2, stmax, stk, m2, c2, l2, st);
+                }
+                state = go ? PS_TRAV : PS_FIN;
+                if (PARK) {
+                    pk(PF_O) = bits_from_f(sray.o.x); pk(PF_O + 1) = bits_from_f(sray.o.y); pk(PF_O + 2) = bits_from_f(sray.o.z);
+                    pk(PF_D) = bits_from_f(sray.d.x); pk(PF_D + 1) = bits_from_f(sray.d.y); pk(PF_D + 2) = bits_from_f(sray.d.z);
+                    pk(PF_HT) = bits_from_f(h2.t); pk(PF_HSLOT) = (uint32_t)h2.slot;
+                    pk(PF_CREF) = c2.ref; pk(PF_CT0) = bits_from_f(c2.t0); pk(PF_CT1) = bits_from_f(c2.t1);
+                    pk(PF_LSLOT) = l2.slot; pk(PF_LLEFT) = l2.left; pk(PF_LTMAX) = bits_from_f(l2.tmax);
+                    pk(PF_LSL) = (uint32_t)l2.sl; pk(PF_MODE) = m2; pk(PF_TMAX) = bits_from_f(stmax);
+                    pk(PF_FLAGS) = (sany ? 1u : 0u) | (o2 ? 2u : 0u);
+                    pk(PF_SP) = (uint32_t)stk.sp; pk(PF_LO) = (uint32_t)stk.lo;
+                } else {
+                    tr = t2;
+                    h = h2;
+                    c = c2;
+                    lf = l2;
+                    mode = m2;
+                    any = sany;
+                    occ = o2;
+                    tmax_any = stmax;
                 }
             }
             if (__ballot(state == PS_FIN || state == PS_BEGIN || state == PS_NEW) == 0ull) break;
+        }
+        if (PARK) {
+            Ray r;
+            r.o = mk(f_from_bits(pk(PF_O)), f_from_bits(pk(PF_O + 1)), f_from_bits(pk(PF_O + 2)));
+            r.d = mk(f_from_bits(pk(PF_D)), f_from_bits(pk(PF_D + 1)), f_from_bits(pk(PF_D + 2)));
+            trav_setup(tr, r);
+            h.t = f_from_bits(pk(PF_HT));
+            h.slot = (int32_t)pk(PF_HSLOT);
+            c.ref = pk(PF_CREF); c.t0 = f_from_bits(pk(PF_CT0)); c.t1 = f_from_bits(pk(PF_CT1));
+            lf.slot = pk(PF_LSLOT); lf.left = pk(PF_LLEFT); lf.tmax = f_from_bits(pk(PF_LTMAX));
+            lf.sl = (int32_t)pk(PF_LSL);
+            mode = pk(PF_MODE);
+            tmax_any = f_from_bits(pk(PF_TMAX));
+            any = (pk(PF_FLAGS) & 1u) != 0u;
+            occ = (pk(PF_FLAGS) & 2u) != 0u;
+            stk.sp = (int)pk(PF_SP);
+            stk.lo = (int)pk(PF_LO);
         }
         if (__ballot(state == PS_TRAV) == 0ull) break;  // every lane done: no path left
         // ---- traversal: one record per lane per iteration, closest or any hit per lane
@@ -1644,8 +1732,8 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
             const uint32_t nfin = (uint32_t)__popcll(__ballot(state == PS_FIN));
             // refill at REFILL finished lanes; once every path is claimed, as soon as
             // the finished lanes are as many as those still traversing (the tail)
-            const uint32_t thr = exhausted ? (ntrav < (uint32_t)REFILL ? (ntrav > 0u ? ntrav : 1u) : (uint32_t)REFILL)
-                                           : (uint32_t)REFILL;
+            const uint32_t thr = exhausted ? (ntrav < PATH_REFILL ? (ntrav > 0u ? ntrav : 1u) : PATH_REFILL)
+                                           : PATH_REFILL;
             if (ntrav == 0u || nfin >= thr) break;
         }
     }
@@ -1656,15 +1744,31 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     }
 }
 
-static void launch_path(bool tex, bool wide, int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp,
-                        const PathLanes& L) {
-    const dim3 g(grid), b(TRAV_BLOCK);
+#ifndef KHP_PATH_PARK
+#define KHP_PATH_PARK 1
+#endif
+constexpr bool PATH_PARK = KHP_PATH_PARK != 0;
+constexpr size_t PATH_LDS = path_lds_bytes(PATH_PARK);
+// BSDF kind sets k_path is instantiated for: every kind, or the fur scenes'
+// (Lambert reflection + Marschner hair: configs 1-3 and the metric row), where
+// the other kinds' code and registers are compiled out.
+constexpr uint32_t KINDS_ALL = (1u << KHP_BSDF_COUNT) - 1u;
+constexpr uint32_t KINDS_FUR = (1u << KHP_BSDF_LAMBERTIAN_REFLECTION) | (1u << KHP_BSDF_MARSCHNER_HAIR);
+template <bool TEX, bool WIDE, uint32_t K>
+static void launch_path_k(int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp, const PathLanes& L) {
+    hipLaunchKernelGGL((k_path<TEX, WIDE, PATH_PARK, K>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L);
+}
+static void launch_path(bool tex, bool wide, bool fur, int grid, hipStream_t s, const DevScene& S, const Wave& W,
+                        SpillArea sp, const PathLanes& L) {
     if (tex) {
-        if (wide) hipLaunchKernelGGL((k_path<true, true>), g, b, PATH_LDS_BYTES, s, S, W, sp, L);
-        else hipLaunchKernelGGL((k_path<true, false>), g, b, PATH_LDS_BYTES, s, S, W, sp, L);
+        if (wide) launch_path_k<true, true, KINDS_ALL>(grid, s, S, W, sp, L);
+        else launch_path_k<true, false, KINDS_ALL>(grid, s, S, W, sp, L);
+    } else if (fur) {
+        if (wide) launch_path_k<false, true, KINDS_FUR>(grid, s, S, W, sp, L);
+        else launch_path_k<false, false, KINDS_FUR>(grid, s, S, W, sp, L);
     } else {
-        if (wide) hipLaunchKernelGGL((k_path<false, true>), g, b, PATH_LDS_BYTES, s, S, W, sp, L);
-        else hipLaunchKernelGGL((k_path<false, false>), g, b, PATH_LDS_BYTES, s, S, W, sp, L);
+        if (wide) launch_path_k<false, true, KINDS_ALL>(grid, s, S, W, sp, L);
+        else launch_path_k<false, false, KINDS_ALL>(grid, s, S, W, sp, L);
     }
 }
 
@@ -2106,6 +2210,7 @@ struct khp_ctx {
     int grid_ext = 0, grid_ext_w = 0, grid_ext_cam = 0, grid_sh = 0, grid_shade = 0;  // k_extend: 64-B, wide, bounce 0
     int grid_sh_w = 0;     // k_shadow on the two-level records
     int grid_path = 0, grid_path_w = 0;   // k_path (64-B / two-level records)
+    uint32_t bsdf_kinds = 0;              // the BSDF kinds the scene's materials use (bit per khp_bsdf_kind)
     int grid_ext_max = 0;  // the k_extend spill columns are sized for the largest grid
     khp_stats st{};
     // rccl gather: pixel lists cached per (W, H, tile, nranks, rank, root)
@@ -2144,12 +2249,19 @@ static void comm_release(khp_ctx* c);
 // the communicator (ncclCommAbort releases its kernels) and fails naming this rank
 // and its peers.  KIRK has no multi-device path; its only failure mode is the loud
 // exit of CPU_PathTracer.cpp:236-240, which this mirrors as a status.
+#ifdef KHP_COMM_TRACE   // diagnostic builds only (tools/build_variant.sh): RCCL steps to stderr
+#define COMM_TRACE(...) do { fprintf(stderr, "[khp comm %.3f] ", std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count()); fprintf(stderr, __VA_ARGS__); fprintf(stderr, "\n"); fflush(stderr); } while (0)
+#else
+#define COMM_TRACE(...) do { } while (0)
+#endif
 static std::string comm_who(const khp_ctx* c) {
     return "rank " + std::to_string(c->rank) + " of " + std::to_string(c->nranks);
 }
 static khp_status comm_abort(khp_ctx* c, const std::string& why) {
     if (c->comm) {
+        COMM_TRACE("ncclCommAbort begin");
         (void)ncclCommAbort(c->comm);
+        COMM_TRACE("ncclCommAbort end");
         c->comm = nullptr;
     }
     c->comm_dead = why;
@@ -2658,17 +2770,22 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     nb = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shadow<false, true>, TRAV_BLOCK, LDS_BYTES));
     c->grid_sh_w = std::min(c->grid_sh, std::max(1, nb) * c->n_cu);  // the spill columns are sized by grid_sh
+    c->bsdf_kinds = 0;   // the kinds the materials use: fur scenes run kernels with the others compiled out
+    for (const khp_material& m : hs.mats)
+        c->bsdf_kinds |= (m.bsdf >= 0 && m.bsdf < KHP_BSDF_COUNT) ? (1u << m.bsdf) : KINDS_ALL;
     nb = 0;
     if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<true, false>), 256, 0));
+    else if ((c->bsdf_kinds & ~KINDS_FUR) == 0u)
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false, KINDS_FUR>), 256, 0));
     else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false>), 256, 0));
     c->grid_shade = std::max(1, nb) * c->n_cu;
     nb = 0;
-    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, false>), TRAV_BLOCK, PATH_LDS_BYTES));
-    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, false>), TRAV_BLOCK, PATH_LDS_BYTES));
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, false, PATH_PARK, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, false, PATH_PARK, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
     c->grid_path = std::max(1, nb) * c->n_cu;
     nb = 0;
-    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, true>), TRAV_BLOCK, PATH_LDS_BYTES));
-    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, true>), TRAV_BLOCK, PATH_LDS_BYTES));
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, true, PATH_PARK, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, true, PATH_PARK, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
     c->grid_path_w = std::min(c->grid_path, std::max(1, nb) * c->n_cu);   // the columns are sized by grid_path
     c->built = true;
     return KHP_OK;
@@ -3175,7 +3292,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 HIPCHK(hipMemsetAsync(reinterpret_cast<char*>(Wv.cnt) + offsetof(Counters, fetch_ext), 0,
                                       sizeof(Counters::fetch_ext), sA));
                 timed(c, f, 3, true, sA);
-                launch_path(c->S.textured != 0, path_wide, grid_path, sA, c->S, Wv, sp_path, PL);
+                launch_path(c->S.textured != 0, path_wide, (c->bsdf_kinds & ~KINDS_FUR) == 0u, grid_path, sA, c->S, Wv, sp_path, PL);
                 timed(c, f, 3, false, sA);
             }
             timed(c, f, 3, true, sA);
@@ -3245,6 +3362,9 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     hipLaunchKernelGGL((k_shade<true, false>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
                 else if (bdm)
                     hipLaunchKernelGGL((k_shade<false, true>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                else if ((c->bsdf_kinds & ~KINDS_FUR) == 0u)   // fur scenes: the other BSDF kinds compiled out
+                    hipLaunchKernelGGL((k_shade<false, false, KINDS_FUR>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb,
+                                       cur, b);
                 else
                     hipLaunchKernelGGL((k_shade<false, false>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
                 timed(c, f, 1, false, sA);
@@ -4009,6 +4129,7 @@ extern "C" khp_status khp_get_stats(khp_ctx* c, khp_stats* out) {
 static khp_status comm_settle(khp_ctx* c, ncclResult_t r, const std::string& what) {
     if (!c->comm) return fail(KHP_EDEVICE, comm_who(c) + ": " + what + ": no communicator");
     const auto t0 = std::chrono::steady_clock::now();
+    COMM_TRACE("settle %s: r=%d", what.c_str(), (int)r);
     for (int spins = 0; r == ncclInProgress; ++spins) {
         ncclResult_t ae = ncclInProgress;
         const ncclResult_t q = ncclCommGetAsyncError(c->comm, &ae);
@@ -4022,6 +4143,7 @@ static khp_status comm_settle(khp_ctx* c, ncclResult_t r, const std::string& wha
         if (spins < 256) std::this_thread::yield();
         else std::this_thread::sleep_for(std::chrono::microseconds(100));
     }
+    COMM_TRACE("settled %s: r=%d", what.c_str(), (int)r);
     if (r != ncclSuccess)
         return comm_abort(c, comm_who(c) + ": " + what + ": " + ncclGetErrorString(r) + "; communicator aborted");
     return KHP_OK;
@@ -4079,7 +4201,9 @@ extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint
     memcpy(&uid, id, 128);
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;   // every RCCL call is then polled with the context's bound (comm_settle)
+    COMM_TRACE("ncclCommInitRankConfig begin (rank %d of %d)", rank, nranks);
     const ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, uid, rank, &cfg);
+    COMM_TRACE("ncclCommInitRankConfig returned %d", (int)r);
     if (r != ncclSuccess && r != ncclInProgress) {
         c->comm = nullptr;
         return fail(KHP_EDEVICE, comm_who(c) + ": ncclCommInitRankConfig: " + ncclGetErrorString(r));
