@@ -20,6 +20,8 @@
 #include <chrono>
 #include <memory>
 #include <string>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -1337,7 +1339,7 @@ static void launch_shadow(bool stats, bool wide, int grid, hipStream_t s, const 
 #define KHP_PATH_WAVES 4
 #endif
 #ifndef KHP_PATH_RING
-#define KHP_PATH_RING 6   // with the parked state (9.5 KB per wave) 16 waves fit a CU's LDS
+#define KHP_PATH_RING 8
 #endif
 #ifndef KHP_PATH_REFILL
 #define KHP_PATH_REFILL 24
@@ -1514,24 +1516,9 @@ __device__ __forceinline__ v3 finish_acc(const DevScene& S, const Ray& r, float 
 
 enum : uint32_t { PS_TRAV = 0u, PS_FIN = 1u, PS_NEW = 2u, PS_BEGIN = 3u, PS_DONE = 4u };
 
-// PARK: while a wave services its finished lanes, every lane's traversal state
-// (20 dwords: ray, hit, cursor, leaf cursor, mode, any-hit limit, flags, stack
-// depth) is parked in LDS, [field][lane], and reloaded after -- so the
-// traversal registers are not live through the shading code, which otherwise
-// holds them for the lanes still traversing (128 VGPRs + scratch without it).
-constexpr int PARK_FIELDS = 20;
-constexpr size_t path_lds_bytes(bool park) {
-    return PATH_LDS_BYTES + (park ? (size_t)PARK_FIELDS * TRAV_BLOCK * sizeof(uint32_t) : 0);
-}
-enum : int { PF_O = 0, PF_D = 3, PF_HT = 6, PF_HSLOT = 7, PF_CREF = 8, PF_CT0 = 9, PF_CT1 = 10, PF_LSLOT = 11,
-             PF_LLEFT = 12, PF_LTMAX = 13, PF_LSL = 14, PF_MODE = 15, PF_TMAX = 16, PF_FLAGS = 17, PF_SP = 18,
-             PF_LO = 19 };
-
-template <bool TEX, bool WIDE, bool PARK, uint32_t KINDS>
+template <bool TEX, bool WIDE, uint32_t KINDS>
 __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wave Wv, SpillArea spill, PathLanes L) {
     extern __shared__ uint32_t lds[];
-    uint32_t* park = lds + 3 * PATH_RING * TRAV_BLOCK;
-    auto pk = [&](int f) -> uint32_t& { return park[f * TRAV_BLOCK + threadIdx.x]; };
     const uint32_t npaths = Wv.P * Wv.n_samples * Wv.n_frames;
     const uint32_t g = blockIdx.x * TRAV_BLOCK + threadIdx.x;
     LdsStack<PATH_RING, false> stk;
@@ -1549,16 +1536,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     Claimer cl;
     cl.init(Wv.cnt->fetch_ext, npaths, 0u, npaths);
     for (;;) {
-        if (PARK) {
-            pk(PF_O) = bits_from_f(tr.r.o.x); pk(PF_O + 1) = bits_from_f(tr.r.o.y); pk(PF_O + 2) = bits_from_f(tr.r.o.z);
-            pk(PF_D) = bits_from_f(tr.r.d.x); pk(PF_D + 1) = bits_from_f(tr.r.d.y); pk(PF_D + 2) = bits_from_f(tr.r.d.z);
-            pk(PF_HT) = bits_from_f(h.t); pk(PF_HSLOT) = (uint32_t)h.slot;
-            pk(PF_CREF) = c.ref; pk(PF_CT0) = bits_from_f(c.t0); pk(PF_CT1) = bits_from_f(c.t1);
-            pk(PF_LSLOT) = lf.slot; pk(PF_LLEFT) = lf.left; pk(PF_LTMAX) = bits_from_f(lf.tmax);
-            pk(PF_LSL) = (uint32_t)lf.sl; pk(PF_MODE) = mode; pk(PF_TMAX) = bits_from_f(tmax_any);
-            pk(PF_FLAGS) = (any ? 1u : 0u) | (occ ? 2u : 0u);
-            pk(PF_SP) = (uint32_t)stk.sp; pk(PF_LO) = (uint32_t)stk.lo;
-        }
         // ---- service: shade finished extension rays, finish shadow rays, claim camera
         //      paths, start traversals -- until every lane traverses or has no work left
         for (;;) {
@@ -1567,32 +1544,13 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
             float stmax = 0.0f;
             sray.o = sray.d = mk(0, 0, 0);
             if (state == PS_FIN) {
-                Ray fr;
-                float fht, ftmax;
-                int32_t fslot;
-                bool fany, focc;
-                if (PARK) {
-                    fr.o = mk(f_from_bits(pk(PF_O)), f_from_bits(pk(PF_O + 1)), f_from_bits(pk(PF_O + 2)));
-                    fr.d = mk(f_from_bits(pk(PF_D)), f_from_bits(pk(PF_D + 1)), f_from_bits(pk(PF_D + 2)));
-                    fht = f_from_bits(pk(PF_HT));
-                    fslot = (int32_t)pk(PF_HSLOT);
-                    ftmax = f_from_bits(pk(PF_TMAX));
-                    fany = (pk(PF_FLAGS) & 1u) != 0u;
-                    focc = (pk(PF_FLAGS) & 2u) != 0u;
-                } else {
-                    fr = tr.r;
-                    fht = h.t;
-                    fslot = h.slot;
-                    ftmax = tmax_any;
-                    fany = any;
-                    focc = occ;
-                }
-                if (!fany) {  // k_shade
+                const Ray fr = tr.r;
+                if (!any) {  // k_shade
                     const float4 f0 = L.col[0][g], f1 = L.col[1][g], f2 = L.col[2][g], f3 = L.col[3][g];
                     const uint32_t bounce = bits_from_f(f3.w) & 0xFFFFu;
                     ShadeOut o;
-                    shade_core<TEX, KINDS>(S, fr, fht, fslot, mk(f0.x, f0.y, f0.z), mk(f1.x, f1.y, f1.z),
-                                    (int)bits_from_f(f0.w), bits_from_f(f1.w), bounce, bounce + 1 >= Wv.depth, o);
+                    shade_core<TEX, KINDS>(S, fr, h.t, h.slot, mk(f0.x, f0.y, f0.z), mk(f1.x, f1.y, f1.z),
+                                           (int)bits_from_f(f0.w), bits_from_f(f1.w), bounce, bounce + 1 >= Wv.depth, o);
                     ++n_ext;
                     const float4 tfo = make_float4(o.T.x, o.T.y, o.T.z, f_from_bits((uint32_t)o.flags));
                     const float4 cko = make_float4(o.C.x, o.C.y, o.C.z, f1.w);
@@ -1623,7 +1581,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                 } else {  // k_shadow_finish
                     const float4 f1 = L.col[1][g], f2 = L.col[2][g], f3 = L.col[3][g], f4 = L.col[4][g];
                     const float4 f5 = L.col[5][g], f6 = L.col[6][g], f7 = L.col[7][g];
-                    const v3 acc = finish_acc(S, fr, ftmax, focc, mk(f4.x, f4.y, f4.z), mk(f5.x, f5.y, f5.z),
+                    const v3 acc = finish_acc(S, fr, tmax_any, occ, mk(f4.x, f4.y, f4.z), mk(f5.x, f5.y, f5.z),
                                               mk(f6.x, f6.y, f6.z), f4.w != 0.0f, mk(f7.x, f7.y, f7.z));
                     ++n_sh;
                     const float4 cko = make_float4(f1.x + acc.x, f1.y + acc.y, f1.z + acc.z, f1.w);
@@ -1677,44 +1635,16 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                     go = trav2_begin<false>(S, t2, stmax, stk, m2, c2, l2, st);
                 }
                 state = go ? PS_TRAV : PS_FIN;
-                if (PARK) {
-                    pk(PF_O) = bits_from_f(sray.o.x); pk(PF_O + 1) = bits_from_f(sray.o.y); pk(PF_O + 2) = bits_from_f(sray.o.z);
-                    pk(PF_D) = bits_from_f(sray.d.x); pk(PF_D + 1) = bits_from_f(sray.d.y); pk(PF_D + 2) = bits_from_f(sray.d.z);
-                    pk(PF_HT) = bits_from_f(h2.t); pk(PF_HSLOT) = (uint32_t)h2.slot;
-                    pk(PF_CREF) = c2.ref; pk(PF_CT0) = bits_from_f(c2.t0); pk(PF_CT1) = bits_from_f(c2.t1);
-                    pk(PF_LSLOT) = l2.slot; pk(PF_LLEFT) = l2.left; pk(PF_LTMAX) = bits_from_f(l2.tmax);
-                    pk(PF_LSL) = (uint32_t)l2.sl; pk(PF_MODE) = m2; pk(PF_TMAX) = bits_from_f(stmax);
-                    pk(PF_FLAGS) = (sany ? 1u : 0u) | (o2 ? 2u : 0u);
-                    pk(PF_SP) = (uint32_t)stk.sp; pk(PF_LO) = (uint32_t)stk.lo;
-                } else {
-                    tr = t2;
-                    h = h2;
-                    c = c2;
-                    lf = l2;
-                    mode = m2;
-                    any = sany;
-                    occ = o2;
-                    tmax_any = stmax;
-                }
+                tr = t2;
+                h = h2;
+                c = c2;
+                lf = l2;
+                mode = m2;
+                any = sany;
+                occ = o2;
+                tmax_any = stmax;
             }
             if (__ballot(state == PS_FIN || state == PS_BEGIN || state == PS_NEW) == 0ull) break;
-        }
-        if (PARK) {
-            Ray r;
-            r.o = mk(f_from_bits(pk(PF_O)), f_from_bits(pk(PF_O + 1)), f_from_bits(pk(PF_O + 2)));
-            r.d = mk(f_from_bits(pk(PF_D)), f_from_bits(pk(PF_D + 1)), f_from_bits(pk(PF_D + 2)));
-            trav_setup(tr, r);
-            h.t = f_from_bits(pk(PF_HT));
-            h.slot = (int32_t)pk(PF_HSLOT);
-            c.ref = pk(PF_CREF); c.t0 = f_from_bits(pk(PF_CT0)); c.t1 = f_from_bits(pk(PF_CT1));
-            lf.slot = pk(PF_LSLOT); lf.left = pk(PF_LLEFT); lf.tmax = f_from_bits(pk(PF_LTMAX));
-            lf.sl = (int32_t)pk(PF_LSL);
-            mode = pk(PF_MODE);
-            tmax_any = f_from_bits(pk(PF_TMAX));
-            any = (pk(PF_FLAGS) & 1u) != 0u;
-            occ = (pk(PF_FLAGS) & 2u) != 0u;
-            stk.sp = (int)pk(PF_SP);
-            stk.lo = (int)pk(PF_LO);
         }
         if (__ballot(state == PS_TRAV) == 0ull) break;  // every lane done: no path left
         // ---- traversal: one record per lane per iteration, closest or any hit per lane
@@ -1744,11 +1674,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     }
 }
 
-#ifndef KHP_PATH_PARK
-#define KHP_PATH_PARK 1
-#endif
-constexpr bool PATH_PARK = KHP_PATH_PARK != 0;
-constexpr size_t PATH_LDS = path_lds_bytes(PATH_PARK);
+constexpr size_t PATH_LDS = PATH_LDS_BYTES;
 // BSDF kind sets k_path is instantiated for: every kind, or the fur scenes'
 // (Lambert reflection + Marschner hair: configs 1-3 and the metric row), where
 // the other kinds' code and registers are compiled out.
@@ -1756,7 +1682,7 @@ constexpr uint32_t KINDS_ALL = (1u << KHP_BSDF_COUNT) - 1u;
 constexpr uint32_t KINDS_FUR = (1u << KHP_BSDF_LAMBERTIAN_REFLECTION) | (1u << KHP_BSDF_MARSCHNER_HAIR);
 template <bool TEX, bool WIDE, uint32_t K>
 static void launch_path_k(int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp, const PathLanes& L) {
-    hipLaunchKernelGGL((k_path<TEX, WIDE, PATH_PARK, K>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L);
+    hipLaunchKernelGGL((k_path<TEX, WIDE, K>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L);
 }
 static void launch_path(bool tex, bool wide, bool fur, int grid, hipStream_t s, const DevScene& S, const Wave& W,
                         SpillArea sp, const PathLanes& L) {
@@ -2780,12 +2706,12 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false>), 256, 0));
     c->grid_shade = std::max(1, nb) * c->n_cu;
     nb = 0;
-    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, false, PATH_PARK, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
-    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, false, PATH_PARK, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, false, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, false, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
     c->grid_path = std::max(1, nb) * c->n_cu;
     nb = 0;
-    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, true, PATH_PARK, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
-    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, true, PATH_PARK, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, true, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, true, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
     c->grid_path_w = std::min(c->grid_path, std::max(1, nb) * c->n_cu);   // the columns are sized by grid_path
     c->built = true;
     return KHP_OK;
@@ -4188,6 +4114,21 @@ static void leave_local_group(khp_ctx* c) {
     }
 }
 
+// RCCL's ncclCommInitRankConfig does not return while a peer is missing, even
+// for a non-blocking communicator (measured on this image, RCCL 2.27.7: it stays
+// in its bootstrap, profiles/r04d_comm_probe.log).  The call therefore runs on
+// a helper thread and the caller waits for it with the context's bound; on a
+// timeout the caller returns KHP_EDEVICE and the thread is left to finish
+// alone: if the init ever completes it aborts the communicator nobody waits
+// for, otherwise it stays blocked until the process exits.
+struct CommInitJob {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclSuccess;
+};
+
 extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint8_t id[128]) {
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(KHP_EINVAL, "bad comm arguments");
     HIPCHK(hipSetDevice(c->device));
@@ -4199,16 +4140,51 @@ extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint
     c->rank = rank;
     ncclUniqueId uid;
     memcpy(&uid, id, 128);
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = 0;   // every RCCL call is then polled with the context's bound (comm_settle)
-    COMM_TRACE("ncclCommInitRankConfig begin (rank %d of %d)", rank, nranks);
-    const ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, uid, rank, &cfg);
-    COMM_TRACE("ncclCommInitRankConfig returned %d", (int)r);
+    auto job = std::make_shared<CommInitJob>();
+    const int device = c->device;
+    try {
+        std::thread([job, uid, nranks, rank, device]() mutable {
+            (void)hipSetDevice(device);
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;   // every later RCCL call is polled with the context's bound (comm_settle)
+            ncclComm_t comm = nullptr;
+            COMM_TRACE("ncclCommInitRankConfig begin (rank %d of %d)", rank, nranks);
+            const ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, uid, rank, &cfg);
+            COMM_TRACE("ncclCommInitRankConfig returned %d", (int)r);
+            std::lock_guard<std::mutex> lk(job->m);
+            if (job->abandoned) {   // the caller gave up: nobody will use this communicator
+                if (comm) (void)ncclCommAbort(comm);
+                return;
+            }
+            job->comm = comm;
+            job->r = r;
+            job->done = true;
+            job->cv.notify_all();
+        }).detach();
+    } catch (const std::exception& e) {
+        return fail(KHP_EDEVICE, std::string("khp_comm_init: cannot start the init thread: ") + e.what());
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    {
+        std::unique_lock<std::mutex> lk(job->m);
+        if (!job->cv.wait_for(lk, std::chrono::milliseconds(c->comm_timeout_ms), [&] { return job->done; })) {
+            job->abandoned = true;
+            return fail(KHP_EDEVICE, comm_who(c) + ": RCCL communicator init did not return within " +
+                                         std::to_string(c->comm_timeout_ms) +
+                                         " ms (a peer never joined); this context has no communicator");
+        }
+    }
+    const ncclResult_t r = job->r;
     if (r != ncclSuccess && r != ncclInProgress) {
-        c->comm = nullptr;
+        if (job->comm) (void)ncclCommAbort(job->comm);
         return fail(KHP_EDEVICE, comm_who(c) + ": ncclCommInitRankConfig: " + ncclGetErrorString(r));
     }
+    c->comm = job->comm;
+    const uint32_t spent = (uint32_t)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const uint32_t bound = c->comm_timeout_ms;
+    c->comm_timeout_ms = bound > spent ? bound - spent : 1u;   // the init's remaining time
     const khp_status s = comm_settle(c, r, "RCCL communicator init");
+    c->comm_timeout_ms = bound;
     if (s != KHP_OK) c->comm_dead.clear();   // nothing was enqueued on the comm: the context stays usable
     return s;
 }
