@@ -47,7 +47,7 @@ struct alignas(128) Counters {
     unsigned long long node_visits, prim_tests, sh_node_visits, sh_prim_tests, spills;
     unsigned long long pruned, sh_pruned;  // entries popped only to fail the prune test
     unsigned long long iters, lanes_busy, sh_iters, sh_lanes_busy;  // wave iterations, lanes with work
-    unsigned long long step_cycles[4];  // unused (khp_stats.step_cycles stays 0)
+    unsigned long long step_cycles[4];  // diagnostic builds only (KHP_PATH_PROFILE), else 0
 };
 
 // One bounce's shadow-ray queue (count + claim cursors).  Two of them
@@ -1535,7 +1535,14 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     float tmax_any = 0.0f;
     Claimer cl;
     cl.init(Wv.cnt->fetch_ext, npaths, 0u, npaths);
+#ifdef KHP_PATH_PROFILE   // diagnostic builds: wave cycles in service / traversal, service rounds, iterations
+    unsigned long long pc_serv = 0, pc_trav = 0, pc_rounds = 0, pc_iters = 0, pc_t = clock64();
+#endif
     for (;;) {
+#ifdef KHP_PATH_PROFILE
+        pc_t = clock64();
+        ++pc_rounds;
+#endif
         // ---- service: shade finished extension rays, finish shadow rays, claim camera
         //      paths, start traversals -- until every lane traverses or has no work left
         for (;;) {
@@ -1646,9 +1653,16 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
             }
             if (__ballot(state == PS_FIN || state == PS_BEGIN || state == PS_NEW) == 0ull) break;
         }
+#ifdef KHP_PATH_PROFILE
+        pc_serv += clock64() - pc_t;
+        pc_t = clock64();
+#endif
         if (__ballot(state == PS_TRAV) == 0ull) break;  // every lane done: no path left
         // ---- traversal: one record per lane per iteration, closest or any hit per lane
         for (;;) {
+#ifdef KHP_PATH_PROFILE
+            ++pc_iters;
+#endif
             if (state == PS_TRAV) {
                 bool o2 = false;
                 const bool f = WIDE ? iterwk<2, false>(S, tr, h, tmax_any, stk, mode, c, lf, st, o2, any)
@@ -1666,11 +1680,20 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                                            : PATH_REFILL;
             if (ntrav == 0u || nfin >= thr) break;
         }
+#ifdef KHP_PATH_PROFILE
+        pc_trav += clock64() - pc_t;
+#endif
     }
     const unsigned long long se = wave_sum((unsigned long long)n_ext), ss = wave_sum((unsigned long long)n_sh);
     if (lane_id() == 0) {
         atomicAdd(&Wv.cnt->ext_rays, se);
         atomicAdd(&Wv.cnt->sh_rays, ss);
+#ifdef KHP_PATH_PROFILE
+        atomicAdd(&Wv.cnt->step_cycles[0], pc_serv);
+        atomicAdd(&Wv.cnt->step_cycles[1], pc_trav);
+        atomicAdd(&Wv.cnt->step_cycles[2], pc_rounds);
+        atomicAdd(&Wv.cnt->step_cycles[3], pc_iters);
+#endif
     }
 }
 

@@ -48,7 +48,9 @@ for name, spp, tex in (("gui", 1, True), ("sync", 8, False)):
                           "device_ms": round(st["render_ms"], 3), "extend_ms": round(st["extend_ms"], 3),
                           "shade_ms": round(st["shade_ms"], 3), "shadow_ms": round(st["shadow_ms"], 3),
                           "bounce_extend_ms": [round(x, 3) for x in st["bounce_extend_ms"][:D]],
-                          "bounce_shadow_ms": [round(x, 3) for x in st["bounce_shadow_ms"][:D]]})
+                          "bounce_shadow_ms": [round(x, 3) for x in st["bounce_shadow_ms"][:D]],
+                          "step_cycles": st["step_cycles"], "extend_rays": st["extend_rays"],
+                          "shadow_rays": st["shadow_rays"]})
         k += spp
 print(json.dumps(out), flush=True)
 ctx.close()
