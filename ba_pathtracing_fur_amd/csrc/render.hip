@@ -1535,13 +1535,14 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     float tmax_any = 0.0f;
     Claimer cl;
     cl.init(Wv.cnt->fetch_ext, npaths, 0u, npaths);
-#ifdef KHP_PATH_PROFILE   // diagnostic builds: wave cycles in service / traversal, service rounds, iterations
-    unsigned long long pc_serv = 0, pc_trav = 0, pc_rounds = 0, pc_iters = 0, pc_t = clock64();
+#ifdef KHP_PATH_PROFILE   // diagnostic builds: launch timeline (100 MHz wall clock): first start, last
+    // claim exhaustion seen, last end, longest drain of one wave (its end - its exhaustion)
+    const unsigned long long pc_start = wall_clock64();
+    unsigned long long pc_exh = 0;
 #endif
     for (;;) {
 #ifdef KHP_PATH_PROFILE
-        pc_t = clock64();
-        ++pc_rounds;
+        if (exhausted && pc_exh == 0) pc_exh = wall_clock64();
 #endif
         // ---- service: shade finished extension rays, finish shadow rays, claim camera
         //      paths, start traversals -- until every lane traverses or has no work left
@@ -1653,16 +1654,9 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
             }
             if (__ballot(state == PS_FIN || state == PS_BEGIN || state == PS_NEW) == 0ull) break;
         }
-#ifdef KHP_PATH_PROFILE
-        pc_serv += clock64() - pc_t;
-        pc_t = clock64();
-#endif
         if (__ballot(state == PS_TRAV) == 0ull) break;  // every lane done: no path left
         // ---- traversal: one record per lane per iteration, closest or any hit per lane
         for (;;) {
-#ifdef KHP_PATH_PROFILE
-            ++pc_iters;
-#endif
             if (state == PS_TRAV) {
                 bool o2 = false;
                 const bool f = WIDE ? iterwk<2, false>(S, tr, h, tmax_any, stk, mode, c, lf, st, o2, any)
@@ -1680,19 +1674,18 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                                            : PATH_REFILL;
             if (ntrav == 0u || nfin >= thr) break;
         }
-#ifdef KHP_PATH_PROFILE
-        pc_trav += clock64() - pc_t;
-#endif
     }
     const unsigned long long se = wave_sum((unsigned long long)n_ext), ss = wave_sum((unsigned long long)n_sh);
     if (lane_id() == 0) {
         atomicAdd(&Wv.cnt->ext_rays, se);
         atomicAdd(&Wv.cnt->sh_rays, ss);
 #ifdef KHP_PATH_PROFILE
-        atomicAdd(&Wv.cnt->step_cycles[0], pc_serv);
-        atomicAdd(&Wv.cnt->step_cycles[1], pc_trav);
-        atomicAdd(&Wv.cnt->step_cycles[2], pc_rounds);
-        atomicAdd(&Wv.cnt->step_cycles[3], pc_iters);
+        const unsigned long long pc_end = wall_clock64();
+        if (pc_exh == 0) pc_exh = pc_end;
+        atomicMax(&Wv.cnt->step_cycles[0], ~pc_start);
+        atomicMax(&Wv.cnt->step_cycles[1], pc_exh);
+        atomicMax(&Wv.cnt->step_cycles[2], pc_end);
+        atomicMax(&Wv.cnt->step_cycles[3], pc_end - pc_exh);
 #endif
     }
 }
@@ -2171,6 +2164,7 @@ struct khp_ctx {
     // polls with this bound and ncclCommGetAsyncError instead of blocking
     uint32_t comm_timeout_ms = 120000;
     std::string comm_dead;   // why the comm was aborted ("" while alive or never created)
+    std::shared_ptr<void> comm_job;   // the init's arguments (CommInitJob), kept while the comm lives
     // ABI 8 in-process group (khp_comm_init_local): the gather's transport between
     // contexts of one process instead of RCCL; a sender's k-th gather packs into
     // ring slot k % LG_SLOTS, the root's k-th gather copies every sender's slot k.
@@ -4105,6 +4099,7 @@ static void comm_release(khp_ctx* c) {
     if (comm_settle(c, ncclCommFinalize(c->comm), "ncclCommFinalize") == KHP_OK && c->comm)
         (void)ncclCommDestroy(c->comm);
     c->comm = nullptr;
+    c->comm_job.reset();
     c->comm_dead.clear();
 }
 
@@ -4150,6 +4145,10 @@ struct CommInitJob {
     bool done = false, abandoned = false;
     ncclComm_t comm = nullptr;
     ncclResult_t r = ncclSuccess;
+    // A non-blocking init goes on in RCCL's background job after the call
+    // returns, and may still read its arguments: they live here, with the job.
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    ncclUniqueId uid;
 };
 
 extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint8_t id[128]) {
@@ -4166,13 +4165,13 @@ extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint
     auto job = std::make_shared<CommInitJob>();
     const int device = c->device;
     try {
-        std::thread([job, uid, nranks, rank, device]() mutable {
+        job->uid = uid;
+        job->cfg.blocking = 0;   // every later RCCL call is polled with the context's bound (comm_settle)
+        std::thread([job, nranks, rank, device]() {
             (void)hipSetDevice(device);
-            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-            cfg.blocking = 0;   // every later RCCL call is polled with the context's bound (comm_settle)
             ncclComm_t comm = nullptr;
             COMM_TRACE("ncclCommInitRankConfig begin (rank %d of %d)", rank, nranks);
-            const ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, uid, rank, &cfg);
+            const ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, job->uid, rank, &job->cfg);
             COMM_TRACE("ncclCommInitRankConfig returned %d", (int)r);
             std::lock_guard<std::mutex> lk(job->m);
             if (job->abandoned) {   // the caller gave up: nobody will use this communicator
@@ -4203,6 +4202,7 @@ extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint
         return fail(KHP_EDEVICE, comm_who(c) + ": ncclCommInitRankConfig: " + ncclGetErrorString(r));
     }
     c->comm = job->comm;
+    c->comm_job = job;
     const uint32_t spent = (uint32_t)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     const uint32_t bound = c->comm_timeout_ms;
     c->comm_timeout_ms = bound > spent ? bound - spent : 1u;   // the init's remaining time
