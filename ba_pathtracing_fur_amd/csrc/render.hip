@@ -1344,9 +1344,6 @@ static void launch_shadow(bool stats, bool wide, int grid, hipStream_t s, const 
 #ifndef KHP_PATH_REFILL
 #define KHP_PATH_REFILL 24
 #endif
-#ifndef KHP_PATH_HEAVY
-#define KHP_PATH_HEAVY 500   // path iterations that mark a pixel for longest-first claims (0: off)
-#endif
 constexpr int PATH_WAVES = KHP_PATH_WAVES;
 constexpr uint32_t PATH_REFILL = KHP_PATH_REFILL;   // finished lanes that trigger a wave's service
 constexpr int PATH_RING = KHP_PATH_RING;
@@ -1357,28 +1354,7 @@ struct PathLanes {
     // 3 next ray d.xyz | bounce (bit 31: the path continues after the pending shadow ray)
     // 4 lc.xyz | has_emit   5 Told.xyz   6 AT.xyz   7 ET.xyz  (the deferred NEE terms, k_shade's shadow record)
     float4* col[8];
-    // Longest-first claims (the wavefront's front/back queues, per pixel): a
-    // path whose traversals took more than heavy_T iterations marks its pixel
-    // (heavy, one byte per frame pixel, kept across calls); the next call claims
-    // the chunk's pixels in `order` (k_pix_order: marked pixels first), so the
-    // long paths start early instead of ending the launch.  Scheduling only: a
-    // path's result does not depend on when it is traced.
-    uint8_t* heavy;
-    const uint32_t* order;   // [chunk pixel slot] -> chunk-local pixel; null: identity
-    uint32_t heavy_T;
 };
-
-// Chunk-local pixels in claim order for k_path: the pixels marked heavy by the
-// previous call first (front, counted in cnt->nq[0]), the others after (back,
-// cnt->nqb[0], from the end).
-__global__ __launch_bounds__(256) void k_pix_order(Wave Wv, const uint8_t* heavy, uint32_t* order) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool act = q < Wv.P;
-    const bool hv = act && heavy[Wv.pix[Wv.p_off + (act ? q : 0u)]] != 0;
-    const uint32_t f = wave_alloc(act && hv, &Wv.cnt->nq[0]);
-    const uint32_t b = wave_alloc(act && !hv, &Wv.cnt->nqb[0]);
-    if (act) order[hv ? f : Wv.P - 1u - b] = q;
-}
 
 // k_shade's per-hit operations without the light-path variant (KIRK's traceRay
 // light test, EnvironmentShader / LightShader / SimpleShader /
@@ -1554,19 +1530,11 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     Hit h{FLT_MAX_, -1, 0.0f, 0.0f};
     Cur c{0u, 0.0f, 0.0f, false};
     LeafCur lf{0u, 0u, 0.0f, 0.0f, 0.0f, 0.0f, -1};
-    uint32_t mode = 0u, state = PS_NEW, n_ext = 0, n_sh = 0, it_path = 0;
+    uint32_t mode = 0u, state = PS_NEW, n_ext = 0, n_sh = 0;
     bool any = false, occ = false, exhausted = false;
     float tmax_any = 0.0f;
     Claimer cl;
     cl.init(Wv.cnt->fetch_ext, npaths, 0u, npaths);
-    const uint32_t per_pix = Wv.n_frames * Wv.n_samples;
-    // the path ended: its pixel's longest-first mark for the next call
-    auto mark = [&](uint32_t pid) {
-        if (!L.heavy) return;
-        uint32_t fr, p_local, s_local;
-        path_coords(Wv, pid, fr, p_local, s_local);
-        L.heavy[Wv.pix[Wv.p_off + p_local]] = it_path > L.heavy_T ? 1 : 0;
-    };
 #ifdef KHP_PATH_PROFILE   // diagnostic builds: launch timeline (100 MHz wall clock): first start, last
     // claim exhaustion seen, last end, longest drain of one wave (its end - its exhaustion)
     const unsigned long long pc_start = wall_clock64();
@@ -1616,7 +1584,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                         state = PS_BEGIN;
                     } else {
                         Wv.CK[bits_from_f(f2.w)] = cko;
-                        mark(bits_from_f(f2.w));
                         state = PS_NEW;
                     }
                 } else {  // k_shadow_finish
@@ -1635,25 +1602,17 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                         state = PS_BEGIN;
                     } else {
                         Wv.CK[bits_from_f(f2.w)] = cko;
-                        mark(bits_from_f(f2.w));
                         state = PS_NEW;
                     }
                 }
             }
             const unsigned long long want = __ballot(state == PS_NEW);
             if (want != 0ull) {  // wave-uniform: claim camera paths for the lanes whose path ended
-                uint32_t my = 0, v = 0;
+                uint32_t my = 0, pid = 0;
                 bool got = false;
                 if (!exhausted) got = cl.claim(want, my, exhausted);
                 if (state == PS_NEW) {
-                    if (got && cl.phys(my, v)) {
-                        uint32_t pid = v;
-                        if (L.order) {  // claim slot v -> (pixel slot, frame, sample) -> the ordered pixel's path
-                            const uint32_t q = v / per_pix, r = v - q * per_pix;
-                            const uint32_t fr = r / Wv.n_samples, sl = r - fr * Wv.n_samples;
-                            pid = (uint32_t)path_index(Wv, fr, L.order[q], sl);
-                        }
-                        it_path = 0;
+                    if (got && cl.phys(my, pid)) {
                         uint32_t key;
                         sray = camera_path(S, Wv, pid, key);
                         L.col[0][g] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));
@@ -1700,7 +1659,6 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
         for (;;) {
             if (state == PS_TRAV) {
                 bool o2 = false;
-                ++it_path;
                 const bool f = WIDE ? iterwk<2, false>(S, tr, h, tmax_any, stk, mode, c, lf, st, o2, any)
                                     : iter2k<2, false>(S, tr, h, tmax_any, stk, mode, c, lf, st, o2, any);
                 if (f) {
@@ -2092,7 +2050,7 @@ struct PathSet {
     DevMem heavyb;
     DevMem permb, hkeyb, hclsb;   // shade_order 1
     DevMem lvb;                   // light-path variant: subpath vertices of a chunk's sample slots
-    DevMem plane, pspill, porder; // k_path: per-lane path state columns, traversal-stack spill columns, claim order
+    DevMem plane, pspill;         // k_path: per-lane path state columns, traversal-stack spill columns
     size_t sh_cap = 0;            // shadow-record capacity per parity (cap x connections per path)
     hipStream_t sA = nullptr, sB = nullptr;
 };
@@ -2181,7 +2139,6 @@ struct khp_ctx {
     bool tree_on_device = false;
     uint32_t n_dnodes = 0, n_slots = 0;
     DevMem fb, pix, stage, stage_pix, snap;   // snap: per-bounce Counters snapshots (stats renders)
-    DevMem pheavy;            // k_path's longest-first marks, one byte per frame pixel (PathLanes::heavy)
     int cur_bounce = -1;
     std::vector<float> dump;   // prm.dump_bounce: SoA o.xyz, d.xyz of one bounce's extension queue
     std::vector<float> dump_sh;  // prm.dump_bounce: that bounce's shadow rays, o.xyz d.xyz t_max each
@@ -3093,8 +3050,6 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     if (c->fbW != p->width || c->fbH != p->height || !c->fb.p) {
         HIPCHK(c->fb.ensure(npix * 3 * sizeof(float)));
         HIPCHK(hipMemsetAsync(c->fb.p, 0, npix * 3 * sizeof(float), c->stream));
-        HIPCHK(c->pheavy.ensure(npix));
-        HIPCHK(hipMemsetAsync(c->pheavy.p, 0, npix, c->stream));
         c->fbW = p->width;
         c->fbH = p->height;
     }
@@ -3211,12 +3166,6 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         HIPCHK(w.pspill.ensure(lanes * STACK_MAX * sizeof(int4)));
         for (int k = 0; k < 8; ++k) PL.col[k] = w.plane.as<float4>() + (size_t)k * lanes;
         sp_path = SpillArea{w.pspill.as<int4>(), (uint32_t)lanes};
-        if (KHP_PATH_HEAVY > 0) {
-            HIPCHK(w.porder.ensure((size_t)P_chunk * sizeof(uint32_t)));
-            PL.heavy = c->pheavy.as<uint8_t>();
-            PL.order = w.porder.as<uint32_t>();
-            PL.heavy_T = KHP_PATH_HEAVY;
-        }
     }
     const int grid_path = std::max(1, (path_wide ? c->grid_path_w : c->grid_path) / G);
     if (stats) {
@@ -3285,11 +3234,6 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
             if (use_path) {  // every bounce of the chunk's paths in one launch; then the accumulate below
                 HIPCHK(hipMemsetAsync(reinterpret_cast<char*>(Wv.cnt) + offsetof(Counters, fetch_ext), 0,
                                       sizeof(Counters::fetch_ext), sA));
-                if (PL.order) {  // this chunk's pixels, the previous call's long paths first
-                    HIPCHK(hipMemsetAsync(Wv.cnt, 0, 4 * sizeof(uint32_t), sA));   // nq, nqb
-                    hipLaunchKernelGGL(k_pix_order, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, PL.heavy,
-                                       const_cast<uint32_t*>(PL.order));
-                }
                 timed(c, f, 3, true, sA);
                 launch_path(c->S.textured != 0, path_wide, (c->bsdf_kinds & ~KINDS_FUR) == 0u, grid_path, sA, c->S, Wv, sp_path, PL);
                 timed(c, f, 3, false, sA);
