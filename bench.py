@@ -427,7 +427,8 @@ def main():
         sync_el = frame.max_over_ranks(time.perf_counter() - t1)
         sync_line = {"value": round(args.sync_check_steps * samples_per_step / sync_el / 1e6, 3),
                      "ms_per_step": round(sync_el / args.sync_check_steps * 1e3, 3), "steps": args.sync_check_steps,
-                     "def": "one synchronous khp_render per pass (+ gather), no frame fusion"}
+                     "def": "one synchronous khp_render per pass (+ gather), no frame fusion; synchronous renders "
+                            f"run the path kernel (khp_ctx_params.path_kernel = {params['path_kernel']}, 0 = automatic)"}
 
     # KIRK's GUI pattern (CPU_PathTracer.cpp:17-52): every
     # render() call adds ONE sample to every pixel synchronously and the viewer
@@ -444,7 +445,8 @@ def main():
         gui_line = {"value": round(args.gui_steps * W * H / gui_el / 1e6, 3),
                     "ms_per_call": round(gui_el / args.gui_steps * 1e3, 3), "calls": args.gui_steps,
                     "def": "KIRK GUI render() calls: one synchronous khp_render of 1 spp + khp_read_rgba8 "
-                           "(8-bit texture to the host) per call"}
+                           "(8-bit texture to the host) per call; synchronous renders run the path kernel "
+                           f"(khp_ctx_params.path_kernel = {params['path_kernel']}, 0 = automatic)"}
         k += 1   # those samples belong to the pass slot after the last timed one
         # the same calls pipelined (ABI 8): render() enqueues its 1-spp pass and an
         # asynchronous texture read, the viewer shows textures as they complete;
