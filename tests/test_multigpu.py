@@ -230,3 +230,21 @@ def test_local_group_refuses_out_of_order_gathers():
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_bench_two_ranks_on_one_gpu():
+    """`bench.py --gpus 2` end to end with real HIP contexts on ONE GPU: the
+    launcher, two bench processes rendering their tiles with libkirk_hip.so,
+    asynchronous passes with a gather after each, the synchronous and isolated
+    passes, max-over-ranks timing and rank 0's gather check on a second real
+    context.  Only the transport is replaced (RCCL refuses two ranks on one GPU):
+    tests/_bench_hip_gloo.py moves the product plan's pixels over gloo."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "1", "--width", "64",
+                          "--height", "48", "--spp", "2", "--tile", "16", "--steps", "3", "--warmup", "1",
+                          "--sync-check-steps", "1", "--iso-steps", "1", "--gui-steps", "0", "--no-cpu-baseline",
+                          "--ctx-factory", "tests/_bench_hip_gloo.py:HipGlooCtx", "--launch-timeout", "200"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["gather_check"]["bit_exact"] and line["gather_check"]["passes"] == 1 + 1 + 3 + 1 + 1
