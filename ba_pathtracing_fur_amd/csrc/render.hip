@@ -87,7 +87,8 @@ struct Wave {
     uint32_t sample0;     // global sample index of chunk sample 0
     uint32_t n_samples;   // samples in this chunk (per frame)
     uint32_t n_frames;    // fused frames in this chunk
-    uint32_t pix_major;   // path numbering (khp_ctx_params.path_order): 0 frame-major, 1 pixel-major
+    uint32_t pix_major;   // path numbering (khp_ctx_params.path_order): 0 frame-major, else pixel-major
+    uint8_t* pixheavy;    // path_order 2: per image pixel, its last camera ray took > heavy_T iterations (null: off)
     uint32_t cam0;        // bounce 0 computes camera rays in place (no k_generate queue)
     uint32_t fsample0[KHP_MAX_FUSE];  // per fused frame: global sample index of chunk sample 0
     uint32_t depth;
@@ -441,6 +442,34 @@ __device__ __forceinline__ void flush_stats(const TravStats& st, const Stack& st
     }
 }
 
+// path_order 2 (heavy-first pixels): the camera ray of path pid took more than
+// heavy_T iterations.  The samples of a pixel race on its flag; any of their
+// values is a valid hint (k_pix_order only reorders the pixel list).
+__device__ __forceinline__ void mark_pixel(const Wave& Wv, uint32_t pid, bool long_ray) {
+    uint32_t fr, p_local, s_local;
+    path_coords(Wv, pid, fr, p_local, s_local);
+    Wv.pixheavy[Wv.pix[Wv.p_off + p_local]] = long_ray ? 1 : 0;
+}
+
+// path_order 2: the batch's pixel list with the pixels whose last camera ray was
+// long first (front part, ascending) and the others after them (back part,
+// filled from the end).  A permutation of the owned pixels: paths are
+// independent and each pixel's samples are summed in sample order, so the
+// order changes no result; it moves the longest camera rays to the start of
+// every bounce-0 launch instead of leaving them to its tail.
+__global__ __launch_bounds__(256) void k_pix_order(const uint32_t* __restrict__ pix, uint32_t n,
+                                                  const uint8_t* __restrict__ heavy, uint32_t* __restrict__ out,
+                                                  uint32_t* cnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = i < n;
+    const uint32_t px = in ? pix[i] : 0u;
+    const bool hv = in && heavy[px] != 0;
+    const uint32_t f = wave_alloc(hv, &cnt[0]);
+    const uint32_t b = wave_alloc(in && !hv, &cnt[1]);
+    if (hv) out[f] = px;
+    else if (in) out[n - 1u - b] = px;
+}
+
 // ---- extend: closest hit for every queued ray ------------------------------------------
 // CAM: bounce 0 with Wave::cam0 -- the ray of queue slot idx (= path idx) is
 // the camera ray, computed here instead of loaded.
@@ -488,6 +517,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : CAM ? CAM_WAVES : 
                     Wv.ht[idx] = h.t;
                     Wv.hslot[idx] = -1;
                     Wv.heavy[idx] = 0;
+                    if (CAM && Wv.pixheavy) mark_pixel(Wv, idx, false);
                 }
             }
         }
@@ -514,6 +544,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : CAM ? CAM_WAVES : 
                     Wv.ht[j] = h.t;
                     Wv.hslot[j] = h.slot;
                     Wv.heavy[j] = it > Wv.heavy_T ? 1 : 0;
+                    if (CAM && Wv.pixheavy) mark_pixel(Wv, j, it > Wv.heavy_T);
                     has = false;
                 }
             }
@@ -2052,6 +2083,7 @@ struct PathSet {
     DevMem permb, hkeyb, hclsb;   // shade_order 1
     DevMem lvb;                   // light-path variant: subpath vertices of a chunk's sample slots
     DevMem plane, pspill;         // k_path: per-lane path state columns, traversal-stack spill columns
+    DevMem pixo, pixcnt;          // path_order 2: this batch's heavy-first pixel list, its two cursors
     size_t sh_cap = 0;            // shadow-record capacity per parity (cap x connections per path)
     hipStream_t sA = nullptr, sB = nullptr;
 };
@@ -2140,6 +2172,7 @@ struct khp_ctx {
     bool tree_on_device = false;
     uint32_t n_dnodes = 0, n_slots = 0;
     DevMem fb, pix, stage, stage_pix, snap;   // snap: per-bounce Counters snapshots (stats renders)
+    DevMem pixheavy;                          // path_order 2: per image pixel, its last camera ray was long
     int cur_bounce = -1;
     std::vector<float> dump;   // prm.dump_bounce: SoA o.xyz, d.xyz of one bounce's extension queue
     std::vector<float> dump_sh;  // prm.dump_bounce: that bounce's shadow rays, o.xyz d.xyz t_max each
@@ -2314,7 +2347,7 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     if (prm->trace_kernels > 2) return fail(KHP_EINVAL, "trace_kernels must be 0, 1 or 2");
     if (prm->shade_order > 1) return fail(KHP_EINVAL, "shade_order must be 0 or 1");
     if (prm->serial_stages > 1) return fail(KHP_EINVAL, "serial_stages must be 0 or 1");
-    if (prm->path_order > 1) return fail(KHP_EINVAL, "path_order must be 0 or 1");
+    if (prm->path_order > 2) return fail(KHP_EINVAL, "path_order must be 0, 1 or 2");
     if (prm->path_kernel > 2) return fail(KHP_EINVAL, "path_kernel must be 0, 1 or 2");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
@@ -3051,6 +3084,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     if (c->fbW != p->width || c->fbH != p->height || !c->fb.p) {
         HIPCHK(c->fb.ensure(npix * 3 * sizeof(float)));
         HIPCHK(hipMemsetAsync(c->fb.p, 0, npix * 3 * sizeof(float), c->stream));
+        HIPCHK(c->pixheavy.ensure(npix));
+        HIPCHK(hipMemsetAsync(c->pixheavy.p, 0, npix, c->stream));
         c->fbW = p->width;
         c->fbH = p->height;
     }
@@ -3211,7 +3246,17 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     Wv.H = p->height;
     Wv.seed = p->seed;
     Wv.depth = p->depth;
-    Wv.pix_major = c->prm.path_order;
+    Wv.pix_major = c->prm.path_order != 0 ? 1u : 0u;
+    Wv.pixheavy = nullptr;
+    if (c->prm.path_order == 2 && !use_path && P_all) {  // heavy-first pixel list (k_pix_order), per path set
+        HIPCHK(w.pixo.ensure((size_t)P_all * sizeof(uint32_t)));
+        HIPCHK(w.pixcnt.ensure(2 * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(w.pixcnt.p, 0, 2 * sizeof(uint32_t), sA));
+        hipLaunchKernelGGL(k_pix_order, dim3((P_all + 255) / 256), dim3(256), 0, sA, c->pix.as<uint32_t>(), P_all,
+                           c->pixheavy.as<uint8_t>(), w.pixo.as<uint32_t>(), w.pixcnt.as<uint32_t>());
+        Wv.pix = w.pixo.as<uint32_t>();
+        Wv.pixheavy = c->pixheavy.as<uint8_t>();
+    }
     // camera rays in place at bounce 0 (no generate pass): not for the light-path
     // variant (its image-plane connections add to the queued bounce-0 state) nor
     // when bounce 0's queue is dumped

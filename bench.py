@@ -93,7 +93,7 @@ def parse():
                     help="fused passes re-run with serial_stages=1 for the isolated per-kernel rooflines (0: skip)")
     ap.add_argument("--shade-order", type=int, default=None, help="khp_ctx_params.shade_order (1: hits sorted by shading class)")
     ap.add_argument("--path-order", type=int, default=None,
-                    help="khp_ctx_params.path_order (0: frame-major fused chunks, 1: pixel-major)")
+                    help="khp_ctx_params.path_order (0: frame-major fused chunks, 1: pixel-major, 2: pixel-major heavy-first)")
     ap.add_argument("--wide-from", type=int, default=None,
                     help="khp_ctx_params.wide_from (first bounce on two-level node records; >= depth: never)")
     ap.add_argument("--heavy-iters", type=int, default=None,

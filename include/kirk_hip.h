@@ -293,7 +293,9 @@ typedef struct {
     uint32_t path_order;         /* ABI 9: how a fused chunk numbers its paths.  0: frame-major (frame f's
                                     pixels x samples form one block); 1 (default): pixel-major (all fused
                                     frames' samples of one pixel are adjacent paths, so a wave traces one
-                                    pixel of 8 frames at 8 spp).  Measured in DESIGN.md §5a            */
+                                    pixel of 8 frames at 8 spp); 2: pixel-major, and the wavefront takes the
+                                    pixels whose previous camera ray was long first (a per-batch permutation
+                                    of the pixel list; results unchanged).  Measured in DESIGN.md §5a   */
     uint32_t wide_from;          /* ABI 10: the first bounce whose closest-hit traversal runs on two-level
                                     node records (one 128-B record per step: a node's child boxes and the
                                     near child's own, KIRK's order and counts kept); earlier bounces use the

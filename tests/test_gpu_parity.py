@@ -159,7 +159,7 @@ def test_chunked_and_instrumented_frames(hip_ctx, chunk):
 
 def test_params_are_validated(hip_ctx):
     for bad in (dict(fuse_frames=0), dict(fuse_frames=33), dict(frames_in_flight=4), dict(chunk_paths=100),
-                dict(trace_kernels=3), dict(shade_order=2), dict(serial_stages=2), dict(path_order=2)):
+                dict(trace_kernels=3), dict(shade_order=2), dict(serial_stages=2), dict(path_order=3)):
         with pytest.raises(N.KhpError) as e:
             hip_ctx.set_params(**bad)
         assert e.value.status == N.KHP_EINVAL
@@ -363,14 +363,16 @@ def test_single_rank_communicator():
     ctx.close()
 
 
-@pytest.mark.parametrize("order", ["0", "1"])
+@pytest.mark.parametrize("order", ["0", "1", "2"])
 @pytest.mark.parametrize("fuse", ["2", "4", "3"])
 def test_fused_frames(fuse, order):
     """fuse_frames: asynchronous passes with equal parameters run as one
     batch (one launch per bounce for all of them) and accumulate in call order
     -- the framebuffer is the oracle's 8-spp frame; with a (1-rank) gather
     after every pass, as bench.py does at N > 1, the gathers keep their place.
-    Both path numberings (path_order 0 frame-major, 1 pixel-major)."""
+    Both path numberings (path_order 0 frame-major, 1 pixel-major) and the
+    heavy-first pixel order (2: each batch's pixel list permuted by the previous
+    batch's camera-ray lengths)."""
     from ba_pathtracing_fur_amd.pathtracer import comm_unique_id
     sd = S.config2(72, 48, n_strands=1500)
     want = oracle_ffi.Oracle(sd).render(72, 48, 8, 5, threads=16)
@@ -403,7 +405,8 @@ def test_fused_frames(fuse, order):
 def test_fused_full_size_matches_passes():
     """The metric scene (1M strands, 1080p): 16 progressive 4-spp passes
     fused into one batch (133M paths: 1 chunk at the default 2^27 paths per
-    chunk, 2 at 2^26; frame-major and pixel-major path numbering) give the
+    chunk, 2 at 2^26; frame-major and pixel-major path numbering, and the
+    heavy-first pixel order, whose later batches run a permuted pixel list) give the
     framebuffer of the same passes rendered one by one, bit for bit; sampled
     rows are the oracle's 64-spp frame."""
     ctx = HipContext(0)
@@ -413,7 +416,7 @@ def test_fused_full_size_matches_passes():
         for k in range(16):
             ctx.render(1920, 1080, 4, 5, first_sample=4 * k, readback=False)
         want = ctx.read_framebuffer(1920, 1080)
-        for cap, order in ((0, 0), (1 << 26, 0), (0, 1), (1 << 26, 1)):
+        for cap, order in ((0, 0), (1 << 26, 0), (0, 1), (1 << 26, 1), (0, 2), (1 << 26, 2), (0, 2)):
             ctx.set_params(chunk_paths=cap, path_order=order)
             for k in range(16):
                 ctx.render(1920, 1080, 4, 5, first_sample=4 * k, async_=True)

@@ -34,9 +34,12 @@ def main():
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--ranks-max", type=int, default=8, help="time at most this many ranks per N (spread over 0..N-1)")
     ap.add_argument("--sync-steps", action="store_true", help="no frame pipelining (bench.py --sync-steps)")
+    ap.add_argument("--path-order", type=int, default=None, help="khp_ctx_params.path_order")
     a = ap.parse_args()
     W, H, spp, depth = a.width, a.height, a.spp, a.depth
     ctx = HipContext(0)
+    if a.path_order is not None:
+        ctx.set_params(path_order=a.path_order)
     scenes.config3_device(ctx, W, H, n_strands=a.strands)
     ctx.build_accel()
     out = []
