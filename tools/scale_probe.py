@@ -35,11 +35,14 @@ def main():
     ap.add_argument("--ranks-max", type=int, default=8, help="time at most this many ranks per N (spread over 0..N-1)")
     ap.add_argument("--sync-steps", action="store_true", help="no frame pipelining (bench.py --sync-steps)")
     ap.add_argument("--path-order", type=int, default=None, help="khp_ctx_params.path_order")
+    ap.add_argument("--set", nargs="*", default=[], metavar="KEY=INT", help="other khp_ctx_params fields")
     a = ap.parse_args()
     W, H, spp, depth = a.width, a.height, a.spp, a.depth
     ctx = HipContext(0)
     if a.path_order is not None:
         ctx.set_params(path_order=a.path_order)
+    if a.set:
+        ctx.set_params(**{k: int(v) for k, v in (kv.split("=", 1) for kv in a.set)})
     scenes.config3_device(ctx, W, H, n_strands=a.strands)
     ctx.build_accel()
     out = []
