@@ -3439,6 +3439,16 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
             }
         }
     }
+    if (P_all == 0 && ops) {
+        // a rank that owns no tile runs no chunk, but its gathers and snapshots
+        // still take their place in call order (its peers wait for its gathers)
+        for (const PendingOp& o : *ops) {
+            if (o.kind == PendingOp::RENDER) continue;
+            s = op_now(c, o);
+            if (s != KHP_OK) return s;
+        }
+        if (c->fb_evt) HIPCHK(hipStreamWaitEvent(sA, c->fb_evt, 0));
+    }
     // join: the batch is done when its last chunk has accumulated
     hipEvent_t e_end = slot_event(f.sync_pool, f.sync_next, true);
     HIPCHK(hipEventRecord(e_end, sA));
@@ -4373,9 +4383,12 @@ static khp_status local_receive(khp_ctx* c, int root, size_t* total) {
 
 // RCCL transport: one ncclSend per sender; the root posts one receive per sender
 // in ONE group.  The group is closed on every path, also when a receive fails.
+// A rank that owns no pixel posts no send, and the root no receive from it
+// (both sides know the count from the same plan).
 static khp_status rccl_send(khp_ctx* c, uint32_t P, int root) {
-    if (P) hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
-                              c->stage_pix.as<uint32_t>(), P, c->stage.as<float>());
+    if (P == 0) return KHP_OK;
+    hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
+                       c->stage_pix.as<uint32_t>(), P, c->stage.as<float>());
     HIPCHK(hipGetLastError());
     return comm_settle(c, ncclSend(c->stage.p, (size_t)P * 3, ncclFloat32, root, c->comm, c->stream),
                        "ncclSend of " + std::to_string(P) + " pixels to root " + std::to_string(root));
@@ -4387,7 +4400,7 @@ static khp_status rccl_receive(khp_ctx* c, int root, size_t* total) {
     if (r != ncclSuccess) return comm_settle(c, r, "ncclGroupStart");
     std::string failed;
     for (int q = 0; q < c->nranks && failed.empty(); ++q) {
-        if (q == root) continue;
+        if (q == root || c->gather_counts[q] == 0) continue;
         r = ncclRecv(c->stage.as<float>() + *total * 3, c->gather_counts[q] * 3, ncclFloat32, q, c->comm, c->stream);
         if (r != ncclSuccess && r != ncclInProgress)
             failed = "ncclRecv from rank " + std::to_string(q) + ": " + ncclGetErrorString(r);

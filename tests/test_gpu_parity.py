@@ -119,6 +119,50 @@ def test_tile_shards_match_oracle(hip_ctx, nranks):
         assert_parity(got[m][None], full[m][None], exact=True)
 
 
+EDGE = [("config1", 1, 1, 1, 1), ("config1", 1, 1, 33, 5), ("config2", 37, 23, 3, 1), ("config2", 37, 23, 2, 5)]
+
+
+@pytest.mark.parametrize("path_kernel", [1, 2])
+@pytest.mark.parametrize("name,w,h,spp,depth", EDGE, ids=[f"{c[0]}-{c[1]}x{c[2]}-{c[3]}spp-d{c[4]}" for c in EDGE])
+def test_edge_sizes(hip_ctx, name, w, h, spp, depth, path_kernel):
+    """A 1x1 frame (one pixel: a single, partly filled wave; 33 spp: more paths
+    than a wave), a ragged 37x23 frame, and depth 1 (camera rays and their
+    shadow rays only) -- through the wavefront (path_kernel 1) and the path
+    kernel (2), as one synchronous render and as fused 1-spp asynchronous
+    passes.  Bit-exact against the oracle."""
+    sd = S.build_config(name, width=w, height=h, **({} if name == "config1" else dict(n_strands=800)))
+    want = oracle_ffi.Oracle(sd).render(w, h, spp, depth, threads=16)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    old = hip_ctx.set_params(path_kernel=path_kernel)
+    try:
+        assert_parity(hip_ctx.render(w, h, spp, depth), want, exact=True)
+        for k in range(spp):
+            hip_ctx.render(w, h, 1, depth, first_sample=k, async_=True)
+        hip_ctx.sync()
+        assert_parity(hip_ctx.read_framebuffer(w, h), want, exact=True)
+    finally:
+        hip_ctx.set_params(**old)
+
+
+def test_rank_without_tiles(hip_ctx):
+    """A rank that owns no tile (37x23 in 16-px tiles: 6 tiles for 8 ranks)
+    renders nothing, synchronously or not, without an error; the ranks that do
+    own tiles match the oracle on them."""
+    sd = S.config2(37, 23, n_strands=800)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    full = oracle_ffi.Oracle(sd).render(37, 23, 2, 5, threads=16)
+    for r in range(8):
+        m = sharding.owned_mask(37, 23, r, 8, 16)
+        assert m.any() == (r < 6)
+        got = hip_ctx.render(37, 23, 2, 5, tile_size=16, tile_rank=r, tile_nranks=8)
+        if m.any():
+            assert_parity(got[m][None], full[m][None], exact=True)
+        hip_ctx.render(37, 23, 2, 5, tile_size=16, tile_rank=r, tile_nranks=8, async_=True)
+    hip_ctx.sync()
+
+
 def test_path_chunking(hip_ctx):
     """khp_ctx_params.chunk_paths forces pixel and sample chunking of the wavefront; frames must not change."""
     sd = S.config2(128, 96, n_strands=1500)

@@ -14,6 +14,7 @@ import pytest
 
 import oracle_ffi
 from _util import assert_parity
+from ba_pathtracing_fur_amd import native as N
 from ba_pathtracing_fur_amd import scenes as S
 
 pytestmark = pytest.mark.gpu
@@ -31,11 +32,12 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_rccl_gather_assembles_the_single_gpu_frame(tmp_path, world):
+@pytest.mark.parametrize("world,W,H", [(2, 96, 64), (4, 96, 64), (8, 37, 23)])
+def test_rccl_gather_assembles_the_single_gpu_frame(tmp_path, world, W, H):
+    """Real ranks over RCCL; at 8 ranks a ragged 37x23 frame (6 tiles of 16 px),
+    so ranks 6 and 7 own no pixel and post no send."""
     if _n_gpus() < world:
         pytest.skip(f"needs {world} GPUs, this box has {_n_gpus()}")
-    W, H = 96, 64
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "_rccl_gather_worker.py"),
            str(tmp_path), str(W), str(H)]
@@ -81,6 +83,38 @@ def test_local_group_gather_assembles_the_frame(world, async_):
                                readback=False, async_=async_)
                 ctxs[r].gather_framebuffer(W, H, SPP, 5, TILE, world, r, 0)
         for c in ctxs[1:]:                     # flush the senders' fused batches first
+            c.sync()
+        ctxs[0].sync()
+        assert_parity(ctxs[0].read_framebuffer(W, H), want, exact=True)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("async_", [False, True])
+def test_local_group_gather_with_empty_ranks(async_):
+    """Ragged edges and ranks that own no tile: a 37x23 frame in 16-px tiles has
+    6 tiles (the last column 5 px wide, the last row 7 px high), so of 8 ranks
+    6 and 7 render and send nothing.  Their passes and gathers must still
+    complete, and rank 0's frame is the oracle's bit for bit."""
+    from ba_pathtracing_fur_amd.pathtracer import HipContext, comm_init_local
+    W, H, SPP, TILE, PASSES, world = 37, 23, 2, 16, 2, 8
+    counts, _ = N.gather_plan(W, H, TILE, world, 0, 0)
+    assert list(counts[6:]) == [0, 0] and all(int(c) > 0 for c in counts[1:6])
+    sd = S.config2(W, H, n_strands=800)
+    want = oracle_ffi.Oracle(sd).render(W, H, SPP * PASSES, 5, threads=16)
+    ctxs = [HipContext(0) for _ in range(world)]
+    try:
+        for c in ctxs:
+            c.set_scene(sd)
+            c.build_accel()
+        comm_init_local(ctxs)
+        for k in range(PASSES):
+            for r in reversed(range(world)):
+                ctxs[r].render(W, H, SPP, 5, first_sample=k * SPP, tile_size=TILE, tile_rank=r, tile_nranks=world,
+                               readback=False, async_=async_)
+                ctxs[r].gather_framebuffer(W, H, SPP, 5, TILE, world, r, 0)
+        for c in ctxs[1:]:
             c.sync()
         ctxs[0].sync()
         assert_parity(ctxs[0].read_framebuffer(W, H), want, exact=True)
