@@ -119,7 +119,8 @@ def test_tile_shards_match_oracle(hip_ctx, nranks):
         assert_parity(got[m][None], full[m][None], exact=True)
 
 
-EDGE = [("config1", 1, 1, 1, 1), ("config1", 1, 1, 33, 5), ("config2", 37, 23, 3, 1), ("config2", 37, 23, 2, 5)]
+EDGE = [("config1", 1, 1, 1, 1), ("config1", 1, 1, 33, 5), ("config2", 37, 23, 3, 1), ("config2", 37, 23, 2, 5),
+        ("zoo", 32, 24, 2, 20)]
 
 
 @pytest.mark.parametrize("path_kernel", [1, 2])
@@ -129,8 +130,10 @@ def test_edge_sizes(hip_ctx, name, w, h, spp, depth, path_kernel):
     than a wave), a ragged 37x23 frame, and depth 1 (camera rays and their
     shadow rays only) -- through the wavefront (path_kernel 1) and the path
     kernel (2), as one synchronous render and as fused 1-spp asynchronous
-    passes.  Bit-exact against the oracle."""
-    sd = S.build_config(name, width=w, height=h, **({} if name == "config1" else dict(n_strands=800)))
+    passes; and depth 20 on the all-BSDF scene (glass and mirrors keep paths
+    alive past the usual 5-8 bounces).  Bit-exact against the oracle."""
+    sd = S.build_config(name, width=w, height=h,
+                        **({} if name == "config1" else dict(n_strands=400 if name == "zoo" else 800)))
     want = oracle_ffi.Oracle(sd).render(w, h, spp, depth, threads=16)
     hip_ctx.set_scene(sd)
     hip_ctx.build_accel()
@@ -159,8 +162,18 @@ def test_rank_without_tiles(hip_ctx):
         got = hip_ctx.render(37, 23, 2, 5, tile_size=16, tile_rank=r, tile_nranks=8)
         if m.any():
             assert_parity(got[m][None], full[m][None], exact=True)
-        hip_ctx.render(37, 23, 2, 5, tile_size=16, tile_rank=r, tile_nranks=8, async_=True)
+    # asynchronous passes with an 8-bit snapshot after each: an empty rank's
+    # batch has no chunk, its snapshots must still be delivered
+    bufs, tickets = [], []
+    for r in (0, 6, 7):
+        for k in range(2):
+            hip_ctx.render(37, 23, 1, 5, first_sample=k, tile_size=16, tile_rank=r, tile_nranks=8, async_=True)
+            bufs.append(np.zeros((23, 37, 4), np.uint8))
+            tickets.append(hip_ctx.read_rgba8_async(bufs[-1]))
     hip_ctx.sync()
+    for t, b in zip(tickets, bufs):
+        assert hip_ctx.snapshot_wait(t)
+        assert (b[..., 3] == 255).all()
 
 
 def test_path_chunking(hip_ctx):
