@@ -148,6 +148,52 @@ def test_edge_sizes(hip_ctx, name, w, h, spp, depth, path_kernel):
         hip_ctx.set_params(**old)
 
 
+def _tiny_scene(centers, size=0.3, planar=False):
+    sd = S.SceneData(name="tiny")
+    m = sd.add_material(S.material(diffuse=(0.7, 0.6, 0.5)))
+    c = np.asarray(centers, np.float32)
+    off = np.array([[0, 0, 0], [size, 0, 0], [0, size, 0 if planar else size]], np.float32)
+    v = c[:, None, :] + off[None]
+    sd.add_triangles(v, np.broadcast_to(np.float32([0, 0, 1]), v.shape).copy(), m)
+    sd.lights.append(S.point_light((0.6, 0.6, 1.5), (3.0, 3.0, 3.0), radius=0.05, att_const=1.0, att_quad=0.0))
+    sd.env_color = (0.2, 0.3, 0.4)
+    sd.env_ambient = (0.05, 0.05, 0.05)
+    sd.cam = S.camera((0, 0, 3), (0, 0, -1), (0, 1, 0), 24, 16)
+    return sd
+
+
+TINY = {
+    "one_object": lambda: _tiny_scene([[-0.1, -0.1, 0.0]]),
+    "two_objects": lambda: _tiny_scene([[-0.4, -0.2, 0.0], [0.1, 0.0, 0.2]]),
+    "three_objects": lambda: _tiny_scene(np.random.default_rng(3).uniform(-0.5, 0.5, (3, 3))),
+    # every centroid on one plane: the root is ONE leaf of 3000 candidates (the escaped leaf count)
+    "root_leaf_3000": lambda: _tiny_scene(np.c_[np.random.default_rng(7).uniform(-1, 1, (3000, 2)), np.zeros(3000)],
+                                          size=0.02, planar=True),
+}
+
+
+@pytest.mark.parametrize("path_kernel", [1, 2])
+@pytest.mark.parametrize("name", list(TINY))
+def test_tiny_and_degenerate_trees(hip_ctx, name, path_kernel):
+    """Trees whose root is a leaf (one object; 3000 coplanar centroids, whose
+    leaf count needs the escape word), two- and three-object trees (no
+    two-level record below the root), through the wavefront and the path
+    kernel, synchronous and fused: the oracle's frame bit for bit."""
+    sd = TINY[name]()
+    want = oracle_ffi.Oracle(sd).render(24, 16, 3, 4, threads=16)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    old = hip_ctx.set_params(path_kernel=path_kernel)
+    try:
+        assert_parity(hip_ctx.render(24, 16, 3, 4), want, exact=True)
+        for k in range(3):
+            hip_ctx.render(24, 16, 1, 4, first_sample=k, async_=True)
+        hip_ctx.sync()
+        assert_parity(hip_ctx.read_framebuffer(24, 16), want, exact=True)
+    finally:
+        hip_ctx.set_params(**old)
+
+
 def test_rank_without_tiles(hip_ctx):
     """A rank that owns no tile (37x23 in 16-px tiles: 6 tiles for 8 ranks)
     renders nothing, synchronously or not, without an error; the ranks that do
