@@ -4255,7 +4255,6 @@ extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint
     } catch (const std::exception& e) {
         return fail(KHP_EDEVICE, std::string("khp_comm_init: cannot start the init thread: ") + e.what());
     }
-    const auto t0 = std::chrono::steady_clock::now();
     {
         std::unique_lock<std::mutex> lk(job->m);
         if (!job->cv.wait_for(lk, std::chrono::milliseconds(c->comm_timeout_ms), [&] { return job->done; })) {
@@ -4272,7 +4271,6 @@ extern "C" khp_status khp_comm_init(khp_ctx* c, int nranks, int rank, const uint
     }
     c->comm = job->comm;
     c->comm_job = job;
-    (void)t0;
     const khp_status s = comm_settle(c, r, "RCCL communicator init");   // r is ncclSuccess here
     if (s != KHP_OK) c->comm_dead.clear();   // nothing was enqueued on the comm: the context stays usable
     return s;
