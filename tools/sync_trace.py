@@ -8,7 +8,7 @@ runs the metric scene and, after a warmup, N calls of each pattern:
 printing each call's host wall time (perf_counter, ms) as one JSON line on
 stdout, so tools/sync_breakdown.py can line the trace's kernels up with them.
 usage: rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d D -o run -- \
-         python3 tools/sync_trace.py [calls=4] [path_kernel=0] [wide_from=2] > calls.json
+         python3 tools/sync_trace.py [calls=4] [path_kernel=0] [wide_from=2] [path_order=1] > calls.json
 """
 import json
 import os
@@ -22,9 +22,10 @@ from ba_pathtracing_fur_amd import HipContext, scenes  # noqa: E402
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 PK = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 WF = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+PO = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 W, H, D = 1920, 1080, 5
 ctx = HipContext(0)
-ctx.set_params(path_kernel=PK, wide_from=WF)
+ctx.set_params(path_kernel=PK, wide_from=WF, path_order=PO)
 scenes.config3_device(ctx, W, H, n_strands=1_000_000)
 ctx.build_accel()
 k = 0
