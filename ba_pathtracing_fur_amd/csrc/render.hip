@@ -2571,7 +2571,7 @@ extern "C" khp_status khp_device_copy(khp_ctx* c, void* dst, const void* src, si
     HIPCHK(hipSetDevice(c->device));
     if (bytes)
         HIPCHK(hipMemcpyAsync(dst, src, bytes, to_device ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    KHPCHK(wait_stream(c, c->stream, "a device copy"));
     return KHP_OK;
 }
 
@@ -2678,7 +2678,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         HIPCHK(hipGetLastError());
         uint32_t bad = 1;
         HIPCHK(hipMemcpyAsync(&bad, c->wide_bad.p, sizeof(bad), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        KHPCHK(wait_stream(c, c->stream, "the scene build"));
         wide_ok = bad == 0;
     }
     if (!wide_ok) c->wide.release();
@@ -2687,7 +2687,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         hipLaunchKernelGGL(k_tri_slots, dim3((n_slots + 255) / 256), dim3(256), 0, c->stream, c->prims.as<float4>(),
                            c->aux.as<Aux>(), n_slots, hs.n_tris, c->trislot.as<uint32_t>());
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(c->stream));
+    KHPCHK(wait_stream(c, c->stream, "the scene build"));
     c->st.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     DevScene& S = c->S;
     S.tri_slot = c->trislot.as<uint32_t>();
@@ -3091,7 +3091,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     }
     s = prepare_pixels(c, p);
     if (s != KHP_OK) return s;
-    if (geometry_change) HIPCHK(hipStreamSynchronize(c->stream));
+    if (geometry_change) KHPCHK(wait_stream(c, c->stream, "the framebuffer setup"));
     const uint32_t P_all = (uint32_t)c->pix_host.size();
     // Batches in flight: an asynchronous render takes the next frame slot (its
     // own path set and streams) and returns once enqueued; up to
@@ -3321,7 +3321,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     uint32_t nq[2] = {0, 0};
                     HIPCHK(hipMemcpyAsync(&nq[0], &Wv.cnt->nq[cur], 4, hipMemcpyDeviceToHost, sA));
                     HIPCHK(hipMemcpyAsync(&nq[1], &Wv.cnt->nqb[cur], 4, hipMemcpyDeviceToHost, sA));
-                    HIPCHK(hipStreamSynchronize(sA));
+                    KHPCHK(wait_stream(c, sA, "the queue dump"));
                     const size_t m = (size_t)nq[0] + nq[1];
                     c->dump.resize(6 * m);
                     for (int q = 0; q < 6; ++q) {
@@ -3363,7 +3363,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     HIPCHK(hipStreamWaitEvent(sB, shaded, 0));
                 }
                 if (dump_b == (int)b && p0 == 0 && s0 == 0) {  // this bounce's shadow rays: o, d, t_max
-                    HIPCHK(hipStreamSynchronize(sA));
+                    KHPCHK(wait_stream(c, sA, "the queue dump"));
                     ShadowQ hq;
                     HIPCHK(hipMemcpy(&hq, Wb.shq, sizeof(ShadowQ), hipMemcpyDeviceToHost));
                     std::vector<float4> rec(6 * ((size_t)hq.nsh + hq.nshb));
@@ -3767,7 +3767,7 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
         std::vector<double> hl(n);
         HIPCHK(hipMemcpyAsync(hm.data(), bmax.p, 4 * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(hl.data(), lgv.p, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        KHPCHK(wait_stream(c, c->stream, "the 8-bit texture"));
         float mx = 1e-06f;
         for (uint32_t b = 0; b < nb; ++b) mx = (mx < hm[b]) ? hm[b] : mx;
         float sum = 0.0f;  // RGB_to_Yxy's float running sum, in pixel order
@@ -3806,7 +3806,7 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
                                dmask.as<double>(), mean, cterm.as<double>());
             std::vector<double> hc((size_t)ks * ks);
             HIPCHK(hipMemcpyAsync(hc.data(), cterm.p, 8 * hc.size(), hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
+            KHPCHK(wait_stream(c, c->stream, "the 8-bit texture"));
             double cs = 0.0;  // luminance_from_center's double running sum, in its loop order
             for (double v : hc) cs += v;
             world_lum = (float)(cs / (ks * ks));
@@ -3842,7 +3842,7 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out_rgba, out.p, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    KHPCHK(wait_stream(c, c->stream, "the 8-bit texture"));
     return KHP_OK;
 }
 
@@ -3896,7 +3896,7 @@ extern "C" khp_status khp_read_layout(khp_ctx* c, uint32_t* n_records, uint32_t*
         HIPCHK(hipMemcpyAsync(prim_records, c->prims.p, 64 * (size_t)c->n_slots, hipMemcpyDeviceToHost, c->stream));
     if (prim_aux && c->n_slots)
         HIPCHK(hipMemcpyAsync(prim_aux, c->aux.p, sizeof(Aux) * (size_t)c->n_slots, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    KHPCHK(wait_stream(c, c->stream, "the layout read"));
     return KHP_OK;
 }
 
@@ -3949,7 +3949,7 @@ extern "C" khp_status khp_read_framebuffer(khp_ctx* c, float* out_rgb) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(out_rgb, c->fb.p, (size_t)c->fbW * c->fbH * 3 * sizeof(float), hipMemcpyDeviceToHost,
                           c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    KHPCHK(wait_stream(c, c->stream, "the framebuffer read"));
     return KHP_OK;
 }
 
@@ -4042,7 +4042,7 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
     }
     Counters hc;
     HIPCHK(hipMemcpyAsync(&hc, w.cnt.p, sizeof(hc), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    KHPCHK(wait_stream(c, c->stream, "the ray queries"));
     c->st.node_visits = shadow ? hc.sh_node_visits : hc.node_visits;
     c->st.prim_tests = shadow ? hc.sh_prim_tests : hc.prim_tests;
     c->st.stack_spills = hc.spills;
@@ -4081,7 +4081,7 @@ extern "C" khp_status khp_trace_closest(khp_ctx* c, uint32_t n, const float* ori
     if (uv_out) HIPCHK(hipMemcpyAsync(uv_out, uv.p, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
     unsigned long long sv[2] = {0, 0};
     HIPCHK(hipMemcpyAsync(sv, stb.p, 16, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    KHPCHK(wait_stream(c, c->stream, "the ray queries"));
     c->st.node_visits = sv[0];
     c->st.prim_tests = sv[1];
     return KHP_OK;
@@ -4107,7 +4107,7 @@ extern "C" khp_status khp_trace_any(khp_ctx* c, uint32_t n, const float* orig, c
                        d.as<float>(), tm.as<float>(), h.as<uint8_t>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(hit_out, h.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    KHPCHK(wait_stream(c, c->stream, "the ray queries"));
     return KHP_OK;
 }
 
