@@ -314,3 +314,73 @@ def test_fibers_to_cones_flatten_rule():
     b, a = sd.cone_base_r0, sd.cone_apex_r1
     assert np.allclose(b[0, :3], [0, -0.008, 0]) and np.isclose(b[0, 3], 0.95)      # c <= 3: -5 %
     assert np.isclose(b[4, 3], 0.6 * 0.9) and np.allclose(a[:, 3], rad[0, 1:])      # c > 3: -10 %
+
+
+# ---- integrator quirks, pinned behaviourally ---------------------------------
+def _plane_scene(lights, occluder=None, diffuse=(0.5, 0.5, 0.5), ambient=(0.0, 0.0, 0.0)):
+    """A Lambert plane z = -3 facing the camera at the origin (looking down -z);
+    optionally a black square occluder parallel to it, (z, half-size, centre x)."""
+    sd = S.SceneData(name="plane")
+    m = sd.add_material(S.material(diffuse=diffuse))
+    sd.add_triangles(*S.quad((-20, -20, -3), (20, -20, -3), (20, 20, -3), (-20, 20, -3), (0, 0, 1)), m)
+    if occluder is not None:
+        z, h, cx = occluder
+        black = sd.add_material(S.material(diffuse=(0.0, 0.0, 0.0)))
+        sd.add_triangles(*S.quad((cx - h, -h, z), (cx + h, -h, z), (cx + h, h, z), (cx - h, h, z), (0, 0, 1)), black)
+    sd.lights.extend(lights)
+    sd.env_color = (0.0, 0.0, 0.0)
+    sd.env_ambient = ambient
+    sd.cam = S.camera((0, 0, 0), (0, 0, -1), width=24, height=16)
+    return sd
+
+
+def _pt(pos=(1.0, 0.0, -1.0)):
+    return S.point_light(pos, (4.0, 3.0, 2.0), radius=0.01, att_const=1.0, att_quad=0.0)
+
+
+def test_nee_picks_one_light_without_a_count_factor():
+    """Appendix A.2 (SimpleShader.h:111-148): next-event estimation picks ONE
+    light uniformly and adds its term with no 1/pdf (x N) factor.  Two identical
+    lights at one place therefore give the frame of one light, bit for bit (with
+    the factor it would be twice as bright)."""
+    one = oracle_ffi.Oracle(_plane_scene([_pt()])).render(24, 16, 4, 1, threads=2)
+    two = oracle_ffi.Oracle(_plane_scene([_pt(), _pt()])).render(24, 16, 4, 1, threads=2)
+    assert one.max() > 0.0
+    assert np.array_equal(one.view(np.uint32), two.view(np.uint32))
+
+
+def test_shadow_rays_test_about_one_unit():
+    """Appendix A.1 (Ray.cpp:11-15, SimpleShader.h:115-131): the shadow ray's
+    t_max is |lightpos - origin'| with lightpos = origin + the NORMALISED light
+    direction, i.e. about 1.  A light 2.5 above the plane; a black square 1.5
+    above it would shade the band x in (-1.1, -0.4) of the plane if the shadow
+    ray reached the light, but it is 1.6 units away along those rays and casts
+    nothing there; the same square at 0.6 above the plane (0.64 along the ray)
+    does shade.  Both squares cover the same camera rays (half-sizes scaled with
+    their distance), so the frames differ only by shadows."""
+    light = [_pt((0.5, 0.0, -0.5))]
+    # 32 spp: a point light's NEE term is zero for about half its sphere samples
+    # (Light.cpp:133-142), so a lit pixel is non-zero with probability 1 - 2^-32
+    none = oracle_ffi.Oracle(_plane_scene(light)).render(24, 16, 32, 1, threads=4)
+    far = oracle_ffi.Oracle(_plane_scene(light, occluder=(-1.5, 0.15, 0.0))).render(24, 16, 32, 1, threads=4)
+    near = oracle_ffi.Oracle(_plane_scene(light, occluder=(-2.4, 0.24, 0.0))).render(24, 16, 32, 1, threads=4)
+    lum = lambda im: im.sum(axis=-1)
+    assert (lum(none) > 0).all()
+    # the far square changes only the pixels its own image covers (and their edge)
+    changed = np.argwhere(lum(far) != lum(none))
+    covered = np.argwhere(lum(far) == 0.0)
+    assert len(covered) > 0
+    lo, hi = covered.min(axis=0) - 1, covered.max(axis=0) + 1
+    assert ((changed >= lo) & (changed <= hi)).all()
+    # the near square adds a shadow beside its image: darker pixels, never brighter
+    assert (lum(near) <= lum(far)).all() and (lum(near) < lum(far)).sum() > 4
+
+
+def test_ambient_term_per_hit():
+    """Appendix A.4 (SimpleShader.h:47): with no light and a black environment a
+    Lambert hit adds ambient * evaluateLight(n, n) / pi = ambient * diffuse /
+    pi^2, the whole pixel at depth 1."""
+    sd = _plane_scene([], diffuse=(0.5, 0.25, 1.0), ambient=(0.3, 0.6, 0.9))
+    img = oracle_ffi.Oracle(sd).render(24, 16, 2, 1, threads=2)
+    want = np.float32([0.3, 0.6, 0.9]) * (np.float32([0.5, 0.25, 1.0]) / np.float32(np.pi) / np.float32(np.pi))
+    assert np.allclose(img.reshape(-1, 3), want, rtol=2e-6)
