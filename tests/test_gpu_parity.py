@@ -194,6 +194,38 @@ def test_tiny_and_degenerate_trees(hip_ctx, name, path_kernel):
         hip_ctx.set_params(**old)
 
 
+def _quirk_scenes():
+    import test_oracle_kat as K
+    pl = lambda att=(1.0, 0.0, 0.0): S.point_light((0.5, 0.0, -0.5), (4.0, 3.0, 2.0), radius=0.01, att_const=att[0],
+                                                    att_lin=att[1], att_quad=att[2])
+    return {
+        "two_identical_lights": K._plane_scene([pl(), pl()]),
+        "occluder_0.6_above": K._plane_scene([pl()], occluder=(-2.4, 0.24, 0.0)),
+        "occluder_1.5_above": K._plane_scene([pl()], occluder=(-1.5, 0.15, 0.0)),
+        "ambient_only": K._plane_scene([], diffuse=(0.5, 0.25, 1.0), ambient=(0.3, 0.6, 0.9)),
+        "quadratic_attenuation_only": K._plane_scene([pl((0.0, 0.0, 0.5))]),
+    }
+
+
+@pytest.mark.parametrize("path_kernel", [1, 2])
+@pytest.mark.parametrize("name", ["two_identical_lights", "occluder_0.6_above", "occluder_1.5_above", "ambient_only",
+                                  "quadratic_attenuation_only"])
+def test_quirk_scenes(hip_ctx, name, path_kernel):
+    """The scenes that pin KIRK's integrator quirks in the oracle's known-answer
+    tests (tests/test_oracle_kat.py: one-light NEE without a count factor, the
+    ~1-unit shadow ray, the per-hit ambient term, the attenuation rule) render
+    the oracle's frames bit for bit through both kernels."""
+    sd = _quirk_scenes()[name]
+    want = oracle_ffi.Oracle(sd).render(24, 16, 8, 3, threads=16)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    old = hip_ctx.set_params(path_kernel=path_kernel)
+    try:
+        assert_parity(hip_ctx.render(24, 16, 8, 3), want, exact=True)
+    finally:
+        hip_ctx.set_params(**old)
+
+
 def test_rank_without_tiles(hip_ctx):
     """A rank that owns no tile (37x23 in 16-px tiles: 6 tiles for 8 ranks)
     renders nothing, synchronously or not, without an error; the ranks that do

@@ -384,3 +384,19 @@ def test_ambient_term_per_hit():
     img = oracle_ffi.Oracle(sd).render(24, 16, 2, 1, threads=2)
     want = np.float32([0.3, 0.6, 0.9]) * (np.float32([0.5, 0.25, 1.0]) / np.float32(np.pi) / np.float32(np.pi))
     assert np.allclose(img.reshape(-1, 3), want, rtol=2e-6)
+
+
+def test_distance_attenuation_rule():
+    """Appendix A.11 (Light.h:70-73): distanceAttenuation is 1 / (c + l d + q d^2)
+    only if c > 0 or (l > 0 and q > 0), otherwise 1.  So (0, 0, 0.5) -- a
+    quadratic term alone -- attenuates nothing and gives the frame of (0, 0, 0)
+    and of (1, 0, 0) bit for bit; (0, 1, 1) attenuates."""
+    def frame(att):
+        L = S.point_light((0.5, 0.0, -0.5), (4.0, 3.0, 2.0), radius=0.01, att_const=att[0], att_lin=att[1],
+                          att_quad=att[2])
+        return oracle_ffi.Oracle(_plane_scene([L])).render(24, 16, 4, 1, threads=2)
+    base = frame((0.0, 0.0, 0.0))
+    assert base.max() > 0.0
+    for att in ((0.0, 0.0, 0.5), (1.0, 0.0, 0.0)):
+        assert np.array_equal(frame(att).view(np.uint32), base.view(np.uint32)), att
+    assert frame((0.0, 1.0, 1.0)).sum() < base.sum()
