@@ -204,24 +204,27 @@ def _quirk_scenes():
         "occluder_1.5_above": K._plane_scene([pl()], occluder=(-1.5, 0.15, 0.0)),
         "ambient_only": K._plane_scene([], diffuse=(0.5, 0.25, 1.0), ambient=(0.3, 0.6, 0.9)),
         "quadratic_attenuation_only": K._plane_scene([pl((0.0, 0.0, 0.5))]),
+        "dark_box_depth9": K._dark_box(),
     }
 
 
 @pytest.mark.parametrize("path_kernel", [1, 2])
 @pytest.mark.parametrize("name", ["two_identical_lights", "occluder_0.6_above", "occluder_1.5_above", "ambient_only",
-                                  "quadratic_attenuation_only"])
+                                  "quadratic_attenuation_only", "dark_box_depth9"])
 def test_quirk_scenes(hip_ctx, name, path_kernel):
     """The scenes that pin KIRK's integrator quirks in the oracle's known-answer
     tests (tests/test_oracle_kat.py: one-light NEE without a count factor, the
-    ~1-unit shadow ray, the per-hit ambient term, the attenuation rule) render
+    ~1-unit shadow ray, the per-hit ambient term, the attenuation rule, the
+    throughput cut without Russian roulette) render
     the oracle's frames bit for bit through both kernels."""
     sd = _quirk_scenes()[name]
-    want = oracle_ffi.Oracle(sd).render(24, 16, 8, 3, threads=16)
+    depth = 9 if name.startswith("dark_box") else 3
+    want = oracle_ffi.Oracle(sd).render(24, 16, 8, depth, threads=16)
     hip_ctx.set_scene(sd)
     hip_ctx.build_accel()
     old = hip_ctx.set_params(path_kernel=path_kernel)
     try:
-        assert_parity(hip_ctx.render(24, 16, 8, 3), want, exact=True)
+        assert_parity(hip_ctx.render(24, 16, 8, depth), want, exact=True)
     finally:
         hip_ctx.set_params(**old)
 

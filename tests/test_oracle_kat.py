@@ -400,3 +400,34 @@ def test_distance_attenuation_rule():
     for att in ((0.0, 0.0, 0.5), (1.0, 0.0, 0.0)):
         assert np.array_equal(frame(att).view(np.uint32), base.view(np.uint32)), att
     assert frame((0.0, 1.0, 1.0)).sum() < base.sum()
+
+
+def _dark_box():
+    """The Cornell box of scenes.cornell_box with every wall Lambert, diffuse 0.1."""
+    sd = S.SceneData(name="dark_box")
+    dark = sd.add_material(S.material(diffuse=(0.1, 0.1, 0.1)))
+    a, b = -0.5, 0.5
+    for v, n in [S.quad((a, 0, a), (b, 0, a), (b, 0, b), (a, 0, b), (0, 1, 0)),
+                 S.quad((a, 1, a), (a, 1, b), (b, 1, b), (b, 1, a), (0, -1, 0)),
+                 S.quad((a, 0, a), (a, 1, a), (b, 1, a), (b, 0, a), (0, 0, 1)),
+                 S.quad((a, 0, a), (a, 0, b), (a, 1, b), (a, 1, a), (1, 0, 0)),
+                 S.quad((b, 0, a), (b, 1, a), (b, 1, b), (b, 0, b), (-1, 0, 0))]:
+        sd.add_triangles(v, n, dark)
+    sd.lights.append(S.quad_light((0.0, 0.999, 0.0), (0.0, -1.0, 0.0), (0.25, 0.25), (17.0, 12.0, 4.0),
+                                  att_const=1.0, att_lin=0.0, att_quad=0.0))
+    sd.env_color = (0.0, 0.0, 0.0)
+    sd.env_ambient = (0.0, 0.0, 0.0)
+    sd.cam = S.camera((0.0, 0.5, 1.85), (0.0, 0.0, -1.0), (0.0, 1.0, 0.0), 16, 16)
+    return sd
+
+
+def test_throughput_cut_without_russian_roulette():
+    """Appendix A.5 (SimpleShader.h:61-68): no Russian roulette; a path stops
+    when max(T) < 0.01 (checked before the update).  In a box whose every wall
+    is Lambert with diffuse 0.1, cosine sampling multiplies T by ~0.1 per
+    bounce, so every path has stopped by its fourth hit: depth 5 and depth 9
+    give the same frame bit for bit, while depth 2 does not."""
+    o = oracle_ffi.Oracle(_dark_box())
+    d5, d9, d2 = (o.render(16, 16, 4, d, threads=2) for d in (5, 9, 2))
+    assert np.array_equal(d5.view(np.uint32), d9.view(np.uint32))
+    assert not np.array_equal(d2.view(np.uint32), d5.view(np.uint32))
