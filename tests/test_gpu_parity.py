@@ -229,6 +229,26 @@ def test_quirk_scenes(hip_ctx, name, path_kernel):
         hip_ctx.set_params(**old)
 
 
+@pytest.mark.parametrize("trace_kernels", [0, 1, 2])
+@pytest.mark.parametrize("n_extra", [0, 64])
+def test_equal_t_within_a_leaf(hip_ctx, n_extra, trace_kernels):
+    """Appendix A.9: of two coincident triangles in one leaf the later candidate
+    is the closest hit (t <= best inside a leaf) -- through the batch query
+    kernel and the production traversal kernels (trace_kernels 1: the 64-B
+    loop, 2: with the two-level records), as in the oracle's known-answer test."""
+    import test_oracle_kat as K
+    sd = K._coincident_tris(n_extra)
+    want_t, want_obj, want_uv, _, _ = oracle_ffi.Oracle(sd).trace_closest([[0.0, -0.3, 3.0]], [[0.0, 0.0, -1.0]])
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    old = hip_ctx.set_params(trace_kernels=trace_kernels, wide_from=0 if trace_kernels == 2 else 2)
+    try:
+        t, obj, uv = hip_ctx.trace_closest([[0.0, -0.3, 3.0]], [[0.0, 0.0, -1.0]])
+    finally:
+        hip_ctx.set_params(**old)
+    assert obj[0] == want_obj[0] == 1 and t[0] == want_t[0] and np.array_equal(uv, want_uv)
+
+
 def test_rank_without_tiles(hip_ctx):
     """A rank that owns no tile (37x23 in 16-px tiles: 6 tiles for 8 ranks)
     renders nothing, synchronously or not, without an error; the ranks that do

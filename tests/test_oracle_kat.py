@@ -431,3 +431,34 @@ def test_throughput_cut_without_russian_roulette():
     d5, d9, d2 = (o.render(16, 16, 4, d, threads=2) for d in (5, 9, 2))
     assert np.array_equal(d5.view(np.uint32), d9.view(np.uint32))
     assert not np.array_equal(d2.view(np.uint32), d5.view(np.uint32))
+
+
+def _coincident_tris(n_extra=0):
+    """Two identical triangles (one leaf of two candidates), optionally beside
+    n_extra small far-away triangles so that the pair sits in a deeper leaf."""
+    sd = S.SceneData(name="coincident")
+    m = sd.add_material(S.material())
+    tri = np.float32([[[-1, -1, 0], [1, -1, 0], [0, 1, 0]]])
+    v = np.concatenate([tri, tri])
+    if n_extra:
+        c = np.random.default_rng(5).uniform(5, 9, (n_extra, 3)).astype(np.float32)
+        v = np.concatenate([v, c[:, None, :] + np.float32([[0, 0, 0], [0.1, 0, 0], [0, 0.1, 0]])[None]])
+    sd.add_triangles(v, np.broadcast_to(np.float32([0, 0, 1]), v.shape).copy(), m)
+    sd.cam = S.camera((0, 0, 5), (0, 0, -1), width=8, height=8)
+    return sd
+
+
+@pytest.mark.parametrize("n_extra", [0, 64])
+def test_equal_t_within_a_leaf_takes_the_later_candidate(n_extra):
+    """Appendix A.9 (CPU_BVH.cpp:159-167, Container.cpp:13-25): inside a leaf a
+    candidate is accepted at t <= the current best (the later of two equal-t
+    candidates wins), across leaves only at t < the best.  Two coincident
+    triangles share a leaf, so the closest hit is the one listed later in it."""
+    o = oracle_ffi.Oracle(_coincident_tris(n_extra))
+    boxes, first, count, ids, depth = o.bvh()
+    leaf = [k for k in range(len(count)) if count[k] > 0 and 0 in ids[first[k]:first[k] + count[k]]][0]
+    members = list(ids[first[leaf]:first[leaf] + count[leaf]])
+    assert {0, 1} <= set(members)   # both in one leaf
+    later = [i for i in members if i in (0, 1)][-1]
+    t, obj, uv, _, _ = o.trace_closest([[0.0, -0.3, 3.0]], [[0.0, 0.0, -1.0]])
+    assert abs(t[0] - 3.0) < 1e-6 and obj[0] == later
