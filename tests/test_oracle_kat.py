@@ -223,6 +223,11 @@ def test_glass_normal_incidence(hair_oracle):
     assert np.allclose(r["f"], (1 - F) / 1.5 ** 2, rtol=1e-5)
     r = hair_oracle.bsdf_sample(0, m, [0, 0, 1], [0, 0, 1], [0.5, 0.01], [0, 0])  # sample.y < F -> reflect
     assert np.allclose(r["out"], [0, 0, 1], atol=1e-6) and abs(r["pdf"] - F) < 1e-6
+    # Appendix A.10: the CPU decides on sample.y (Bsdf.cpp:343; the GLSL used .x)
+    assert np.allclose(hair_oracle.bsdf_sample(0, m, [0, 0, 1], [0, 0, 1], [0.01, 0.9], [0, 0])["out"], [0, 0, -1],
+                       atol=1e-6)
+    assert np.allclose(hair_oracle.bsdf_sample(0, m, [0, 0, 1], [0, 0, 1], [0.9, 0.01], [0, 0])["out"], [0, 0, 1],
+                       atol=1e-6)
 
 
 def test_emission_and_transparent(hair_oracle):
@@ -462,3 +467,26 @@ def test_equal_t_within_a_leaf_takes_the_later_candidate(n_extra):
     later = [i for i in members if i in (0, 1)][-1]
     t, obj, uv, _, _ = o.trace_closest([[0.0, -0.3, 3.0]], [[0.0, 0.0, -1.0]])
     assert abs(t[0] - 3.0) < 1e-6 and obj[0] == later
+
+
+def _mirror_scene():
+    sd = S.SceneData(name="mirror")
+    m = sd.add_material(S.material("SpecularReflectionBSDF", specular=(0.5, 0.25, 1.0)))
+    sd.add_triangles(*S.quad((-20, -20, -3), (20, -20, -3), (20, 20, -3), (-20, 20, -3), (0, 0, 1)), m)
+    sd.env_color = (0.2, 0.4, 0.8)
+    sd.env_ambient = (0.0, 0.0, 0.0)
+    sd.cam = S.camera((0, 0, 0), (0, 0, -1), width=8, height=8)
+    return sd
+
+
+def test_misses_add_the_environment_at_any_depth():
+    """Appendix A.6 (CPU_PathTracer.cpp:141-145, EnvironmentShader.h:20-26): a
+    ray that leaves the scene adds env(d) * T at whatever depth.  A camera that
+    sees only a mirror (SpecularReflectionBSDF, specular s) under a constant
+    environment e and no light: every bounce-1 ray escapes, so each pixel is
+    e * s (the mirror's T factor s |cos| / |cos|), and 0 at depth 1 (the
+    camera ray hits the mirror and adds nothing there)."""
+    o = oracle_ffi.Oracle(_mirror_scene())
+    assert np.array_equal(o.render(8, 8, 2, 1, threads=1), np.zeros((8, 8, 3), np.float32))
+    img = o.render(8, 8, 2, 3, threads=1)
+    assert np.allclose(img.reshape(-1, 3), np.float32([0.2, 0.4, 0.8]) * np.float32([0.5, 0.25, 1.0]), rtol=1e-5)
