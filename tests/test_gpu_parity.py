@@ -206,18 +206,21 @@ def _quirk_scenes():
         "quadratic_attenuation_only": K._plane_scene([pl((0.0, 0.0, 0.5))]),
         "dark_box_depth9": K._dark_box(),
         "mirror_under_environment": K._mirror_scene(),
+        "inside_point_light_behind": K._inside_point_light(-0.1),
+        "inside_point_light_front": K._inside_point_light(0.1),
     }
 
 
 @pytest.mark.parametrize("path_kernel", [1, 2])
 @pytest.mark.parametrize("name", ["two_identical_lights", "occluder_0.6_above", "occluder_1.5_above", "ambient_only",
-                                  "quadratic_attenuation_only", "dark_box_depth9", "mirror_under_environment"])
+                                  "quadratic_attenuation_only", "dark_box_depth9", "mirror_under_environment",
+                                  "inside_point_light_behind", "inside_point_light_front"])
 def test_quirk_scenes(hip_ctx, name, path_kernel):
     """The scenes that pin KIRK's integrator quirks in the oracle's known-answer
     tests (tests/test_oracle_kat.py: one-light NEE without a count factor, the
     ~1-unit shadow ray, the per-hit ambient term, the attenuation rule, the
     throughput cut without Russian roulette, misses adding the environment at
-    any depth) render
+    any depth, the point light's rejection of rays leaving its centre) render
     the oracle's frames bit for bit through both kernels."""
     sd = _quirk_scenes()[name]
     depth = 9 if name.startswith("dark_box") else 3

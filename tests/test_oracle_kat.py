@@ -490,3 +490,29 @@ def test_misses_add_the_environment_at_any_depth():
     assert np.array_equal(o.render(8, 8, 2, 1, threads=1), np.zeros((8, 8, 3), np.float32))
     img = o.render(8, 8, 2, 3, threads=1)
     assert np.allclose(img.reshape(-1, 3), np.float32([0.2, 0.4, 0.8]) * np.float32([0.5, 0.25, 1.0]), rtol=1e-5)
+
+
+def _inside_point_light(offset):
+    """A camera inside a point light's sphere (radius 0.8, Light.h:131), the
+    light's centre `offset` along the view direction; nothing else but a
+    constant environment."""
+    sd = S.SceneData(name="inside_light")
+    m = sd.add_material(S.material())
+    sd.add_triangles(*S.quad((100, 100, 100), (101, 100, 100), (101, 101, 100), (100, 101, 100), (0, 0, 1)), m)
+    sd.lights.append(S.point_light((0.0, 0.0, -offset), (2.0, 3.0, 4.0), radius=0.8, att_const=1.0, att_quad=0.0))
+    sd.env_color = (0.25, 0.5, 0.75)
+    sd.env_ambient = (0.0, 0.0, 0.0)
+    sd.cam = S.camera((0, 0, 0), (0, 0, -1), width=8, height=8)
+    return sd
+
+
+def test_point_light_rejects_rays_leaving_its_centre():
+    """Appendix A.3 (Light.cpp:174-175): a point light's sphere rejects a ray
+    with dir . (o - pos) > 0.  From inside the sphere, with the centre 0.1
+    BEHIND the camera every camera ray leaves the centre and sees the
+    environment alone; with the centre 0.1 IN FRONT the rays hit the sphere
+    from inside and add the light (every ray, at every depth)."""
+    behind = oracle_ffi.Oracle(_inside_point_light(-0.1)).render(8, 8, 2, 3, threads=1)
+    front = oracle_ffi.Oracle(_inside_point_light(0.1)).render(8, 8, 2, 3, threads=1)
+    assert np.array_equal(behind, np.broadcast_to(np.float32([0.25, 0.5, 0.75]), behind.shape))
+    assert (front.sum(axis=-1) != behind.sum(axis=-1)).all()
