@@ -3190,9 +3190,16 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         HIPCHK(w.lvb.ensure(lv_bytes));
     }
     const int dump_b = (!async && !ops) ? c->prm.dump_bounce : -1;
-    // the path kernel (khp_ctx_params.path_kernel): automatic for synchronous renders
+    // the path kernel (khp_ctx_params.path_kernel): automatic for synchronous renders of at
+    // most PATH_AUTO_MAX paths.  At the metric row a synchronous call of s spp takes
+    // 8.0 / 12.5 / 16.7 / 20.8 / 29.4 / 37.6 ms through it for s = 1 / 2 / 3 / 4 / 6 / 8
+    // against 14.0 / 17.9 / 21.4 / 24.7 / 31.2 / 37.2 through the wavefront
+    // (profiles/r04aa_sync_spp.json): the wavefront's better steady rate wins from ~7.5 spp
+    constexpr size_t PATH_AUTO_MAX = (size_t)14 << 20;
     const bool path_ok = !stats && !bdm && c->prm.shade_order == 0 && dump_b < 0;
-    const bool use_path = path_ok && (c->prm.path_kernel == 2 || (c->prm.path_kernel == 0 && !async));
+    const size_t call_paths = (size_t)P_all * p->spp * nf;
+    const bool use_path = path_ok && (c->prm.path_kernel == 2 ||
+                                      (c->prm.path_kernel == 0 && !async && call_paths <= PATH_AUTO_MAX));
     const bool path_wide = use_path && c->S.wide != nullptr && c->prm.wide_from == 0;
     PathLanes PL{};
     SpillArea sp_path{nullptr, 0};

@@ -428,7 +428,8 @@ def main():
         sync_line = {"value": round(args.sync_check_steps * samples_per_step / sync_el / 1e6, 3),
                      "ms_per_step": round(sync_el / args.sync_check_steps * 1e3, 3), "steps": args.sync_check_steps,
                      "def": "one synchronous khp_render per pass (+ gather), no frame fusion; synchronous renders "
-                            f"run the path kernel (khp_ctx_params.path_kernel = {params['path_kernel']}, 0 = automatic)"}
+                            f"run the path kernel up to 14 x 2^20 paths per call and the wavefront above "
+                            f"(khp_ctx_params.path_kernel = {params['path_kernel']}, 0 = automatic)"}
 
     # KIRK's GUI pattern (CPU_PathTracer.cpp:17-52): every
     # render() call adds ONE sample to every pixel synchronously and the viewer

@@ -307,8 +307,10 @@ typedef struct {
                                     traces, shades, traces the shadow ray and continues with the next bounce)
                                     instead of the per-bounce wavefront, whose every launch ends with its
                                     slowest ray.  Automatic: synchronous renders (KIRK's own one-call-per-pass
-                                    use).  Not with the light-path variant, hit sorting, instrumented renders
-                                    or queue dumps (those always run the wavefront).  Measured in DESIGN.md */
+                                    use) of at most 14 x 2^20 paths (1080p up to 7 spp; past that the
+                                    wavefront's steady rate wins).  Not with the light-path variant, hit
+                                    sorting, instrumented renders or queue dumps (those always run the
+                                    wavefront).  Measured in DESIGN.md §5b                              */
 } khp_ctx_params;
 
 /* ---- context --------------------------------------------------------------- */
