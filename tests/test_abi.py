@@ -8,7 +8,6 @@ import re
 import subprocess
 import sys
 
-import numpy as np
 import pytest
 
 from ba_pathtracing_fur_amd import native as N

@@ -8,10 +8,8 @@ rounding differ from float64), and the oracle renders scenes built from it;
 tests/test_gpu_flatten.py checks the device generator and GPU frames bit for bit.
 """
 import numpy as np
-import pytest
 
 import oracle_ffi
-from ba_pathtracing_fur_amd import native as N
 from ba_pathtracing_fur_amd import scenes as S
 
 

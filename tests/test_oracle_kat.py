@@ -8,7 +8,6 @@ import numpy as np
 import pytest
 
 import oracle_ffi
-from ba_pathtracing_fur_amd import native as N
 from ba_pathtracing_fur_amd import scenes as S
 
 FLT_MAX = np.float32(3.4028234663852886e38)
