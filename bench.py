@@ -281,37 +281,49 @@ def cpu_baseline(sd, args, budget_s):
                       f"seeds); throughput is spp-linear; oracle BVH build {build_s:.1f} s excluded"}
 
 
+def _pmc_profile(config: str, frames_per_launch: float | None = None):
+    """The committed PMC profile of k_extend for this workload (tools/summarize_prof.py):
+    among the newest round's profiles, the one whose launches carried the number of
+    fused frames nearest this run's (the driver's 20 passes: 10 per launch; the
+    default 32: 8), else the newest.  Returns (file name, contents) or (None, None)."""
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_extend_*.json")))
+    files = [f for f in files if ("_cfg" not in f) == (config == "metric") and
+             (config == "metric" or f"_cfg{config}_" in f)]
+    loaded = []
+    for f in files:
+        try:
+            with open(f) as fh:
+                loaded.append((os.path.basename(f), json.load(fh)))
+        except Exception:
+            continue
+    if not loaded:
+        return None, None
+    rnd = lambda name: name[len("pmc_extend_"):len("pmc_extend_") + 3]   # "r04"
+    newest = max(rnd(n) for n, _ in loaded)
+    cands = [(n, d) for n, d in loaded if rnd(n) == newest]
+    if frames_per_launch is not None:
+        return min(cands, key=lambda nd: (abs(nd[1].get("frames_per_launch", 1) - frames_per_launch),
+                                          -cands.index(nd)))
+    return cands[-1]
+
+
 def pmc_traffic(frames_per_launch: float, config: str):
     """HBM bytes per k_extend launch from the committed PMC profile of this
     workload, scaled to this run's frames per launch (the profile records how
     many fused frames its launches carried), or None."""
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_extend_*.json")))
-    files = [f for f in files if ("_cfg" not in f) == (config == "metric") and
-             (config == "metric" or f"_cfg{config}_" in f)]
-    if not files:
-        return None
+    name, d = _pmc_profile(config, frames_per_launch)
     try:
-        with open(files[-1]) as f:
-            d = json.load(f)
-        return int(d["bytes_per_launch"] / d.get("frames_per_launch", 1) * frames_per_launch)
+        return int(d["bytes_per_launch"] / d.get("frames_per_launch", 1) * frames_per_launch) if d else None
     except Exception:
         return None
 
 
-def pmc_per_bounce(config: str):
-    """Per-bounce measured / algorithmic read bytes of k_extend from the newest
-    committed PMC profile of this workload (tools/summarize_prof.py), or None."""
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_extend_*.json")))
-    files = [f for f in files if ("_cfg" not in f) == (config == "metric") and
-             (config == "metric" or f"_cfg{config}_" in f)]
-    for f in reversed(files):
-        try:
-            with open(f) as fh:
-                d = json.load(fh)
-        except Exception:
-            continue
-        if d.get("per_bounce"):
-            return os.path.basename(f), d["per_bounce"]
+def pmc_per_bounce(config: str, frames_per_launch: float | None = None):
+    """Per-bounce measured / algorithmic read bytes of k_extend from the same
+    committed PMC profile (tools/summarize_prof.py), or None."""
+    name, d = _pmc_profile(config, frames_per_launch)
+    if d and d.get("per_bounce"):
+        return name, d["per_bounce"]
     return None, None
 
 
@@ -496,7 +508,7 @@ def main():
     traffic = None if args.bdpt else pmc_traffic(frames_per_launch, args.config)  # profiles are of the default estimator
     # per bounce: this run's algorithmic rate (exact visit counts, HIP-event launch
     # times) next to the measured/algorithmic read ratio of the committed profile
-    prof_name, prof_pb = (None, None) if args.bdpt else pmc_per_bounce(args.config)
+    prof_name, prof_pb = (None, None) if args.bdpt else pmc_per_bounce(args.config, frames_per_launch)
     per_bounce_rl = []
     for b in range(min(depth, 16)):
         r_b = cnt["bounce_rays"][b]
