@@ -62,3 +62,26 @@ def test_available_cores(bench):
     n, src = bench.available_cores()
     assert 1 <= n <= len(os.sched_getaffinity(0))
     assert src in ("sched_getaffinity", "cgroup cpu.max quota")
+
+
+def test_traffic_profile_matches_the_launch_shape(bench, tmp_path, monkeypatch):
+    """`roofline.traffic` comes from the newest round's committed PMC profile
+    whose launches carried the nearest number of fused frames, scaled to the
+    run's frames per launch; config profiles are kept apart from the metric's."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    def put(name, bytes_per_launch, fpl):
+        (prof / f"pmc_extend_{name}.json").write_text(json.dumps(
+            {"bytes_per_launch": bytes_per_launch, "frames_per_launch": fpl, "per_bounce": [{"bounce": 0}]}))
+    put("r03s", 999, 10.0)          # an older round, even with the exact shape, is not taken
+    put("r04a", 800, 8.0)
+    put("r04b", 1000, 10.0)
+    put("r04c_cfg5_", 50, 1.0)
+    monkeypatch.setattr(bench, "HERE", str(tmp_path))
+    assert bench._pmc_profile("metric", 10.0)[0] == "pmc_extend_r04b.json"
+    assert bench._pmc_profile("metric", 8.0)[0] == "pmc_extend_r04a.json"
+    assert bench.pmc_traffic(10.0, "metric") == 1000 and bench.pmc_traffic(8.0, "metric") == 800
+    assert bench._pmc_profile("metric", 9.0)[0] == "pmc_extend_r04b.json"   # a tie goes to the newer profile
+    assert bench._pmc_profile("5", 1.0)[0] == "pmc_extend_r04c_cfg5_.json"
+    assert bench._pmc_profile("2", 1.0) == (None, None)
+    assert bench.pmc_per_bounce("metric", 8.0)[0] == "pmc_extend_r04a.json"
