@@ -885,11 +885,19 @@ __device__ __forceinline__ void block_alloc2(bool p0, bool p1, uint32_t* c0, uin
     __syncthreads();  // sh is reused by the next iteration
 }
 
+// k_shade's block: 512 threads (8 waves).  Its queue allocation is one device atomic
+// per output kind per block iteration; 512-thread blocks halve those against 256 and
+// measured +1.4% (default bench) / +1.6% (driver's command) on the whole frame; 128
+// threads doubled them and lost 4% (profiles/r04ah_shade_block.json).
+#ifndef KHP_SHADE_BLOCK
+#define KHP_SHADE_BLOCK 512
+#endif
+constexpr uint32_t SHADE_BLOCK = KHP_SHADE_BLOCK, SHADE_NW = KHP_SHADE_BLOCK / 64;
 // Four outputs (next-bounce rays and shadow rays, each front or back): a lane
 // sets at most one of p0/p1 and one of p2/p3; i01 / i23 is its index in the
 // queue it was counted in.
 struct BlockAlloc4 {
-    uint32_t wcnt[4][4];
+    uint32_t wcnt[4][SHADE_NW];
     uint32_t base[4];
 };
 __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3, uint32_t* c0, uint32_t* c1,
@@ -903,7 +911,8 @@ __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3,
     __syncthreads();
     if (threadIdx.x < 4) {
         const uint32_t q = threadIdx.x;
-        const uint32_t tot = sh.wcnt[q][0] + sh.wcnt[q][1] + sh.wcnt[q][2] + sh.wcnt[q][3];
+        uint32_t tot = 0;
+        for (uint32_t w = 0; w < SHADE_NW; ++w) tot += sh.wcnt[q][w];
         uint32_t* ctr = q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : c3;
         sh.base[q] = tot ? atomicAdd(ctr, tot) : 0u;
     }
@@ -922,7 +931,7 @@ __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3,
 #define KHP_SHADE_WAVES 1   // min waves per SIMD for k_shade's register budget (1: unconstrained)
 #endif
 template <bool TEX, bool BD, uint32_t KINDS = 0xFFFFFFFFu>
-__global__ __launch_bounds__(256, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
+__global__ __launch_bounds__(KHP_SHADE_BLOCK, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
     const uint32_t nf = Wv.cnt->nq[cur], n = nf + Wv.cnt->nqb[cur];
     const int nxt = cur ^ 1;
     const bool last = bounce + 1 >= Wv.depth;
@@ -2751,10 +2760,10 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     for (const khp_material& m : hs.mats)
         c->bsdf_kinds |= (m.bsdf >= 0 && m.bsdf < KHP_BSDF_COUNT) ? (1u << m.bsdf) : KINDS_ALL;
     nb = 0;
-    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<true, false>), 256, 0));
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<true, false>), SHADE_BLOCK, 0));
     else if ((c->bsdf_kinds & ~KINDS_FUR) == 0u)
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false, KINDS_FUR>), 256, 0));
-    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false>), 256, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false, KINDS_FUR>), SHADE_BLOCK, 0));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false>), SHADE_BLOCK, 0));
     c->grid_shade = std::max(1, nb) * c->n_cu;
     nb = 0;
     if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, false, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
@@ -3353,16 +3362,16 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     hipLaunchKernelGGL(k_hit_scatter, dim3(c->grid_shade), dim3(256), 0, sA, Wb, cur);
                 }
                 if (c->S.textured && bdm)
-                    hipLaunchKernelGGL((k_shade<true, true>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                    hipLaunchKernelGGL((k_shade<true, true>), dim3(c->grid_shade), dim3(SHADE_BLOCK), 0, sA, c->S, Wb, cur, b);
                 else if (c->S.textured)
-                    hipLaunchKernelGGL((k_shade<true, false>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                    hipLaunchKernelGGL((k_shade<true, false>), dim3(c->grid_shade), dim3(SHADE_BLOCK), 0, sA, c->S, Wb, cur, b);
                 else if (bdm)
-                    hipLaunchKernelGGL((k_shade<false, true>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                    hipLaunchKernelGGL((k_shade<false, true>), dim3(c->grid_shade), dim3(SHADE_BLOCK), 0, sA, c->S, Wb, cur, b);
                 else if ((c->bsdf_kinds & ~KINDS_FUR) == 0u)   // fur scenes: the other BSDF kinds compiled out
-                    hipLaunchKernelGGL((k_shade<false, false, KINDS_FUR>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb,
+                    hipLaunchKernelGGL((k_shade<false, false, KINDS_FUR>), dim3(c->grid_shade), dim3(SHADE_BLOCK), 0, sA, c->S, Wb,
                                        cur, b);
                 else
-                    hipLaunchKernelGGL((k_shade<false, false>), dim3(c->grid_shade), dim3(256), 0, sA, c->S, Wb, cur, b);
+                    hipLaunchKernelGGL((k_shade<false, false>), dim3(c->grid_shade), dim3(SHADE_BLOCK), 0, sA, c->S, Wb, cur, b);
                 timed(c, f, 1, false, sA);
                 if (sB != sA) {
                     hipEvent_t shaded = slot_event(f.sync_pool, f.sync_next, true);
