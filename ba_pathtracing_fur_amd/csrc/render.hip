@@ -21,6 +21,7 @@
 #include <memory>
 #include <string>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <thread>
 #include <type_traits>
@@ -1556,6 +1557,16 @@ __device__ __forceinline__ v3 finish_acc(const DevScene& S, const Ray& r, float 
 
 enum : uint32_t { PS_TRAV = 0u, PS_FIN = 1u, PS_NEW = 2u, PS_BEGIN = 3u, PS_DONE = 4u };
 
+#ifdef KHP_PATH_PROFILE
+// Diagnostic builds: one record per k_path wave (100 MHz wall clock): start,
+// claim exhaustion seen, end, (traversal-loop iterations << 32 | those after
+// exhaustion), traversing lanes summed over the drain iterations, (block << 32 |
+// lanes with a path at exhaustion).  Read and reset by khp_debug_wave_profile.
+#define KHP_WPROF_MAX 65536
+__device__ unsigned long long g_wprof[6 * KHP_WPROF_MAX];
+__device__ uint32_t g_wprof_n;
+#endif
+
 template <bool TEX, bool WIDE, uint32_t KINDS>
 __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wave Wv, SpillArea spill, PathLanes L) {
     extern __shared__ uint32_t lds[];
@@ -1579,10 +1590,15 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     // claim exhaustion seen, last end, longest drain of one wave (its end - its exhaustion)
     const unsigned long long pc_start = wall_clock64();
     unsigned long long pc_exh = 0;
+    uint32_t pw_iters = 0, pw_drain_iters = 0, pw_ntrav_exh = 0;   // per-wave record (g_wprof)
+    unsigned long long pw_drain_lanes = 0;
 #endif
     for (;;) {
 #ifdef KHP_PATH_PROFILE
-        if (exhausted && pc_exh == 0) pc_exh = wall_clock64();
+        if (exhausted && pc_exh == 0) {
+            pc_exh = wall_clock64();
+            pw_ntrav_exh = (uint32_t)__popcll(__ballot(state == PS_TRAV || state == PS_FIN || state == PS_BEGIN));
+        }
 #endif
         // ---- service: shade finished extension rays, finish shadow rays, claim camera
         //      paths, start traversals -- until every lane traverses or has no work left
@@ -1708,6 +1724,13 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
             }
             const uint32_t ntrav = (uint32_t)__popcll(__ballot(state == PS_TRAV));
             const uint32_t nfin = (uint32_t)__popcll(__ballot(state == PS_FIN));
+#ifdef KHP_PATH_PROFILE
+            ++pw_iters;
+            if (pc_exh != 0) {
+                ++pw_drain_iters;
+                pw_drain_lanes += ntrav;
+            }
+#endif
             // refill at REFILL finished lanes; once every path is claimed, as soon as
             // the finished lanes are as many as those still traversing (the drain;
             // servicing at every finished lane there measured 5% slower)
@@ -1727,6 +1750,16 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
         atomicMax(&Wv.cnt->step_cycles[1], pc_exh);
         atomicMax(&Wv.cnt->step_cycles[2], pc_end);
         atomicMax(&Wv.cnt->step_cycles[3], pc_end - pc_exh);
+        const uint32_t slot = atomicAdd(&g_wprof_n, 1u);
+        if (slot < KHP_WPROF_MAX) {
+            unsigned long long* r = g_wprof + 6 * (size_t)slot;
+            r[0] = pc_start;
+            r[1] = pc_exh;
+            r[2] = pc_end;
+            r[3] = ((unsigned long long)pw_iters << 32) | pw_drain_iters;
+            r[4] = pw_drain_lanes;
+            r[5] = ((unsigned long long)blockIdx.x << 32) | pw_ntrav_exh;
+        }
 #endif
     }
 }
@@ -2135,6 +2168,7 @@ struct Snapshot {
     uint8_t* pinned = nullptr;
     hipEvent_t done = nullptr;
     bool enqueued = false;
+    bool touched = false;   // an asynchronous operation on dbuf / pinned was queued (snapshot_now)
 };
 static hipEvent_t slot_event(std::vector<hipEvent_t>& pool, size_t& next, bool no_timing) {
     if (next == pool.size()) {
@@ -2209,6 +2243,17 @@ struct khp_ctx {
     uint32_t comm_timeout_ms = 120000;
     std::string comm_dead;   // why the comm was aborted ("" while alive or never created)
     std::shared_ptr<void> comm_job;   // the init's arguments (CommInitJob), kept while the comm lives
+    // RCCL operations enqueued on the stream, oldest first: `pre` is recorded just
+    // before the operation (it can run once pre has completed), `post` just after.
+    // The bound of a device wait counts only the time an operation has been
+    // runnable without completing: compute alone never times out.
+    struct CommOp {
+        hipEvent_t pre = nullptr, post = nullptr;
+        bool runnable = false;
+        std::chrono::steady_clock::time_point since;
+    };
+    std::deque<CommOp> comm_ops;
+    std::vector<hipEvent_t> comm_evt_free;
     // ABI 8 in-process group (khp_comm_init_local): the gather's transport between
     // contexts of one process instead of RCCL; a sender's k-th gather packs into
     // ring slot k % LG_SLOTS, the root's k-th gather copies every sender's slot k.
@@ -2256,9 +2301,50 @@ static khp_status comm_abort(khp_ctx* c, const std::string& why) {
 }
 static bool bounded_waits(const khp_ctx* c) { return c->comm != nullptr || !c->comm_dead.empty(); }
 
+// Brackets of an RCCL operation on the context stream (CommOp).
+static hipError_t comm_evt(khp_ctx* c, hipEvent_t* e) {
+    if (!c->comm_evt_free.empty()) {
+        *e = c->comm_evt_free.back();
+        c->comm_evt_free.pop_back();
+        return hipSuccess;
+    }
+    return hipEventCreateWithFlags(e, hipEventDisableTiming);
+}
+static hipError_t comm_op_begin(khp_ctx* c) {
+    khp_ctx::CommOp op;
+    hipError_t e = comm_evt(c, &op.pre);
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(op.pre, c->stream);
+    if (e != hipSuccess) {
+        c->comm_evt_free.push_back(op.pre);
+        return e;
+    }
+    c->comm_ops.push_back(op);
+    return hipSuccess;
+}
+static hipError_t comm_op_end(khp_ctx* c) {
+    khp_ctx::CommOp& op = c->comm_ops.back();
+    hipError_t e = comm_evt(c, &op.post);
+    if (e != hipSuccess) return e;
+    return hipEventRecord(op.post, c->stream);
+}
+// The oldest RCCL operation that has not completed, after retiring the
+// completed ones (nullptr: none in flight).  An operation whose `post` was never
+// recorded (its enqueue failed) is retired once its `pre` has completed.
+static khp_ctx::CommOp* comm_op_pending(khp_ctx* c) {
+    while (!c->comm_ops.empty()) {
+        khp_ctx::CommOp& op = c->comm_ops.front();
+        const hipError_t q = hipEventQuery(op.post ? op.post : op.pre);
+        if (q == hipErrorNotReady) return &op;
+        for (hipEvent_t e : {op.pre, op.post})
+            if (e) c->comm_evt_free.push_back(e);
+        c->comm_ops.pop_front();
+    }
+    return nullptr;
+}
+
 template <typename Query>
 static khp_status poll_wait(khp_ctx* c, Query query, const char* what) {
-    const auto t0 = std::chrono::steady_clock::now();
     for (int spins = 0;; ++spins) {
         const hipError_t q = query();
         if (q == hipSuccess) return KHP_OK;
@@ -2270,7 +2356,19 @@ static khp_status poll_wait(khp_ctx* c, Query query, const char* what) {
                 return comm_abort(c, comm_who(c) + ": RCCL error while waiting for " + what + ": " +
                                          ncclGetErrorString(r != ncclSuccess ? r : ae) + "; communicator aborted");
         }
-        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        // the bound counts only the time the oldest pending RCCL operation has been
+        // runnable (its preceding work done) without completing: a wait on
+        // compute alone is never cut short, however long it takes
+        khp_ctx::CommOp* op = comm_op_pending(c);
+        double ms = 0.0;
+        if (op) {
+            const auto now = std::chrono::steady_clock::now();
+            if (!op->runnable && hipEventQuery(op->pre) == hipSuccess) {
+                op->runnable = true;
+                op->since = now;
+            }
+            if (op->runnable) ms = std::chrono::duration<double, std::milli>(now - op->since).count();
+        }
         if (ms > c->comm_timeout_ms) {
             if (!c->comm)
                 return fail(KHP_EDEVICE, comm_who(c) + ": " + what + " still running " +
@@ -3662,6 +3760,7 @@ static khp_status snapshot_now(khp_ctx* c, uint64_t id) {
     if (!sn->done) HIPCHK(hipEventCreateWithFlags(&sn->done, hipEventDisableTiming));
     if (!c->snap_evt) HIPCHK(hipEventCreateWithFlags(&c->snap_evt, hipEventDisableTiming));
     if (c->fb_evt) HIPCHK(hipStreamWaitEvent(c->stream, c->fb_evt, 0));
+    sn->touched = true;   // from here on the buffers may be in use by the device
     hipLaunchKernelGGL(k_rgba8, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(), n,
                        sn->dbuf.as<uint8_t>());
     HIPCHK(hipGetLastError());
@@ -3671,6 +3770,23 @@ static khp_status snapshot_now(khp_ctx* c, uint64_t id) {
     HIPCHK(hipEventRecord(sn->done, c->stream));
     sn->enqueued = true;
     return KHP_OK;
+}
+
+// A snapshot whose conversion or copy was not (completely) enqueued: its ticket is
+// removed by id, and its buffers are reused only if nothing was queued on them,
+// or once the stream has finished whatever was; if that wait fails
+// the snapshot is leaked rather than handed to a later copy still in flight.
+static void retire_failed_snapshot(khp_ctx* c, Snapshot* sn) {
+    for (size_t i = 0; i < c->snaps.size(); ++i)
+        if (c->snaps[i] == sn) {
+            c->snaps.erase(c->snaps.begin() + (ptrdiff_t)i);
+            break;
+        }
+    sn->out = nullptr;
+    sn->enqueued = false;
+    if (sn->touched && wait_stream(c, c->stream, "a failed 8-bit snapshot") != KHP_OK) return;   // leaked
+    sn->touched = false;
+    c->snap_free.push_back(sn);
 }
 
 // Copy completed snapshots with id <= upto into their callers' buffers, oldest first.
@@ -3685,12 +3801,11 @@ static khp_status deliver_snapshots(khp_ctx* c, uint64_t upto, bool wait) {
                 // its conversion never reached the device (an error inside the flush
                 // above or an earlier one): drop this ticket only, so later snapshots
                 // and syncs still work
-                c->snaps.erase(c->snaps.begin());
-                sn->out = nullptr;
-                c->snap_free.push_back(sn);
-                return s != KHP_OK ? s
-                                   : fail(KHP_EDEVICE, "snapshot " + std::to_string(sn->id) +
-                                                           " was not enqueued (an earlier call failed); dropped");
+                const std::string err = s != KHP_OK ? std::string(khp_last_error())
+                                                    : "snapshot " + std::to_string(sn->id) +
+                                                          " was not enqueued (an earlier call failed); dropped";
+                retire_failed_snapshot(c, sn);
+                return fail(s != KHP_OK ? s : KHP_EDEVICE, err);
             }
             if (s != KHP_OK) return s;
         }
@@ -3705,6 +3820,7 @@ static khp_status deliver_snapshots(khp_ctx* c, uint64_t upto, bool wait) {
         c->snaps.erase(c->snaps.begin());
         sn->out = nullptr;
         sn->enqueued = false;
+        sn->touched = false;
         c->snap_free.push_back(sn);
     }
     return KHP_OK;
@@ -3748,10 +3864,10 @@ extern "C" khp_status khp_read_rgba8_async(khp_ctx* c, uint8_t* out_rgba, uint64
         return KHP_OK;
     }
     const khp_status st = snapshot_now(c, sn->id);
-    if (st != KHP_OK) {  // not enqueued: the ticket is void, the buffer goes back to the free list
-        c->snaps.pop_back();
-        sn->out = nullptr;
-        c->snap_free.push_back(sn);
+    if (st != KHP_OK) {  // not (completely) enqueued: the ticket is void
+        const std::string err = khp_last_error();
+        retire_failed_snapshot(c, sn);
+        return fail(st, err);
     }
     return st;
 }
@@ -4139,6 +4255,24 @@ extern "C" khp_status khp_get_stats(khp_ctx* c, khp_stats* out) {
     return KHP_OK;
 }
 
+#ifdef KHP_PATH_PROFILE
+// Diagnostic builds only (not part of the ABI): copies the k_path per-wave
+// records written since the last call (6 x u64 each, see g_wprof) and resets them.
+extern "C" khp_status khp_debug_wave_profile(khp_ctx* c, unsigned long long* out, uint32_t max_waves, uint32_t* n) {
+    if (!c || !out || !n) return fail(KHP_EINVAL, "null argument");
+    KHPCHK(drain(c));
+    HIPCHK(hipSetDevice(c->device));
+    uint32_t cnt = 0;
+    HIPCHK(hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_wprof_n), sizeof(cnt)));
+    cnt = std::min<uint32_t>(std::min<uint32_t>(cnt, KHP_WPROF_MAX), max_waves);
+    if (cnt) HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wprof), 6 * sizeof(unsigned long long) * cnt));
+    const uint32_t zero = 0;
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_wprof_n), &zero, sizeof(zero)));
+    *n = cnt;
+    return KHP_OK;
+}
+#endif
+
 // ---- RCCL ---------------------------------------------------------------------------------
 // The communicator is non-blocking (ncclConfig_t.blocking = 0, ABI 11): an RCCL call
 // may return ncclInProgress while RCCL finishes it in the background, and the
@@ -4173,12 +4307,19 @@ static khp_status comm_settle(khp_ctx* c, ncclResult_t r, const std::string& wha
 // Frees the communicator: finalize (flushes issued operations; bounded), then
 // destroy; a finalize that does not settle aborts instead.
 static void comm_release(khp_ctx* c) {
-    if (!c->comm) return;
-    if (comm_settle(c, ncclCommFinalize(c->comm), "ncclCommFinalize") == KHP_OK && c->comm)
+    if (c->comm && comm_settle(c, ncclCommFinalize(c->comm), "ncclCommFinalize") == KHP_OK && c->comm)
         (void)ncclCommDestroy(c->comm);
     c->comm = nullptr;
     c->comm_job.reset();
+    // also after an abort (comm already null): the dead communicator's state
+    // must not keep the next group's or the local group's waits polling
     c->comm_dead.clear();
+    for (const khp_ctx::CommOp& op : c->comm_ops)
+        for (hipEvent_t e : {op.pre, op.post})
+            if (e) (void)hipEventDestroy(e);
+    c->comm_ops.clear();
+    for (hipEvent_t e : c->comm_evt_free) (void)hipEventDestroy(e);
+    c->comm_evt_free.clear();
 }
 
 extern "C" khp_status khp_comm_unique_id(uint8_t out_id[128]) {
@@ -4410,12 +4551,16 @@ static khp_status rccl_send(khp_ctx* c, uint32_t P, int root) {
     hipLaunchKernelGGL(k_pack, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->fb.as<float>(),
                        c->stage_pix.as<uint32_t>(), P, c->stage.as<float>());
     HIPCHK(hipGetLastError());
-    return comm_settle(c, ncclSend(c->stage.p, (size_t)P * 3, ncclFloat32, root, c->comm, c->stream),
-                       "ncclSend of " + std::to_string(P) + " pixels to root " + std::to_string(root));
+    HIPCHK(comm_op_begin(c));
+    KHPCHK(comm_settle(c, ncclSend(c->stage.p, (size_t)P * 3, ncclFloat32, root, c->comm, c->stream),
+                       "ncclSend of " + std::to_string(P) + " pixels to root " + std::to_string(root)));
+    HIPCHK(comm_op_end(c));
+    return KHP_OK;
 }
 
 static khp_status rccl_receive(khp_ctx* c, int root, size_t* total) {
     *total = 0;
+    HIPCHK(comm_op_begin(c));
     ncclResult_t r = ncclGroupStart();
     if (r != ncclSuccess) return comm_settle(c, r, "ncclGroupStart");
     std::string failed;
@@ -4431,7 +4576,9 @@ static khp_status rccl_receive(khp_ctx* c, int root, size_t* total) {
         (void)comm_settle(c, e, "ncclGroupEnd");
         return comm_abort(c, comm_who(c) + ": " + failed + "; communicator aborted");
     }
-    return comm_settle(c, e, "the gather's ncclGroupEnd (receives from every sender)");
+    KHPCHK(comm_settle(c, e, "the gather's ncclGroupEnd (receives from every sender)"));
+    HIPCHK(comm_op_end(c));
+    return KHP_OK;
 }
 
 static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root) {

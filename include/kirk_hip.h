@@ -464,9 +464,11 @@ khp_status khp_comm_unique_id(uint8_t out_id[128]);
  * the communicator is non-blocking (ncclConfig_t.blocking = 0) and no call of
  * this context waits without a bound while it exists: RCCL calls are polled to
  * completion, and every device wait (khp_sync, synchronous renders, reads,
- * khp_destroy) polls ncclCommGetAsyncError.  An RCCL error, or no progress
- * within the context's timeout (khp_comm_set_timeout, default 120 s: e.g. a
- * peer that never joins or a gather without its counterpart), aborts the
+ * khp_destroy) polls ncclCommGetAsyncError.  An RCCL error, or an RCCL
+ * operation that stays runnable (the work queued before it done) without
+ * completing for the context's timeout (khp_comm_set_timeout, default 120 s:
+ * e.g. a peer that never joins or a gather without its counterpart; a wait on
+ * compute alone is never cut short, ABI 11 as amended in round 5), aborts the
  * communicator (ncclCommAbort) and returns KHP_EDEVICE with a message naming
  * this rank and its peers; gathers then return KHP_ENOTREADY until the next
  * khp_comm_init.  KIRK has no multi-device path; its only failure mode is the
@@ -485,8 +487,11 @@ khp_status khp_gather_framebuffer(khp_ctx* ctx, const khp_render_params* p, int 
  * sender's k-th gather packs into ring slot k % 64, stamped with k; the root's
  * k-th gather copies every sender's slot k, so each sender must have ENQUEUED
  * its k-th gather (khp_sync flushes fused frames) before the root's k-th gather
- * is enqueued (else the root's call returns KHP_ENOTREADY and can be repeated),
- * and a sender 64 gathers ahead of the root gets KHP_ENOTREADY instead of
+ * is enqueued (else the root's call returns KHP_ENOTREADY; a gather issued
+ * with no asynchronous renders pending can then be repeated, but one queued
+ * behind pending asynchronous renders runs when that fused batch is enqueued,
+ * and its KHP_ENOTREADY then ends the batch where it stands: khp_sync the
+ * senders before such a root gather), and a sender 64 gathers ahead of the root gets KHP_ENOTREADY instead of
  * overwriting a slot the root has not taken (ABI 11: stamps; before, both cases
  * copied stale pixels silently).  A member's pack into a slot waits for the
  * root's copy of its previous content.  Re-initialising a member removes it

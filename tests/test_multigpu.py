@@ -181,6 +181,84 @@ def test_rccl_single_rank_gather_on_one_gpu():
         ctx.close()
 
 
+def test_rccl_compute_waits_are_not_bounded():
+    """the communicator's bound applies to RCCL operations that are
+    runnable but not completing, never to compute.  With a one-rank communicator
+    and a 1 ms bound, synchronous renders, fused passes with gathers between them
+    and reads that each take far longer than 1 ms must all succeed (they used to
+    abort the communicator and return KHP_EDEVICE), and the frame is the oracle's."""
+    from ba_pathtracing_fur_amd.pathtracer import HipContext, comm_unique_id
+    W, H, SPP = 96, 64, 4
+    sd = S.config2(W, H, n_strands=2000)
+    want = oracle_ffi.Oracle(sd).render(W, H, 3 * SPP, 5, threads=16)
+    ctx = HipContext(0)
+    try:
+        ctx.set_scene(sd)
+        ctx.build_accel()
+        ctx.comm_init(1, 0, comm_unique_id(), timeout_ms=30000)
+        ctx.comm_set_timeout(1)
+        ctx.render(W, H, SPP, 5, first_sample=0, tile_size=16, tile_rank=0, tile_nranks=1, readback=False)
+        ctx.gather_framebuffer(W, H, SPP, 5, 16, 1, 0, 0)
+        for k in (1, 2):
+            ctx.render(W, H, SPP, 5, first_sample=k * SPP, tile_size=16, tile_rank=0, tile_nranks=1,
+                       readback=False, async_=True)
+            ctx.gather_framebuffer(W, H, SPP, 5, 16, 1, 0, 0)
+        ctx.sync()
+        assert_parity(ctx.read_framebuffer(W, H), want, exact=True)
+    finally:
+        ctx.close()
+
+
+_ABORT_THEN_LOCAL = r"""
+import os, sys
+sys.path.insert(0, %(root)r)
+import numpy as np
+import torch.distributed as dist
+from ba_pathtracing_fur_amd import native as N, scenes as S
+from ba_pathtracing_fur_amd.pathtracer import HipContext, comm_init_local, comm_unique_id
+rank = int(os.environ["RANK"])
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d", rank=rank, world_size=2)
+ctx = HipContext(rank)
+sd = S.config2(64, 48, n_strands=1500)
+ctx.set_scene(sd); ctx.build_accel()
+uid = [comm_unique_id() if rank == 0 else None]
+dist.broadcast_object_list(uid, src=0)
+ctx.comm_init(2, rank, uid[0], timeout_ms=60000)
+dist.barrier()
+if rank == 1:                       # rank 1 never sends: the root's gather must abort
+    dist.barrier()
+    ctx.close(); print("ABORT_LOCAL_OK"); sys.exit(0)
+ctx.comm_set_timeout(2000)
+ctx.render(64, 48, 1, 5, tile_size=16, tile_rank=0, tile_nranks=2, readback=False)
+try:
+    ctx.gather_framebuffer(64, 48, 1, 5, 16, 2, 0, 0)
+    ctx.sync()
+    print("UNEXPECTED: gather completed"); sys.exit(1)
+except N.KhpError as e:
+    assert e.status == N.KHP_EDEVICE, e
+dist.barrier()
+comm_init_local([ctx])              # a one-member local group: no communicator any more
+img = ctx.render(512, 384, 16, 5)   # far longer than the old 2 s bound on an aborted comm
+assert img.shape == (384, 512, 3)
+ctx.close(); print("ABORT_LOCAL_OK")
+"""
+
+
+def test_rccl_abort_then_local_group_waits_unbounded(tmp_path):
+    """after a communicator abort, khp_comm_init_local must clear the
+    dead communicator's state, so the context's later waits block normally
+    instead of failing after the old bound with "still running after the abort"."""
+    if _n_gpus() < 2:
+        pytest.skip(f"needs 2 GPUs, this box has {_n_gpus()}")
+    src = tmp_path / "abort_local.py"
+    src.write_text(_ABORT_THEN_LOCAL % {"root": ROOT, "port": _port()})
+    procs = [subprocess.Popen([sys.executable, str(src)], env={**os.environ, "RANK": str(r)},
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0 and "ABORT_LOCAL_OK" in o, (o[-2000:], e[-3000:])
+
+
 _NO_PEER = r"""
 import sys, time
 sys.path.insert(0, %(root)r)
