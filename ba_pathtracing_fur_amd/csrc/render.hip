@@ -2254,6 +2254,14 @@ struct khp_ctx {
     };
     std::deque<CommOp> comm_ops;
     std::vector<hipEvent_t> comm_evt_free;
+    // khp_read_rgba8's buffers, kept between calls (no allocation per texture):
+    // device 8-bit texture, Yxy, block maxima, log terms; pinned host copies of
+    // the log terms and maxima; one event per log-term chunk
+    DevMem tm_out, tm_yxy, tm_bmax, tm_lgv;
+    double* tm_hl = nullptr;
+    float* tm_hm = nullptr;
+    size_t tm_hl_n = 0, tm_hm_n = 0;
+    hipEvent_t tm_ev[16] = {};
     // ABI 8 in-process group (khp_comm_init_local): the gather's transport between
     // contexts of one process instead of RCCL; a sender's k-th gather packs into
     // ring slot k % LG_SLOTS, the root's k-th gather copies every sender's slot k.
@@ -2545,6 +2553,10 @@ extern "C" void khp_destroy(khp_ctx* c) {
     }
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     for (auto e : c->sync_pool) (void)hipEventDestroy(e);
+    if (c->tm_hl) (void)hipHostFree(c->tm_hl);
+    if (c->tm_hm) (void)hipHostFree(c->tm_hm);
+    for (hipEvent_t e : c->tm_ev)
+        if (e) (void)hipEventDestroy(e);
     for (auto* v : {&c->snaps, &c->snap_free})
         for (Snapshot* sn : *v) {
             if (sn->pinned) (void)hipHostFree(sn->pinned);
@@ -3881,7 +3893,16 @@ extern "C" khp_status khp_snapshot_wait(khp_ctx* c, uint64_t ticket, int wait) {
     return KHP_OK;
 }
 
+#ifdef KHP_TM_TRACE   // diagnostic builds only: phase times of khp_read_rgba8 to stderr
+#define TM_MARK(k) tm_t[k] = std::chrono::steady_clock::now()
+#else
+#define TM_MARK(k) do { } while (0)
+#endif
 extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t* out_rgba) {
+#ifdef KHP_TM_TRACE
+    std::chrono::steady_clock::time_point tm_t[8];
+    TM_MARK(0);
+#endif
     if (c) {  // complete asynchronous frames first
         khp_status dr = drain(c);
         if (dr != KHP_OK) return dr;
@@ -3891,7 +3912,8 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
     HIPCHK(hipSetDevice(c->device));
     const uint32_t n = c->fbW * c->fbH;
     const uint32_t nb = (n + 255) / 256;
-    DevMem out, yxy, bmax, lgv;
+    DevMem& out = c->tm_out;
+    DevMem &yxy = c->tm_yxy, &bmax = c->tm_bmax, &lgv = c->tm_lgv;
     HIPCHK(out.ensure(4 * (size_t)n));
     if (!tm) {
         hipLaunchKernelGGL(k_rgba8, dim3(nb), dim3(256), 0, c->stream, c->fb.as<float>(), n, out.as<uint8_t>());
@@ -3899,17 +3921,62 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
         HIPCHK(yxy.ensure(12 * (size_t)n));
         HIPCHK(bmax.ensure(4 * (size_t)nb));
         HIPCHK(lgv.ensure(8 * (size_t)n));
+        if (c->tm_hl_n < n) {
+            if (c->tm_hl) (void)hipHostFree(c->tm_hl);
+            c->tm_hl = nullptr;
+            c->tm_hl_n = 0;
+            HIPCHK(hipHostMalloc((void**)&c->tm_hl, 8 * (size_t)n, hipHostMallocDefault));
+            c->tm_hl_n = n;
+        }
+        if (c->tm_hm_n < nb) {
+            if (c->tm_hm) (void)hipHostFree(c->tm_hm);
+            c->tm_hm = nullptr;
+            c->tm_hm_n = 0;
+            HIPCHK(hipHostMalloc((void**)&c->tm_hm, 4 * (size_t)nb, hipHostMallocDefault));
+            c->tm_hm_n = nb;
+        }
+        for (hipEvent_t& e : c->tm_ev)
+            if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        TM_MARK(1);
         hipLaunchKernelGGL(k_tm_yxy, dim3(nb), dim3(256), 0, c->stream, c->fb.as<float>(), n, yxy.as<float>(),
                            bmax.as<float>(), lgv.as<double>());
-        std::vector<float> hm(nb);
-        std::vector<double> hl(n);
-        HIPCHK(hipMemcpyAsync(hm.data(), bmax.p, 4 * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(hl.data(), lgv.p, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
-        KHPCHK(wait_stream(c, c->stream, "the 8-bit texture"));
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(c->tm_hm, bmax.p, 4 * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
+        // the log terms come back in chunks, each summed on the host as soon as it has
+        // landed, while the next ones are still in flight
+        constexpr uint32_t NCH = 16;
+        const uint32_t per = (n + NCH - 1) / NCH;
+        for (uint32_t ch = 0; ch < NCH; ++ch) {
+            const uint32_t a = std::min(n, ch * per), b = std::min(n, a + per);
+            if (b > a)
+                HIPCHK(hipMemcpyAsync(c->tm_hl + a, lgv.as<double>() + a, 8 * (size_t)(b - a), hipMemcpyDeviceToHost,
+                                      c->stream));
+            HIPCHK(hipEventRecord(c->tm_ev[ch], c->stream));
+        }
+        TM_MARK(2);
+        float sum = 0.0f;  // RGB_to_Yxy's float running sum, in pixel order (log_sum_feed: bit for bit)
+        for (uint32_t ch = 0; ch < NCH; ++ch) {
+            // polled, not hipEventSynchronize: a blocking wait per chunk cost ~0.15 ms of
+            // wake-up each (2.4 ms per texture, profiles/r05e_tonemap_trace.txt)
+            if (bounded_waits(c)) {
+                KHPCHK(wait_event(c, c->tm_ev[ch], "the 8-bit texture's log luminances"));
+            } else {
+                for (;;) {
+                    const hipError_t q = hipEventQuery(c->tm_ev[ch]);
+                    if (q == hipSuccess) break;
+                    if (q != hipErrorNotReady) HIPCHK(q);
+                }
+            }
+            const uint32_t a = std::min(n, ch * per), b = std::min(n, a + per);
+            sum = log_sum_feed(sum, c->tm_hl + a, b - a);
+#ifdef KHP_TM_TRACE
+            if (ch == 0) TM_MARK(3);
+#endif
+        }
+        TM_MARK(4);
+        const float* hm = c->tm_hm;
         float mx = 1e-06f;
         for (uint32_t b = 0; b < nb; ++b) mx = (mx < hm[b]) ? hm[b] : mx;
-        float sum = 0.0f;  // RGB_to_Yxy's float running sum, in pixel order
-        for (uint32_t k = 0; k < n; ++k) sum = (float)((double)sum + hl[k]);
         // Tonemapper::map / tonemapping scalars, in KIRK's float/double mix
         float world_lum = sum / (float)n;
         if (tm->center_weight) {
@@ -3977,10 +4044,19 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
         t.white = tm->white;
         t.black = tm->black;
         hipLaunchKernelGGL(k_tm_map, dim3(nb), dim3(256), 0, c->stream, yxy.as<float>(), n, t, out.as<uint8_t>());
+        TM_MARK(5);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out_rgba, out.p, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
     KHPCHK(wait_stream(c, c->stream, "the 8-bit texture"));
+#ifdef KHP_TM_TRACE
+    TM_MARK(6);
+    if (tm) {
+        auto d = [&](int a, int b) { return std::chrono::duration<double, std::milli>(tm_t[b] - tm_t[a]).count(); };
+        fprintf(stderr, "[khp tm] setup %.3f enqueue %.3f first-chunk %.3f sum %.3f map-enqueue %.3f out %.3f total %.3f ms\n",
+                d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5), d(5, 6), d(0, 6));
+    }
+#endif
     return KHP_OK;
 }
 

@@ -124,6 +124,9 @@ std::string gather_plan(uint32_t W, uint32_t H, uint32_t T, int nranks, int rank
 
 // Per-thread message behind khp_last_error(); every failing entry point sets it.
 khp_status fail(khp_status s, const std::string& msg);
+// tonemap_host.cpp: KIRK's sequential float running sum s <- (float)((double)s + l[k])
+// over n terms, continued from s (RGB_to_Yxy's log-luminance sum), bit for bit.
+float log_sum_feed(float s, const double* l, size_t n);
 const char* last_error();
 
 }  // namespace khp

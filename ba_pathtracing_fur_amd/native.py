@@ -167,7 +167,8 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_device_free", "khp_device_copy", "khp_fibers_to_triangles", "khp_gen_hairball_tris_device",
             "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params", "khp_debug_shadow_queue",
             "khp_bdpt_params_defaults", "khp_set_bdpt", "khp_get_bdpt", "khp_gather_plan",
-            "khp_read_rgba8_async", "khp_snapshot_wait", "khp_comm_init_local", "khp_comm_set_timeout"]
+            "khp_read_rgba8_async", "khp_snapshot_wait", "khp_comm_init_local", "khp_comm_set_timeout",
+            "khp_tonemap_log_sum"]
 
 # the include/kirk_hip.h this module mirrors (load_library refuses another)
 ABI_VERSION = 11
@@ -236,6 +237,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_comm_unique_id": (c_int, [P(c_uint8)]),
         "khp_comm_init": (c_int, [c_void_p, c_int, c_int, P(c_uint8)]),
         "khp_comm_set_timeout": (c_int, [c_void_p, c_uint32]),
+        "khp_tonemap_log_sum": (c_int, [P(ctypes.c_double), ctypes.c_uint64, c_float, P(c_float)]),
         "khp_gather_framebuffer": (c_int, [c_void_p, P(RenderParams), c_int]),
         "khp_comm_init_local": (c_int, [P(c_void_p), c_int]),
         "khp_gather_plan": (c_int, [c_uint32, c_uint32, c_uint32, c_int, c_int, c_int, P(c_uint64), P(c_uint32),
@@ -278,6 +280,16 @@ class KhpError(RuntimeError):
 def check(lib, status: int, where: str):
     if status != KHP_OK:
         raise KhpError(status, where, (lib.khp_last_error() or b"").decode())
+
+
+def tonemap_log_sum(terms: np.ndarray, start: float = 0.0) -> np.float32:
+    """khp_tonemap_log_sum (host only): KIRK's float running sum of double terms, in order."""
+    lib = load_library()
+    t = np.ascontiguousarray(terms, dtype=np.float64)
+    out = c_float(0.0)
+    check(lib, lib.khp_tonemap_log_sum(t.ctypes.data_as(POINTER(ctypes.c_double)), t.size, float(start),
+                                       ctypes.byref(out)), "khp_tonemap_log_sum")
+    return np.float32(out.value)
 
 
 def host_build(scene) -> dict:

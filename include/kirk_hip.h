@@ -535,6 +535,14 @@ khp_status khp_host_build(const khp_scene* scene, uint32_t* n_nodes, uint32_t* d
                           int32_t* node_first, int32_t* node_count, int32_t* object_ids, float* obj_bounds,
                           float* records);
 
+/* Round 5: the host half of the tonemapped texture (khp_read_rgba8 with a
+ * khp_tonemap): KIRK's `float sum; sum += log(...)` over the per-pixel log
+ * luminances (Tonemapping.cpp:66-91, the terms in double, every step rounded
+ * to float), continued from `start`, bit for bit but at one double add per
+ * pixel (tonemap_host.cpp).  Exposed for tests and hosts that tonemap their own
+ * framebuffer reads. */
+khp_status khp_tonemap_log_sum(const double* terms, uint64_t n, float start, float* out);
+
 /* Debug introspection: when the last synchronous khp_render ran with
  * khp_ctx_params.dump_bounce = b, the extension rays of bounce b (queue order) are
  * kept on the host.  Call with null arrays to get *n, then with [n][3] arrays. */

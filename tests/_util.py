@@ -22,7 +22,7 @@ def compare_images(a: np.ndarray, b: np.ndarray):
     fb = np.isfinite(b).all(-1)
     mask_equal = np.array_equal(fa, fb)
     both = fa & fb
-    d = np.linalg.norm((a - b)[both], axis=-1) if both.any() else np.zeros(1, np.float32)
+    d = np.linalg.norm(a[both] - b[both], axis=-1) if both.any() else np.zeros(1, np.float32)   # mask first
     return {"bitexact": bitexact, "mask_equal": mask_equal, "max_l2": float(d.max(initial=0.0)),
             "mean_l2": float(d.mean()) if d.size else 0.0, "n_div": int((d > PIXEL_L2_TOL).sum()),
             "n_nonfinite": int((~fa).sum())}

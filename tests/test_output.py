@@ -9,11 +9,10 @@ Utils/Tonemapping.cpp:9-245 (map and its stages).
 Tolerances, written here because they are the contract:
   * no tonemapping: bytes identical (the conversion is one IEEE multiply and two
     compares on both sides);
-  * tonemapping: the reference accumulates the log-luminance sum in float in
-    pixel order, the device reduces it in double in parallel, and the device's
-    expf/logf/powf are ocml's, not glibc's.  Mapped values agree to ~1e-5
-    relative, so a byte may flip by 1 where a value sits on a truncation edge:
-    bytes differ by at most 1 on at most 1% of channels.
+  * tonemapping: bytes identical too -- the log-luminance sum is KIRK's
+    sequential float running sum on both sides (the library's host half,
+    khp_tonemap_log_sum, checked against the plain loop below), and the
+    transcendental calls are kmath.h's on both sides.
 The tonemapper has no golden vectors in the reference (no tests, it cannot be
 built here); the oracle is pinned by an independent float64 numpy restatement
 and analytic known answers below (parity unpinned by the reference itself).
@@ -142,6 +141,42 @@ def test_oracle_center_weight():
     # a window that would read past the image (the reference's indexing) is refused
     with pytest.raises(ValueError):
         O.tonemap(img, N.Tonemap.defaults(center_weight=1, center_x=81, center_y=49, kernel_multiplier=0.5))
+
+
+def _kirk_log_sum(terms, start=0.0):
+    s = np.float32(start)
+    with np.errstate(invalid="ignore"):   # inf + -inf = NaN, as in KIRK's loop
+        for v in terms:   # RGB_to_Yxy: float sum += (double) log(...)
+            s = np.float32(np.float64(s) + v)
+    return s
+
+
+@pytest.mark.parametrize("case", ["uniform", "dark", "zeros", "bright", "mixed_sign", "tiny", "start", "nonfinite"])
+def test_log_sum_is_kirks_sequential_float_sum(case):
+    """khp_tonemap_log_sum (the library's host half of the tonemapped texture:
+    one double add per term, every step re-checked against KIRK's expression)
+    equals the plain float running sum bit for bit -- including sums that cross
+    binades in both directions, start at 0 or elsewhere, or meet inf / NaN terms."""
+    rng = np.random.default_rng(sum(map(ord, case)))
+    n = 30000
+    Y = {"uniform": rng.random(n), "dark": rng.random(n) ** 4 * 0.01, "zeros": np.where(rng.random(n) < 0.5, 0.0,
+         rng.random(n)), "bright": np.exp(6 * rng.random(n)), "mixed_sign": np.exp(12 * (rng.random(n) - 0.5)),
+         "tiny": rng.random(n) * 1e-7, "start": rng.random(n), "nonfinite": rng.random(n)}[case]
+    terms = np.log(2.3e-5 + Y.astype(np.float32).astype(np.float64))
+    start = 0.0
+    if case == "start":
+        start = -12345.678
+    if case == "nonfinite":
+        terms[1000] = np.inf
+        terms[20000] = -np.inf
+    want = _kirk_log_sum(terms, start)
+    got = N.tonemap_log_sum(terms, start)
+    assert np.float32(got).view(np.uint32) == want.view(np.uint32), (got, want)
+    # chunked, as khp_read_rgba8 feeds it
+    s = np.float32(start)
+    for a in range(0, n, 7001):
+        s = N.tonemap_log_sum(terms[a:a + 7001], float(s))
+    assert np.float32(s).view(np.uint32) == want.view(np.uint32)
 
 
 def test_tonemap_struct_defaults_match_library():
