@@ -37,7 +37,16 @@ float log_sum_feed(float s, const double* l, size_t n) {
     size_t k = 0;
     while (k < n) {
         const size_t m = n - k < B ? n - k : B;
-        if (s == 0.0f || !std::isfinite(s)) {  // no binade (or inf / NaN): KIRK's step as written
+        if (s != s) return s;  // NaN absorbs every later term (x86 keeps the first operand's NaN)
+        if (std::isinf(s)) {
+            // +-inf stays itself until a NaN or the opposite infinity turns it into NaN
+            // (an inf pixel blacks out KIRK's whole texture; its frame must not cost a
+            // step per remaining pixel)
+            for (; k < n; ++k)
+                if (l[k] != l[k] || l[k] == (double)-s) return kirk_step(s, l[k]);
+            return s;
+        }
+        if (s == 0.0f) {  // no binade yet: KIRK's step as written
             s = kirk_step(s, l[k]);
             ++k;
             continue;

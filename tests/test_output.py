@@ -151,7 +151,8 @@ def _kirk_log_sum(terms, start=0.0):
     return s
 
 
-@pytest.mark.parametrize("case", ["uniform", "dark", "zeros", "bright", "mixed_sign", "tiny", "start", "nonfinite"])
+@pytest.mark.parametrize("case", ["uniform", "dark", "zeros", "bright", "mixed_sign", "tiny", "start", "nonfinite",
+                                  "inf_only", "nan_term"])
 def test_log_sum_is_kirks_sequential_float_sum(case):
     """khp_tonemap_log_sum (the library's host half of the tonemapped texture:
     one double add per term, every step re-checked against KIRK's expression)
@@ -161,14 +162,19 @@ def test_log_sum_is_kirks_sequential_float_sum(case):
     n = 30000
     Y = {"uniform": rng.random(n), "dark": rng.random(n) ** 4 * 0.01, "zeros": np.where(rng.random(n) < 0.5, 0.0,
          rng.random(n)), "bright": np.exp(6 * rng.random(n)), "mixed_sign": np.exp(12 * (rng.random(n) - 0.5)),
-         "tiny": rng.random(n) * 1e-7, "start": rng.random(n), "nonfinite": rng.random(n)}[case]
+         "tiny": rng.random(n) * 1e-7, "start": rng.random(n), "nonfinite": rng.random(n), "inf_only": rng.random(n),
+         "nan_term": rng.random(n)}[case]
     terms = np.log(2.3e-5 + Y.astype(np.float32).astype(np.float64))
     start = 0.0
     if case == "start":
         start = -12345.678
-    if case == "nonfinite":
+    if case == "nonfinite":   # inf, then the opposite infinity: NaN from there on
         terms[1000] = np.inf
         terms[20000] = -np.inf
+    if case == "inf_only":    # an inf pixel (KIRK's texture goes black): the sum stays inf
+        terms[777] = np.inf
+    if case == "nan_term":
+        terms[5000] = np.nan
     want = _kirk_log_sum(terms, start)
     got = N.tonemap_log_sum(terms, start)
     assert np.float32(got).view(np.uint32) == want.view(np.uint32), (got, want)

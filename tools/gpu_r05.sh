@@ -29,4 +29,25 @@ tmtrace)
   timeout -k 10 400 python -u -m pytest tests/test_output.py -x -v --timeout 200 --timeout-method thread -m gpu > gpurun_out/$T/tests_out.log 2>&1 || exit 1
   env KHP_LIB=variants/libkirk_tmtrace.so timeout -k 10 200 python -u tools/sync_calls.py 2 > gpurun_out/$T/tmtrace.jsonl 2> gpurun_out/$T/tmtrace.log || exit 1
   ;;
+ab)   # in-tree library (A) against variants/libkirk_<base>.so (B), alternated; $3 = B's name; $4 = bench args
+  B=${3:-base}
+  for r in 1 2; do
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline $4 > gpurun_out/$T/ab_A$r.json 2> gpurun_out/$T/ab_A$r.log || exit 1
+    env KHP_LIB=variants/libkirk_$B.so timeout -k 10 300 python -u bench.py --no-cpu-baseline $4 > gpurun_out/$T/ab_B$r.json 2> gpurun_out/$T/ab_B$r.log || exit 1
+  done
+  python - $T <<'PY'
+import json, sys
+t = sys.argv[1]
+for k in ("A1", "B1", "A2", "B2"):
+    d = json.loads(open(f"gpurun_out/{t}/ab_{k}.json").read().strip().splitlines()[-1])
+    f = d["frame"]
+    print(k, d["value"], "sync", (d.get("sync_steps") or {}).get("value"), "gui", (d.get("gui_steps") or {}).get("value"),
+          "ext", f["extend_ms"], "b0/b1", [b["extend_ms"] for b in f["per_bounce"]], "dev", f["device_ms"],
+          "iso_ext", (d.get("isolated") or {}).get("k_extend", {}).get("ms_per_frame"),
+          "iso_sh", (d.get("isolated") or {}).get("k_shadow", {}).get("ms_per_frame"), "tm", (d.get("output_stage") or {}).get("tonemap_rgba8_ms"))
+PY
+  ;;
+parity)
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -m gpu > gpurun_out/$T/tests_parity.log 2>&1 || exit 1
+  ;;
 esac
