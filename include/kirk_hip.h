@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 11
+#define KHP_ABI_VERSION 12
 
 typedef struct khp_ctx khp_ctx;
 
@@ -311,7 +311,14 @@ typedef struct {
                                     wavefront's steady rate wins).  Not with the light-path variant, hit
                                     sorting, instrumented renders or queue dumps (those always run the
                                     wavefront).  Measured in DESIGN.md §5b                              */
-} khp_ctx_params;
+    uint32_t ray_sort_from;      /* ABI 12: the first bounce whose extension rays are regrouped before
+                                    k_extend by the Morton cell (32^3 over the scene box) of their origin, so
+                                    that the rays of a claim block start close together and share cache
+                                    lines; the path state stays in place.  Which lane traces which ray
+                                    changes no result.  Default 2 (measured); 0 or >= depth:
+                                    never.  Not with hit sorting (shade_order 1), the light-path variant or
+                                    queue dumps; the path kernel never sorts                              */
+} khp_ctx_params;   /* 56 bytes (52 + tail padding) */
 
 /* ---- context --------------------------------------------------------------- */
 /* device: HIP device ordinal (one process per GPU). */
@@ -535,7 +542,7 @@ khp_status khp_host_build(const khp_scene* scene, uint32_t* n_nodes, uint32_t* d
                           int32_t* node_first, int32_t* node_count, int32_t* object_ids, float* obj_bounds,
                           float* records);
 
-/* Round 5: the host half of the tonemapped texture (khp_read_rgba8 with a
+/* ABI 12 (round 5): the host half of the tonemapped texture (khp_read_rgba8 with a
  * khp_tonemap): KIRK's `float sum; sum += log(...)` over the per-pixel log
  * luminances (Tonemapping.cpp:66-91, the terms in double, every step rounded
  * to float), continued from `start`, bit for bit but at one double add per

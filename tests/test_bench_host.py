@@ -52,10 +52,11 @@ def test_explicit_sizes_override_config(bench, monkeypatch):
 def test_scheduling_knobs_parse(bench, monkeypatch):
     """Knobs map onto khp_ctx_params fields (they change scheduling, never frames)."""
     a = _parse(bench, monkeypatch, "--fuse", "16", "--frames-in-flight", "2", "--chunk-paths", "4096",
-               "--shade-order", "1", "--heavy-iters", "80")
-    assert (a.fuse, a.frames_in_flight, a.chunk_paths, a.shade_order, a.heavy_iters) == (16, 2, 4096, 1, 80)
+               "--shade-order", "1", "--heavy-iters", "80", "--ray-sort-from", "3")
+    assert (a.fuse, a.frames_in_flight, a.chunk_paths, a.shade_order, a.heavy_iters, a.ray_sort_from) == \
+        (16, 2, 4096, 1, 80, 3)
     b = _parse(bench, monkeypatch)
-    assert (b.fuse, b.frames_in_flight, b.chunk_paths, b.shade_order, b.heavy_iters) == (None,) * 5
+    assert (b.fuse, b.frames_in_flight, b.chunk_paths, b.shade_order, b.heavy_iters, b.ray_sort_from) == (None,) * 6
 
 
 def test_available_cores(bench):

@@ -797,6 +797,36 @@ def test_wide_records_frames(hip_ctx, name, kw, w, h, spp, depth):
     assert len(counts) == 1
 
 
+@pytest.mark.parametrize("name,kw,w,h,spp,depth", [CASES[1], CASES[4], CASES[5], CASES[8]],
+                         ids=["config2", "config5", "zoo", "textured"])
+def test_ray_sorting_frames(hip_ctx, name, kw, w, h, spp, depth):
+    """khp_ctx_params.ray_sort_from (ABI 12): the wavefront's extension rays
+    regrouped by origin cell from bounce 1, 2 (default), 3 or never give the
+    oracle's frame bit for bit -- synchronous, instrumented and fused
+    asynchronous -- and KIRK's visit counts do not change.  The path kernel never
+    sorts, so the synchronous calls here run the wavefront (path_kernel 1)."""
+    sd = S.build_config(name, width=w, height=h, **kw)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    want = oracle_ffi.Oracle(sd).render(w, h, spp, depth, threads=16)
+    counts = set()
+    old = hip_ctx.params()
+    try:
+        for rs in (0, 1, 2, 3):
+            hip_ctx.set_params(ray_sort_from=rs, path_kernel=1)
+            assert_parity(hip_ctx.render(w, h, spp, depth), want, exact=True)
+            assert_parity(hip_ctx.render(w, h, spp, depth, stats=True), want, exact=True)
+            st = hip_ctx.stats()
+            counts.add((st["node_visits"], st["prim_tests"]))
+            for k in range(spp):   # fused 1-spp passes
+                hip_ctx.render(w, h, 1, depth, first_sample=k, async_=True)
+            hip_ctx.sync()
+            assert_parity(hip_ctx.read_framebuffer(w, h), want, exact=True)
+    finally:
+        hip_ctx.set_params(**old)
+    assert len(counts) == 1
+
+
 PK_CASES = [CASES[0], CASES[1], CASES[2], CASES[3], CASES[4], CASES[5], CASES[8]]
 
 

@@ -47,7 +47,32 @@ for k in ("A1", "B1", "A2", "B2"):
           "iso_sh", (d.get("isolated") or {}).get("k_shadow", {}).get("ms_per_frame"), "tm", (d.get("output_stage") or {}).get("tonemap_rgba8_ms"))
 PY
   ;;
+vars)   # the in-tree library and variants/libkirk_<v>.so for v in $3 (space-separated), alternated twice; $4 = bench args
+  for r in 1 2; do
+    for v in base $3; do
+      if [ $v = base ]; then L=""; else L="KHP_LIB=variants/libkirk_$v.so"; fi
+      env $L timeout -k 10 300 python -u bench.py --no-cpu-baseline $4 > gpurun_out/$T/v_${v}_$r.json 2> gpurun_out/$T/v_${v}_$r.log || exit 1
+    done
+  done
+  python - $T base $3 <<'PY'
+import json, sys
+t = sys.argv[1]
+for v in sys.argv[2:]:
+    for r in (1, 2):
+        d = json.loads(open(f"gpurun_out/{t}/v_{v}_{r}.json").read().strip().splitlines()[-1])
+        f = d["frame"]
+        print(v, r, d["value"], "sync", (d.get("sync_steps") or {}).get("value"), "ext", f["extend_ms"],
+              "per_bounce", [b["extend_ms"] for b in f["per_bounce"]], "shade", f["shade_ms"], "dev", f["device_ms"])
+PY
+  ;;
 parity)
-  timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -m gpu > gpurun_out/$T/tests_parity.log 2>&1 || exit 1
+  # a variant library (KHP_LIB) is not named libkirk_hip.so: skip the mapping check then
+  D=""; [ -n "$KHP_LIB" ] && D="--deselect tests/test_gpu_parity.py::test_native_library_is_loaded"
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -m gpu $D > gpurun_out/$T/tests_parity.log 2>&1 || exit 1
+  ;;
+full)   # every GPU test, then the driver's bench command and the default one
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || exit 1
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver.json 2> gpurun_out/$T/bench_driver.log || exit 1
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/$T/bench_default.json 2> gpurun_out/$T/bench_default.log || exit 1
   ;;
 esac
