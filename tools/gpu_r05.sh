@@ -70,6 +70,16 @@ parity)
   D=""; [ -n "$KHP_LIB" ] && D="--deselect tests/test_gpu_parity.py::test_native_library_is_loaded"
   timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -m gpu $D > gpurun_out/$T/tests_parity.log 2>&1 || exit 1
   ;;
+r05r)   # fused shadow stage parity + A/B, octant keys, rank probe
+  env KHP_LIB=variants/libkirk_fsh.so bash tools/gpu_r05.sh parity $T || exit 1
+  mv gpurun_out/$T/tests_parity.log gpurun_out/$T/tests_parity_fsh.log
+  env KHP_LIB=variants/libkirk_fsh5.so bash tools/gpu_r05.sh parity $T || exit 1
+  mv gpurun_out/$T/tests_parity.log gpurun_out/$T/tests_parity_fsh5.log
+  bash tools/gpu_r05.sh vars $T "fsh fsh5 oct" > gpurun_out/$T/vars.txt || exit 1
+  env KHP_LIB=variants/libkirk_oct.so timeout -k 10 300 python -u bench.py --no-cpu-baseline --ray-sort-from 1 > gpurun_out/$T/oct_rs1.json 2> gpurun_out/$T/oct_rs1.log || exit 1
+  timeout -k 10 300 python -u tools/rank_probe.py > gpurun_out/$T/rank_probe.json 2> gpurun_out/$T/rank_probe.log || exit 1
+  env KHP_LIB=variants/libkirk_fsh.so timeout -k 10 300 python -u tools/rank_probe.py > gpurun_out/$T/rank_probe_fsh.json 2> gpurun_out/$T/rank_probe_fsh.log || exit 1
+  ;;
 full)   # every GPU test, then the driver's bench command and the default one
   timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver.json 2> gpurun_out/$T/bench_driver.log || exit 1
