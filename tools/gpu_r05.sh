@@ -80,6 +80,20 @@ r05r)   # fused shadow stage parity + A/B, octant keys, rank probe
   timeout -k 10 300 python -u tools/rank_probe.py > gpurun_out/$T/rank_probe.json 2> gpurun_out/$T/rank_probe.log || exit 1
   env KHP_LIB=variants/libkirk_fsh.so timeout -k 10 300 python -u tools/rank_probe.py > gpurun_out/$T/rank_probe_fsh.json 2> gpurun_out/$T/rank_probe_fsh.log || exit 1
   ;;
+coop)   # cooperative leaf step: parity, GUI/synchronous calls (k_path), bench A/B (k_extend/k_shadow), rank probe
+  env KHP_LIB=variants/libkirk_coopP32.so bash tools/gpu_r05.sh parity $T || exit 1
+  mv gpurun_out/$T/tests_parity.log gpurun_out/$T/tests_parity_coopP32.log
+  env KHP_LIB=variants/libkirk_coopT32.so bash tools/gpu_r05.sh parity $T || exit 1
+  mv gpurun_out/$T/tests_parity.log gpurun_out/$T/tests_parity_coopT32.log
+  for r in 1 2; do
+    for v in base coopP16 coopP32 coopP48; do
+      if [ $v = base ]; then L=""; else L="KHP_LIB=variants/libkirk_$v.so"; fi
+      env $L timeout -k 10 200 python -u tools/sync_calls.py 8 >> gpurun_out/$T/sync_calls.jsonl 2>> gpurun_out/$T/sync_calls.log || exit 1
+    done
+  done
+  bash tools/gpu_r05.sh vars $T "coopT32" > gpurun_out/$T/vars.txt || exit 1
+  env KHP_LIB=variants/libkirk_coopT32.so timeout -k 10 300 python -u tools/rank_probe.py > gpurun_out/$T/rank_probe_coopT32.json 2> gpurun_out/$T/rank_probe_coopT32.log || exit 1
+  ;;
 full)   # every GPU test, then the driver's bench command and the default one
   timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver.json 2> gpurun_out/$T/bench_driver.log || exit 1
