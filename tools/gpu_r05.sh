@@ -94,6 +94,12 @@ coop)   # cooperative leaf step: parity, GUI/synchronous calls (k_path), bench A
   bash tools/gpu_r05.sh vars $T "coopT32" > gpurun_out/$T/vars.txt || exit 1
   env KHP_LIB=variants/libkirk_coopT32.so timeout -k 10 300 python -u tools/rank_probe.py > gpurun_out/$T/rank_probe_coopT32.json 2> gpurun_out/$T/rank_probe_coopT32.log || exit 1
   ;;
+one)   # one variant $3: parity, bench A/B, rank probe
+  env KHP_LIB=variants/libkirk_$3.so bash tools/gpu_r05.sh parity $T || exit 1
+  bash tools/gpu_r05.sh vars $T "$3" > gpurun_out/$T/vars.txt || exit 1
+  timeout -k 10 300 python -u tools/rank_probe.py > gpurun_out/$T/rank_probe_base.json 2> gpurun_out/$T/rank_probe_base.log || exit 1
+  env KHP_LIB=variants/libkirk_$3.so timeout -k 10 300 python -u tools/rank_probe.py > gpurun_out/$T/rank_probe_$3.json 2> gpurun_out/$T/rank_probe_$3.log || exit 1
+  ;;
 full)   # every GPU test, then the driver's bench command and the default one
   timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver.json 2> gpurun_out/$T/bench_driver.log || exit 1
