@@ -42,6 +42,10 @@ struct DevScene {
     int32_t textured;
     khp_env_map env_map;
     const uint32_t* __restrict__ tri_slot;  // object-id order: the slot of each triangle (NaN-origin shadow rays)
+    // khp_ctx_params.lds_nodes: the tree's top TOP_NODES interior records (BFS order) with
+    // the refs between them rewritten to TOP_REF | index, and the root's ref in that form
+    const float4* __restrict__ top;
+    int32_t top_root;
 };
 
 // ---- textures (ABI 6) -------------------------------------------------------------------

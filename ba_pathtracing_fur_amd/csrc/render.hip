@@ -300,10 +300,11 @@ constexpr size_t EXT_LDS_BYTES = 3 * EXT_RING * TRAV_BLOCK * sizeof(uint32_t);
 constexpr int CAM_RING = KHP_CAM_RING;
 constexpr int CAM_WAVES = KHP_CAM_WAVES;
 constexpr size_t CAM_LDS_BYTES = 3 * CAM_RING * TRAV_BLOCK * sizeof(uint32_t);
-template <bool STATS>
-using TravStack = LdsStack<RING, STATS>;
-template <bool STATS, bool CAM = false>
-using ExtStack = LdsStack<CAM ? CAM_RING : EXT_RING, STATS>;
+template <bool STATS, bool TOP = false>
+using TravStack = LdsStack<RING, STATS, TOP>;
+template <bool STATS, bool CAM = false, bool TOP = false>
+using ExtStack = LdsStack<CAM ? CAM_RING : EXT_RING, STATS, TOP>;
+constexpr size_t TOP_LDS_BYTES = TOP_NODES * sizeof(DevNode);   // added to a TOP instance's LDS
 
 struct SpillArea {
     int4* base;
@@ -480,12 +481,14 @@ __global__ __launch_bounds__(256) void k_pix_order(const uint32_t* __restrict__ 
 // CAM: bounce 0 with Wave::cam0 -- the ray of queue slot idx (= path idx) is
 // the camera ray, computed here instead of loaded.
 // WIDE: the two-level records (S.wide, traverse.h iterw) instead of the 64-B loop.
-template <bool STATS, bool CAM = false, bool WIDE = false>
+// TOP: the tree's top records staged in LDS (khp_ctx_params.lds_nodes; 64-B loop only).
+template <bool STATS, bool CAM = false, bool WIDE = false, bool TOP = false>
 __global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : CAM ? CAM_WAVES : EXT_WAVES) void k_extend(DevScene S, Wave Wv, int cur, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t nf = Wv.cnt->nq[cur], nb = Wv.cnt->nqb[cur];
-    ExtStack<STATS, CAM> stk;
+    ExtStack<STATS, CAM, TOP> stk;
     stk.init(lds, spill.base, spill.stride);
+    if (TOP) stk.stage_top(S.top);
     TravStats st{0, 0, 0};
     TravRay tr;
     Hit h;
@@ -565,8 +568,13 @@ __global__ __launch_bounds__(TRAV_BLOCK, WIDE ? EXT_WAVES_W : CAM ? CAM_WAVES : 
 
 // Host-side launch of the k_extend instance for (stats, camera rays in place, wide records).
 static void launch_extend(bool stats, bool cam, bool wide, int grid, hipStream_t s, const DevScene& S, const Wave& W,
-                          int cur, SpillArea sp) {
+                          int cur, SpillArea sp, bool top = false) {
     const dim3 g(grid), b(TRAV_BLOCK);
+    if (top && !stats && !wide && S.top) {   // the top records in LDS (lds_nodes)
+        if (cam) hipLaunchKernelGGL((k_extend<false, true, false, true>), g, b, CAM_LDS_BYTES + TOP_LDS_BYTES, s, S, W, cur, sp);
+        else hipLaunchKernelGGL((k_extend<false, false, false, true>), g, b, EXT_LDS_BYTES + TOP_LDS_BYTES, s, S, W, cur, sp);
+        return;
+    }
 #define KHP_EXT(ST, CA, WI) \
     hipLaunchKernelGGL((k_extend<ST, CA, WI>), g, b, CA ? CAM_LDS_BYTES : EXT_LDS_BYTES, s, S, W, cur, sp)
     if (wide) {
@@ -1393,12 +1401,13 @@ __global__ __launch_bounds__(256) void k_shadow_finish(DevScene S, Wave Wv, int 
 }
 
 // WIDE: the two-level records (traverse.h iterw) instead of the 64-B loop.
-template <bool STATS, bool WIDE = false>
+template <bool STATS, bool WIDE = false, bool TOP = false>
 __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, Wave Wv, SpillArea spill) {
     extern __shared__ uint32_t lds[];
     const uint32_t nf = Wv.shq->nsh, nb = Wv.shq->nshb;
-    TravStack<STATS> stk;
+    TravStack<STATS, TOP> stk;
     stk.init(lds, spill.base, spill.stride);
+    if (TOP) stk.stage_top(S.top);
     TravStats st{0, 0, 0};
     TravRay tr;
     Cur c{0u, 0.0f, 0.0f, false};
@@ -1464,8 +1473,13 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, W
 }
 
 // Host-side launch of the k_shadow instance for (stats, wide records).
-static void launch_shadow(bool stats, bool wide, int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp) {
+static void launch_shadow(bool stats, bool wide, int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp,
+                          bool top = false) {
     const dim3 g(grid), b(TRAV_BLOCK);
+    if (top && !stats && !wide && S.top) {
+        hipLaunchKernelGGL((k_shadow<false, false, true>), g, b, LDS_BYTES + TOP_LDS_BYTES, s, S, W, sp);
+        return;
+    }
     if (wide) {
         if (stats) hipLaunchKernelGGL((k_shadow<true, true>), g, b, LDS_BYTES, s, S, W, sp);
         else hipLaunchKernelGGL((k_shadow<false, true>), g, b, LDS_BYTES, s, S, W, sp);
@@ -2152,6 +2166,37 @@ __global__ void k_tri_slots(const float4* prims, const Aux* aux, uint32_t n_slot
 // std::max union of its children's boxes, or a child box of it is not ordered
 // (mn <= mx on every axis, NaN fails): the composition in iterw would not be
 // KIRK's slab then, and the context keeps the 64-B loop.
+// The tree's top three levels of interior nodes in BFS order, for the instances
+// that stage them in LDS (khp_ctx_params.lds_nodes): the refs between them
+// rewritten to TOP_REF | index; everything else (boxes, leaf and deeper refs,
+// counts) as in the node array, so the walk, its order and its counts are KIRK's.
+__global__ void k_top_nodes(const DevNode* __restrict__ nodes, int32_t root_ref, DevNode* __restrict__ top) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    uint32_t ids[TOP_NODES], depth[TOP_NODES], n = 0;
+    if (((uint32_t)root_ref & LEAF_BIT) == 0u) {
+        ids[n] = (uint32_t)root_ref;
+        depth[n++] = 0;
+    }
+    for (uint32_t k = 0; k < n; ++k)
+        for (int ch = 0; ch < 2; ++ch) {
+            const uint32_t r = (uint32_t)nodes[ids[k]].ref[ch];
+            if ((r & LEAF_BIT) == 0u && depth[k] + 1u < 3u && n < TOP_NODES) {
+                ids[n] = r;
+                depth[n++] = depth[k] + 1u;
+            }
+        }
+    for (uint32_t k = 0; k < TOP_NODES; ++k) {
+        DevNode o{};
+        if (k < n) {
+            o = nodes[ids[k]];
+            for (int ch = 0; ch < 2; ++ch)
+                for (uint32_t j = 1; j < n; ++j)
+                    if ((uint32_t)o.ref[ch] == ids[j]) o.ref[ch] = (int32_t)(TOP_REF | j);
+        }
+        top[k] = o;
+    }
+}
+
 __global__ void k_wide_records(const DevNode* nodes, uint32_t n, float4* wide, uint32_t* bad) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
@@ -2308,6 +2353,7 @@ struct khp_ctx {
     bool scene_set = false, built = false;
     DevMem prims, aux, trinrm, trifrm, nodes, mats, lights, trislot;
     DevMem wide, wide_bad;   // two-level node records (KHP_WIDE), the build's union check flag
+    DevMem topn;             // the top three levels' records for the LDS-staged instances (k_top_nodes)
     DevMem triuv, coneh, texd, texels, mtex;   // ABI 6 textures
     DevScene S{};
     khp_ctx_params prm{};
@@ -2565,6 +2611,7 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->wide_from = KHP_WIDE_FROM;  // two-level records from bounce 2
     out->path_kernel = 0;       // automatic: k_path for synchronous renders
     out->ray_sort_from = 2;     // bounces 2.. regrouped by origin cell, +1.8%
+    out->lds_nodes = 0;         // the top records in LDS, measured
 }
 
 extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {
@@ -2585,6 +2632,7 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     if (prm->serial_stages > 1) return fail(KHP_EINVAL, "serial_stages must be 0 or 1");
     if (prm->path_order > 2) return fail(KHP_EINVAL, "path_order must be 0, 1 or 2");
     if (prm->path_kernel > 2) return fail(KHP_EINVAL, "path_kernel must be 0, 1 or 2");
+    if (prm->lds_nodes != 0 && prm->lds_nodes != TOP_NODES) return fail(KHP_EINVAL, "lds_nodes must be 0 or 7");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
     if (dr != KHP_OK) return dr;
@@ -2922,6 +2970,12 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
         wide_ok = bad == 0;
     }
     if (!wide_ok) c->wide.release();
+    if (n_dnodes > 0) {   // the top-of-tree records for khp_ctx_params.lds_nodes
+        HIPCHK(c->topn.ensure(TOP_NODES * sizeof(DevNode)));
+        hipLaunchKernelGGL(k_top_nodes, dim3(1), dim3(64), 0, c->stream, c->nodes.as<DevNode>(), root_ref,
+                           c->topn.as<DevNode>());
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(c->trislot.ensure(4 * (size_t)std::max(hs.n_tris, 1u)));
     if (hs.n_tris > 0 && n_slots > 0)
         hipLaunchKernelGGL(k_tri_slots, dim3((n_slots + 255) / 256), dim3(256), 0, c->stream, c->prims.as<float4>(),
@@ -2937,6 +2991,8 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     S.tri_frame = host_build ? c->trifrm.as<float>() : c->obj.tri_frame.as<float>();
     S.nodes = c->nodes.as<DevNode>();
     S.wide = wide_ok ? c->wide.as<float4>() : nullptr;
+    S.top = n_dnodes > 0 ? c->topn.as<float4>() : nullptr;
+    S.top_root = n_dnodes > 0 && ((uint32_t)root_ref & LEAF_BIT) == 0u ? (int32_t)TOP_REF : root_ref;
     S.mats = c->mats.as<khp_material>();
     S.lights = c->lights.as<DevLight>();
     S.n_lights = (int32_t)hs.lights.size();
@@ -3601,7 +3657,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 const bool cam = b == 0 && Wv.cam0;
                 const bool wide = c->S.wide != nullptr && b >= c->prm.wide_from;
                 launch_extend(stats, cam, wide, wide ? grid_ext_w : cam ? grid_ext_cam : grid_ext, sA, c->S, Wb, cur,
-                              sp_ext);
+                              sp_ext, c->prm.lds_nodes != 0);
                 timed(c, f, 0, false, sA);
                 if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));
                 timed(c, f, 1, true, sA);
@@ -3676,7 +3732,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 }
                 timed(c, f, 2, true, sB);
                 const bool wide_sh = c->S.wide != nullptr && b >= std::max(c->prm.wide_from, (uint32_t)KHP_WIDE_SH_FROM);
-                launch_shadow(stats, wide_sh, wide_sh ? grid_sh_w : grid_sh, sB, c->S, Wb, sp_sh);
+                launch_shadow(stats, wide_sh, wide_sh ? grid_sh_w : grid_sh, sB, c->S, Wb, sp_sh, c->prm.lds_nodes != 0);
                 timed(c, f, 2, false, sB);
                 timed(c, f, 4, true, sB);   // shadow stage = any-hit traversal + finish
                 if (bdm) hipLaunchKernelGGL(k_shadow_finish<true>, dim3(c->grid_fin), dim3(256), 0, sB, c->S, Wb, cur ^ 1);

@@ -120,9 +120,17 @@ constexpr uint32_t TRAV_BLOCK = KHP_TRAV_BLOCK;
 // start of the kernel's dynamic LDS; a lane's column starts at its threadIdx.x.
 // The spill area is [STACK_MAX][grid lanes] int4, addressed from blockIdx /
 // threadIdx only on the (rare) spill path, so it costs no registers.
-template <int R, bool COUNT>
+// Top-of-tree staging (khp_ctx_params.lds_nodes, SURVEY north_star "node records
+// staged in LDS"): a kernel instance with TOP stages the tree's top TOP_NODES
+// interior records (three levels) after its rings, and a ref with TOP_REF set
+// (interior refs keep bits 24-30 clear) names one of them.
+constexpr uint32_t TOP_NODES = 7;
+constexpr uint32_t TOP_REF = 0x40000000u;
+template <int R, bool COUNT, bool TOP = false>
 struct LdsStack {
     static_assert(R >= 2 && R <= 16, "ring size");
+    static constexpr bool kTop = TOP;
+    static constexpr size_t kRingBytes = 3 * (size_t)R * TRAV_BLOCK * sizeof(uint32_t);
     uint32_t* lds;
     int4* spill;
     uint32_t stride;
@@ -134,6 +142,17 @@ struct LdsStack {
         stride = grid_lanes;
         sp = lo = 0;
         spills = 0;
+    }
+    // the staged top records (TOP instances; read-only after stage_top)
+    __device__ __forceinline__ const float4* top() const {
+        return reinterpret_cast<const float4*>(lds + 3 * R * TRAV_BLOCK);
+    }
+    // Copies the top records into this block's LDS (one-wave blocks: every lane
+    // takes part, then a barrier).
+    __device__ __forceinline__ void stage_top(const float4* __restrict__ src) {
+        float4* dst = reinterpret_cast<float4*>(lds + 3 * R * TRAV_BLOCK);
+        for (uint32_t i = threadIdx.x; i < 4 * TOP_NODES; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
     }
     __device__ __forceinline__ void clear() { sp = lo = 0; }
     __device__ __forceinline__ bool empty() const { return sp == 0; }
@@ -469,7 +488,7 @@ __device__ __forceinline__ bool trav2_begin(const DevScene& S, const TravRay& tr
         mode = M_POP;
         return true;
     }
-    take_entry<STATS>(S, (uint32_t)S.root_ref, t0, t1, mode, c, lf, st);
+    take_entry<STATS>(S, (uint32_t)(Stack::kTop ? S.top_root : S.root_ref), t0, t1, mode, c, lf, st);
     return true;
 }
 
@@ -499,7 +518,13 @@ __device__ __forceinline__ bool iter2k(const DevScene& S, const TravRay& tr, Hit
     const bool fetch = in_leaf || mode == M_NODE;
     const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
     float4 q0, q1, q2, q3;
-    if (fetch) {
+    if (Stack::kTop && fetch && !in_leaf && (c.ref & TOP_REF) != 0u) {   // a staged top record (LDS)
+        const float4* t = stk.top() + 4 * (c.ref & 0xFFu);
+        q0 = t[0];
+        q1 = t[1];
+        q2 = t[2];
+        q3 = t[3];
+    } else if (fetch) {
         q0 = p[0];
         q1 = p[1];
         q2 = p[2];

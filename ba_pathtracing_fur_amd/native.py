@@ -119,12 +119,13 @@ class Stats(ctypes.Structure):
 
 class CtxParams(ctypes.Structure):
     """khp_ctx_params (ABI 12 layout, 56 bytes; path_order since ABI 9, wide_from since
-    ABI 10, path_kernel since ABI 11, ray_sort_from since ABI 12): scheduling knobs of a
+    ABI 10, path_kernel since ABI 11, ray_sort_from and lds_nodes since ABI 12): scheduling knobs of a
     context; no value changes any result."""
     _fields_ = [("fuse_frames", c_uint32), ("frames_in_flight", c_uint32), ("chunk_paths", c_uint64),
                 ("heavy_iters", c_uint32), ("dump_bounce", c_int32), ("trace_kernels", c_uint32),
                 ("shade_order", c_uint32), ("serial_stages", c_uint32), ("path_order", c_uint32),
-                ("wide_from", c_uint32), ("path_kernel", c_uint32), ("ray_sort_from", c_uint32)]
+                ("wide_from", c_uint32), ("path_kernel", c_uint32), ("ray_sort_from", c_uint32),
+                ("lds_nodes", c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

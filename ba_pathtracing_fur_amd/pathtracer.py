@@ -171,7 +171,7 @@ class HipContext:
     def set_params(self, **kw) -> dict:
         """khp_set_params with the given fields changed (fuse_frames, frames_in_flight,
         chunk_paths, heavy_iters, dump_bounce, trace_kernels, shade_order, serial_stages,
-        path_order, wide_from, path_kernel, ray_sort_from); returns the previous values."""
+        path_order, wide_from, path_kernel, ray_sort_from, lds_nodes); returns the previous values."""
         prm = N.CtxParams()
         N.check(self.lib, self.lib.khp_get_params(self.ptr, ctypes.byref(prm)), "khp_get_params")
         old = prm.as_dict()

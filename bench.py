@@ -98,6 +98,8 @@ def parse():
                     help="khp_ctx_params.wide_from (first bounce on two-level node records; >= depth: never)")
     ap.add_argument("--ray-sort-from", type=int, default=None,
                     help="khp_ctx_params.ray_sort_from (first bounce whose rays are regrouped by origin cell; 0: never)")
+    ap.add_argument("--lds-nodes", type=int, default=None,
+                    help="khp_ctx_params.lds_nodes (0 or 7: the tree's top records staged in LDS)")
     ap.add_argument("--heavy-iters", type=int, default=None,
                     help="khp_ctx_params.heavy_iters (longest-first queue threshold, traversal iterations)")
     ap.add_argument("--bdpt", default=None, metavar="PATHS,VERTICES",
@@ -392,7 +394,8 @@ def main():
     knobs = {k: v for k, v in (("fuse_frames", args.fuse), ("chunk_paths", args.chunk_paths),
                                ("frames_in_flight", args.frames_in_flight), ("shade_order", args.shade_order),
                                ("heavy_iters", args.heavy_iters), ("path_order", args.path_order),
-                               ("wide_from", args.wide_from), ("ray_sort_from", args.ray_sort_from))
+                               ("wide_from", args.wide_from), ("ray_sort_from", args.ray_sort_from),
+                               ("lds_nodes", args.lds_nodes))
              if v is not None}
     if knobs:
         ctx.set_params(**knobs)

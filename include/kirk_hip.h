@@ -318,7 +318,11 @@ typedef struct {
                                     changes no result.  Default 2 (measured); 0 or >= depth:
                                     never.  Not with hit sorting (shade_order 1), the light-path variant or
                                     queue dumps; the path kernel never sorts                              */
-} khp_ctx_params;   /* 56 bytes (52 + tail padding) */
+    uint32_t lds_nodes;          /* ABI 12: 0 (default) or 7: the tree's top three levels of node records
+                                    staged in each traversal wave's LDS beside its stack rings (the 64-B
+                                    loops of k_extend and k_shadow), the rest fetched from HBM as before.
+                                    Same walk, same counts, same frames.  Measured in DESIGN.md §4    */
+} khp_ctx_params;   /* 56 bytes */
 
 /* ---- context --------------------------------------------------------------- */
 /* device: HIP device ordinal (one process per GPU). */

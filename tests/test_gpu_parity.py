@@ -172,18 +172,19 @@ TINY = {
 }
 
 
-@pytest.mark.parametrize("path_kernel", [1, 2])
+@pytest.mark.parametrize("path_kernel,lds_nodes", [(1, 0), (2, 0), (1, 7)])
 @pytest.mark.parametrize("name", list(TINY))
-def test_tiny_and_degenerate_trees(hip_ctx, name, path_kernel):
+def test_tiny_and_degenerate_trees(hip_ctx, name, path_kernel, lds_nodes):
     """Trees whose root is a leaf (one object; 3000 coplanar centroids, whose
     leaf count needs the escape word), two- and three-object trees (no
-    two-level record below the root), through the wavefront and the path
+    two-level record below the root; fewer top records than LDS slots),
+    through the wavefront (also with the top records in LDS) and the path
     kernel, synchronous and fused: the oracle's frame bit for bit."""
     sd = TINY[name]()
     want = oracle_ffi.Oracle(sd).render(24, 16, 3, 4, threads=16)
     hip_ctx.set_scene(sd)
     hip_ctx.build_accel()
-    old = hip_ctx.set_params(path_kernel=path_kernel)
+    old = hip_ctx.set_params(path_kernel=path_kernel, lds_nodes=lds_nodes)
     try:
         assert_parity(hip_ctx.render(24, 16, 3, 4), want, exact=True)
         for k in range(3):
@@ -825,6 +826,38 @@ def test_ray_sorting_frames(hip_ctx, name, kw, w, h, spp, depth):
     finally:
         hip_ctx.set_params(**old)
     assert len(counts) == 1
+
+
+@pytest.mark.parametrize("name,kw,w,h,spp,depth", [CASES[0], CASES[1], CASES[4], CASES[5], CASES[8]],
+                         ids=["config1", "config2", "config5", "zoo", "textured"])
+def test_lds_top_nodes_frames(hip_ctx, name, kw, w, h, spp, depth):
+    """khp_ctx_params.lds_nodes (ABI 12): the tree's top three levels of node
+    records staged in each traversal wave's LDS (the 64-B loops of k_extend and
+    k_shadow) give the oracle's frame bit for bit -- synchronous through the
+    wavefront, and fused asynchronous passes -- with every bounce on the 64-B
+    loop (wide_from past the depth) and with the default two-level records."""
+    sd = S.build_config(name, width=w, height=h, **kw)
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    want = oracle_ffi.Oracle(sd).render(w, h, spp, depth, threads=16)
+    old = hip_ctx.params()
+    try:
+        for wf in (64, 2):
+            hip_ctx.set_params(lds_nodes=7, path_kernel=1, wide_from=wf)
+            assert_parity(hip_ctx.render(w, h, spp, depth), want, exact=True)
+            for k in range(spp):
+                hip_ctx.render(w, h, 1, depth, first_sample=k, async_=True)
+            hip_ctx.sync()
+            assert_parity(hip_ctx.read_framebuffer(w, h), want, exact=True)
+    finally:
+        hip_ctx.set_params(**old)
+
+
+def test_lds_top_nodes_rejects_other_counts(hip_ctx):
+    old = hip_ctx.params()
+    with pytest.raises(Exception):
+        hip_ctx.set_params(lds_nodes=3)
+    assert hip_ctx.params() == old
 
 
 PK_CASES = [CASES[0], CASES[1], CASES[2], CASES[3], CASES[4], CASES[5], CASES[8]]

@@ -100,6 +100,24 @@ one)   # one variant $3: parity, bench A/B, rank probe
   timeout -k 10 300 python -u tools/rank_probe.py > gpurun_out/$T/rank_probe_base.json 2> gpurun_out/$T/rank_probe_base.log || exit 1
   env KHP_LIB=variants/libkirk_$3.so timeout -k 10 300 python -u tools/rank_probe.py > gpurun_out/$T/rank_probe_$3.json 2> gpurun_out/$T/rank_probe_$3.log || exit 1
   ;;
+args)   # the in-tree library without / with bench args $3, alternated twice; then parity
+  for r in 1 2; do
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/$T/v_base_$r.json 2> gpurun_out/$T/v_base_$r.log || exit 1
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline $3 > gpurun_out/$T/v_args_$r.json 2> gpurun_out/$T/v_args_$r.log || exit 1
+  done
+  python - $T base args <<'PY' > gpurun_out/$T/vars.txt
+import json, sys
+t = sys.argv[1]
+for v in sys.argv[2:]:
+    for r in (1, 2):
+        d = json.loads(open(f"gpurun_out/{t}/v_{v}_{r}.json").read().strip().splitlines()[-1])
+        f = d["frame"]
+        print(v, r, d["value"], "sync", (d.get("sync_steps") or {}).get("value"), "ext", f["extend_ms"],
+              "per_bounce", [b["extend_ms"] for b in f["per_bounce"]], "shade", f["shade_ms"], "dev", f["device_ms"],
+              "iso_ext", d["isolated"]["k_extend"]["ms_per_frame"], "iso_sh", d["isolated"]["k_shadow"]["ms_per_frame"])
+PY
+  bash tools/gpu_r05.sh parity $T || exit 1
+  ;;
 full)   # every GPU test, then the driver's bench command and the default one
   timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver.json 2> gpurun_out/$T/bench_driver.log || exit 1
