@@ -97,7 +97,8 @@ def parse():
     ap.add_argument("--wide-from", type=int, default=None,
                     help="khp_ctx_params.wide_from (first bounce on two-level node records; >= depth: never)")
     ap.add_argument("--ray-sort-from", type=int, default=None,
-                    help="khp_ctx_params.ray_sort_from (first bounce whose rays are regrouped by origin cell; 0: never)")
+                    help="khp_ctx_params.ray_sort_from (first bounce whose rays are regrouped by origin cell; "
+                         "0: automatic, >= depth: never)")
     ap.add_argument("--lds-nodes", type=int, default=None,
                     help="khp_ctx_params.lds_nodes (0 or 7: the tree's top records staged in LDS)")
     ap.add_argument("--heavy-iters", type=int, default=None,

@@ -315,7 +315,9 @@ typedef struct {
                                     k_extend by the Morton cell (32^3 over the scene box) of their origin, so
                                     that the rays of a claim block start close together and share cache
                                     lines; the path state stays in place.  Which lane traces which ray
-                                    changes no result.  Default 2 (measured); 0 or >= depth:
+                                    changes no result.  0 (default): automatic -- bounce 2 when the tree's
+                                    node records exceed 64 MB, else never (a cache-resident tree has no
+                                    misses to save; measured); 1..: that bounce; >= depth:
                                     never.  Not with hit sorting (shade_order 1), the light-path variant or
                                     queue dumps; the path kernel never sorts                              */
     uint32_t lds_nodes;          /* ABI 12: 0 (default) or 7: the tree's top three levels of node records

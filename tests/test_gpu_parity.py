@@ -802,8 +802,9 @@ def test_wide_records_frames(hip_ctx, name, kw, w, h, spp, depth):
                          ids=["config2", "config5", "zoo", "textured"])
 def test_ray_sorting_frames(hip_ctx, name, kw, w, h, spp, depth):
     """khp_ctx_params.ray_sort_from (ABI 12): the wavefront's extension rays
-    regrouped by origin cell from bounce 1, 2 (default), 3 or never give the
-    oracle's frame bit for bit -- synchronous, instrumented and fused
+    regrouped by origin cell from bounce 1, 2 (the automatic choice for large
+    trees), 3, never (64) or automatic (0: never for these small trees) give
+    the oracle's frame bit for bit -- synchronous, instrumented and fused
     asynchronous -- and KIRK's visit counts do not change.  The path kernel never
     sorts, so the synchronous calls here run the wavefront (path_kernel 1)."""
     sd = S.build_config(name, width=w, height=h, **kw)
@@ -813,7 +814,7 @@ def test_ray_sorting_frames(hip_ctx, name, kw, w, h, spp, depth):
     counts = set()
     old = hip_ctx.params()
     try:
-        for rs in (0, 1, 2, 3):
+        for rs in (0, 1, 2, 3, 64):
             hip_ctx.set_params(ray_sort_from=rs, path_kernel=1)
             assert_parity(hip_ctx.render(w, h, spp, depth), want, exact=True)
             assert_parity(hip_ctx.render(w, h, spp, depth, stats=True), want, exact=True)

@@ -118,6 +118,27 @@ for v in sys.argv[2:]:
 PY
   bash tools/gpu_r05.sh parity $T || exit 1
   ;;
+cfgs)   # the configs' bench lines, then the instruction-mix PMC passes at the driver's shape
+  for c in 1 2 3 5; do
+    timeout -k 10 400 python -u bench.py --config $c > gpurun_out/$T/cfg$c.json 2> gpurun_out/$T/cfg$c.log || exit 1
+  done
+  STEPS=20 bash tools/profile.sh $T mix mix2 || exit 1
+  ;;
+cfgsort)   # configs 1 and 2 with and without ray regrouping, alternated; claim-block variants on the metric row
+  for r in 1 2; do
+    for c in 1 2; do
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline --config $c > gpurun_out/$T/cfg${c}_rs2_$r.json 2> gpurun_out/$T/cfg${c}_rs2_$r.log || exit 1
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline --config $c --ray-sort-from 0 > gpurun_out/$T/cfg${c}_rs0_$r.json 2> gpurun_out/$T/cfg${c}_rs0_$r.log || exit 1
+    done
+  done
+  bash tools/gpu_r05.sh vars $T "cb8 cb11" > gpurun_out/$T/vars.txt || exit 1
+  ;;
+autosort)   # parity, then the configs and the metric row with the library defaults
+  bash tools/gpu_r05.sh parity $T || exit 1
+  for c in 1 2 metric; do
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --config $c > gpurun_out/$T/cfg$c.json 2> gpurun_out/$T/cfg$c.log || exit 1
+  done
+  ;;
 full)   # every GPU test, then the driver's bench command and the default one
   timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver.json 2> gpurun_out/$T/bench_driver.log || exit 1
