@@ -807,8 +807,8 @@ __device__ __forceinline__ bool bd_connection(const DevScene& S, const BdptDev& 
 // holds rays that start close together, and whose near subtrees therefore share
 // L2 lines.  Which lane traces which ray changes no result (every entry is
 // claimed exactly once and written to its own slot).  All counts stay on the
-// device: k_rsort_count / k_rsort_scan / k_rsort_scatter build the permutation,
-// k_rsort_gather writes the regrouped ray columns and the state indirection.
+// device: k_rsort_count (cells), k_rsort_scan (cell offsets), k_rsort_scatter
+// (the regrouped ray columns and the state indirection).
 constexpr uint32_t RS_LOG = 5;   // cells per axis = 2^RS_LOG (16^3 cells measured the same)
 constexpr uint32_t RS_CELLS = 1u << (3 * RS_LOG);
 __device__ __forceinline__ uint32_t rs_spread(uint32_t v) {   // 5 bits -> every third bit
@@ -879,11 +879,17 @@ __global__ __launch_bounds__(1024) void k_rsort_scan(const uint32_t* hist, uint3
         run += hist[t * PER + k];
     }
 }
-// scatter: each block reserves one range per cell it holds, then places its rays
+// scatter: each block reserves one range per cell it holds, then writes its rays'
+// columns and their state slots there (reads coalesced; the writes come in runs,
+// one per cell and block).  Regrouped entry j goes to the physical slot virtual
+// index j had, so the queue's front / back counts still describe it; its state
+// stays at slot qsrc[j].  (A permutation plus a gather pass with scattered reads
+// measured 0.06 ms per frame slower, profiles/r05ab_sort_scatter_ab.txt.)
 __global__ __launch_bounds__(RS_THREADS) void k_rsort_scatter(Wave Wv, int q, const uint32_t* keys, uint32_t* cursor,
-                                                              uint32_t* perm) {
+                                                              float* cols, uint32_t* qsrc) {
     __shared__ uint32_t lh[RS_CELLS];
     const uint32_t nf = Wv.cnt->nq[q], n = nf + Wv.cnt->nqb[q];
+    const size_t cap = Wv.cap;
     for (uint32_t c = threadIdx.x; c < RS_CELLS; c += RS_THREADS) lh[c] = 0u;
     __syncthreads();
     uint32_t a, b;
@@ -893,16 +899,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rsort_scatter(Wave Wv, int q, co
     for (uint32_t c = threadIdx.x; c < RS_CELLS; c += RS_THREADS)
         if (lh[c]) lh[c] = atomicAdd(&cursor[c], lh[c]);
     __syncthreads();
-    for (uint32_t v = a + threadIdx.x; v < b; v += RS_THREADS) perm[atomicAdd(&lh[keys[v]], 1u)] = q_phys(v, nf, Wv.cap);
-}
-// regrouped entry j goes to the physical slot virtual index j had (so the queue's
-// front/back counts still describe it); its state stays at slot perm[j] (qsrc)
-__global__ __launch_bounds__(256) void k_rsort_gather(Wave Wv, int q, const uint32_t* perm, float* cols,
-                                                      uint32_t* qsrc) {
-    const uint32_t nf = Wv.cnt->nq[q], n = nf + Wv.cnt->nqb[q];
-    const size_t cap = Wv.cap;
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        const uint32_t src = perm[j], dst = q_phys(j, nf, Wv.cap);
+    for (uint32_t v = a + threadIdx.x; v < b; v += RS_THREADS) {
+        const uint32_t src = q_phys(v, nf, Wv.cap);
+        const uint32_t dst = q_phys(atomicAdd(&lh[keys[v]], 1u), nf, Wv.cap);
         for (int k = 0; k < 3; ++k) {
             cols[k * cap + dst] = Wv.qo[q][k][src];
             cols[(3 + k) * cap + dst] = Wv.qd[q][k][src];
@@ -911,7 +910,6 @@ __global__ __launch_bounds__(256) void k_rsort_gather(Wave Wv, int q, const uint
         qsrc[dst] = src;
     }
 }
-
 constexpr uint32_t NCLS = 1 + KHP_BSDF_COUNT;
 static_assert(NCLS <= 16, "hit classes");
 __device__ __forceinline__ uint32_t hit_class(const DevScene& S, int32_t slot) {
@@ -2290,7 +2288,7 @@ struct PathSet {
     DevMem lvb;                   // light-path variant: subpath vertices of a chunk's sample slots
     DevMem plane, pspill;         // k_path: per-lane path state columns, traversal-stack spill columns
     DevMem pixo, pixcnt;          // path_order 2: this batch's heavy-first pixel list, its two cursors
-    DevMem rs_cols, rs_qsrc, rs_perm, rs_hist, rs_keys;   // ray sorting: regrouped ray columns, state slots, permutation, cells
+    DevMem rs_cols, rs_qsrc, rs_hist, rs_keys;   // ray sorting: regrouped ray columns, state slots, cell counts, cells
     size_t sh_cap = 0;            // shadow-record capacity per parity (cap x connections per path)
     hipStream_t sA = nullptr, sB = nullptr;
 };
@@ -3690,7 +3688,6 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                         const size_t cp = w.cap;
                         HIPCHK(w.rs_cols.ensure(7 * cp * sizeof(float)));
                         HIPCHK(w.rs_qsrc.ensure(cp * sizeof(uint32_t)));
-                        HIPCHK(w.rs_perm.ensure(cp * sizeof(uint32_t)));
                         HIPCHK(w.rs_keys.ensure(cp * sizeof(uint32_t)));
                         HIPCHK(w.rs_hist.ensure(2 * RS_CELLS * sizeof(uint32_t)));
                         uint32_t* hist = w.rs_hist.as<uint32_t>();
@@ -3703,9 +3700,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                                            w.rs_keys.as<uint32_t>());
                         hipLaunchKernelGGL(k_rsort_scan, dim3(1), dim3(1024), 0, sA, hist, hist + RS_CELLS);
                         hipLaunchKernelGGL(k_rsort_scatter, rs_grid, dim3(RS_THREADS), 0, sA, Wn, cur ^ 1,
-                                           w.rs_keys.as<uint32_t>(), hist + RS_CELLS, w.rs_perm.as<uint32_t>());
-                        hipLaunchKernelGGL(k_rsort_gather, dim3(c->grid_shade), dim3(256), 0, sA, Wn, cur ^ 1,
-                                           w.rs_perm.as<uint32_t>(), w.rs_cols.as<float>(), w.rs_qsrc.as<uint32_t>());
+                                           w.rs_keys.as<uint32_t>(), hist + RS_CELLS, w.rs_cols.as<float>(),
+                                           w.rs_qsrc.as<uint32_t>());
                         HIPCHK(hipGetLastError());
                         timed(c, f, 1, false, sA);
                     }
