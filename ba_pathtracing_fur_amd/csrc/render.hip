@@ -3625,6 +3625,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
             }
             hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
             bool sorted = false;          // this bounce's queue was regrouped by origin cell (rs_*)
+            bool prepped = false;         // this bounce's k_prep was enqueued before the previous fork
             for (uint32_t b = 0; b < (use_path ? 0u : p->depth); ++b) {
                 const int cur = b & 1;
                 c->cur_bounce = (int)b;
@@ -3655,7 +3656,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                         HIPCHK(hipMemcpy(dst + nq[0], col + (Wv.cap - nq[1]), 4 * (size_t)nq[1], hipMemcpyDeviceToHost));
                     }
                 }
-                hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
+                if (!prepped) hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
+                prepped = false;
                 timed(c, f, 0, true, sA);
                 const bool cam = b == 0 && Wv.cam0;
                 const bool wide = c->S.wide != nullptr && b >= c->prm.wide_from;
@@ -3709,6 +3711,16 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 };
                 KHPCHK(sort_next());   // before the shadow stage forks: alone on the chip it takes ~0.2 ms
                                        // per frame, beside the shadow stage's persistent grid ~2 ms
+                if (!stats && sB != sA && b + 1 < p->depth) {
+                    // the next bounce's counter reset before the fork, so its k_extend is ready on
+                    // stream A when the shadow stage becomes ready on B (the queues it resets are
+                    // consumed: this bounce's, and the previous bounce's shadow queue, which
+                    // k_shade waited for); +0.4%, profiles/r05ad_early_prep_ab.txt.  Instrumented
+                    // renders keep the reset at the bounce's start (per-bounce counter snapshots)
+                    hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, w.shqb.as<ShadowQ>() + (cur ^ 1),
+                                       cur ^ 1);
+                    prepped = true;
+                }
                 if (sB != sA) {
                     hipEvent_t shaded = slot_event(f.sync_pool, f.sync_next, true);
                     HIPCHK(hipEventRecord(shaded, sA));

@@ -139,6 +139,42 @@ autosort)   # parity, then the configs and the metric row with the library defau
     timeout -k 10 300 python -u bench.py --no-cpu-baseline --config $c > gpurun_out/$T/cfg$c.json 2> gpurun_out/$T/cfg$c.log || exit 1
   done
   ;;
+args2)   # in-tree defaults vs bench args $3 vs bench args $4, alternated twice
+  for r in 1 2; do
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/$T/v_base_$r.json 2> gpurun_out/$T/v_base_$r.log || exit 1
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline $3 > gpurun_out/$T/v_a_$r.json 2> gpurun_out/$T/v_a_$r.log || exit 1
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline $4 > gpurun_out/$T/v_b_$r.json 2> gpurun_out/$T/v_b_$r.log || exit 1
+  done
+  python - $T base a b <<'PY' > gpurun_out/$T/vars.txt
+import json, sys
+t = sys.argv[1]
+for v in sys.argv[2:]:
+    for r in (1, 2):
+        d = json.loads(open(f"gpurun_out/{t}/v_{v}_{r}.json").read().strip().splitlines()[-1])
+        f = d["frame"]
+        print(v, r, d["value"], "sync", (d.get("sync_steps") or {}).get("value"), "ext", f["extend_ms"],
+              "per_bounce", [b["extend_ms"] for b in f["per_bounce"]], "shade", f["shade_ms"], "dev", f["device_ms"])
+PY
+  ;;
+drv)   # variant $3: parity, then the driver's command alternated with the in-tree library 3 times
+  env KHP_LIB=variants/libkirk_$3.so bash tools/gpu_r05.sh parity $T || exit 1
+  for r in 1 2 3; do
+    for v in base $3; do
+      if [ $v = base ]; then L=""; else L="KHP_LIB=variants/libkirk_$v.so"; fi
+      env $L timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/$T/d_${v}_$r.json 2> gpurun_out/$T/d_${v}_$r.log || exit 1
+    done
+  done
+  python - $T base $3 <<'PY' > gpurun_out/$T/vars.txt
+import json, sys
+t = sys.argv[1]
+for v in sys.argv[2:]:
+    for r in (1, 2, 3):
+        d = json.loads(open(f"gpurun_out/{t}/d_{v}_{r}.json").read().strip().splitlines()[-1])
+        f = d["frame"]
+        print(v, r, d["value"], "sync", (d.get("sync_steps") or {}).get("value"), "ext", [b["extend_ms"] for b in f["per_bounce"]],
+              "sh", [b["shadow_ms"] for b in f["per_bounce"]], "dev", f["device_ms"])
+PY
+  ;;
 full)   # every GPU test, then the driver's bench command and the default one
   timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver.json 2> gpurun_out/$T/bench_driver.log || exit 1
