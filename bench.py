@@ -291,7 +291,10 @@ def _pmc_profile(config: str, frames_per_launch: float | None = None):
     among the newest round's profiles, the one whose launches carried the number of
     fused frames nearest this run's (the driver's 20 passes: 10 per launch; the
     default 32: 8), else the newest.  Returns (file name, contents) or (None, None)."""
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_extend_*.json")))
+    def tag_order(f):   # r05p < r05z < r05aa: a round's tags run a..z, then aa, ab, ...
+        t = os.path.basename(f)[len("pmc_extend_"):].split(".")[0].split("_")[0]
+        return (t[:3], len(t), t, f)
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_extend_*.json")), key=tag_order)
     files = [f for f in files if ("_cfg" not in f) == (config == "metric") and
              (config == "metric" or f"_cfg{config}_" in f)]
     loaded = []
