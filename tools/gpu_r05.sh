@@ -175,6 +175,23 @@ for v in sys.argv[2:]:
               "sh", [b["shadow_ms"] for b in f["per_bounce"]], "dev", f["device_ms"])
 PY
   ;;
+drv2)   # variants $3 and $4 [and $5]: the driver's command alternated with the in-tree library 2 times each
+  for r in 1 2; do
+    for v in base $3 $4 $5; do
+      if [ $v = base ]; then L=""; else L="KHP_LIB=variants/libkirk_$v.so"; fi
+      env $L timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/$T/d_${v}_$r.json 2> gpurun_out/$T/d_${v}_$r.log || exit 1
+    done
+  done
+  python - $T base $3 $4 $5 <<'PY' > gpurun_out/$T/vars.txt
+import json, sys
+t = sys.argv[1]
+for v in sys.argv[2:]:
+    for r in (1, 2):
+        d = json.loads(open(f"gpurun_out/{t}/d_{v}_{r}.json").read().strip().splitlines()[-1])
+        f = d["frame"]
+        print(v, r, d["value"], "ext", [b["extend_ms"] for b in f["per_bounce"]], "lane", [b["lane_use"] for b in f["per_bounce"]], "dev", f["device_ms"])
+PY
+  ;;
 full)   # every GPU test, then the driver's bench command and the default one
   timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver.json 2> gpurun_out/$T/bench_driver.log || exit 1
