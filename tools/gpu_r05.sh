@@ -192,6 +192,27 @@ for v in sys.argv[2:]:
         print(v, r, d["value"], "ext", [b["extend_ms"] for b in f["per_bounce"]], "lane", [b["lane_use"] for b in f["per_bounce"]], "dev", f["device_ms"])
 PY
   ;;
+drvp)   # variant $3: parity, then the driver's command and the default bench alternated with the in-tree library
+  env KHP_LIB=variants/libkirk_$3.so bash tools/gpu_r05.sh parity $T || exit 1
+  env KHP_LIB=variants/libkirk_$3.so timeout -k 10 400 python -u -m pytest tests/test_output.py tests/test_multigpu.py -x -q --timeout 200 --timeout-method thread -m gpu > gpurun_out/$T/tests_other.log 2>&1 || exit 1
+  for r in 1 2; do
+    for v in base $3; do
+      if [ $v = base ]; then L=""; else L="KHP_LIB=variants/libkirk_$v.so"; fi
+      env $L timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/$T/d_${v}_$r.json 2> gpurun_out/$T/d_${v}_$r.log || exit 1
+      env $L timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/$T/v_${v}_$r.json 2> gpurun_out/$T/v_${v}_$r.log || exit 1
+    done
+  done
+  python - $T base $3 <<'PY' > gpurun_out/$T/vars.txt
+import json, sys
+t = sys.argv[1]
+for v in sys.argv[2:]:
+    for k in ("d", "v"):
+        for r in (1, 2):
+            d = json.loads(open(f"gpurun_out/{t}/{k}_{v}_{r}.json").read().strip().splitlines()[-1])
+            f = d["frame"]
+            print(v, k, r, d["value"], "sync", (d.get("sync_steps") or {}).get("value"), "ext", [b["extend_ms"] for b in f["per_bounce"]], "dev", f["device_ms"])
+PY
+  ;;
 full)   # every GPU test, then the driver's bench command and the default one
   timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver.json 2> gpurun_out/$T/bench_driver.log || exit 1
