@@ -280,8 +280,8 @@ constexpr int EXT_WAVES_W = KHP_EXT_WAVES_W;  // k_extend over the two-level rec
 #ifndef KHP_REFILL_CAM
 #define KHP_REFILL_CAM KHP_EXT_REFILL
 #endif
-#ifndef KHP_REFILL_NARROW
-#define KHP_REFILL_NARROW KHP_EXT_REFILL
+#ifndef KHP_REFILL_NARROW   // 28 in round 5 (bounce 1: 7.17 against 7.21-7.25 ms per frame, +0.2%)
+#define KHP_REFILL_NARROW 28
 #endif
 #ifndef KHP_REFILL_WIDE   // 16 since the ray regrouping (round 5: lane use 0.73 -> 0.76 at bounce 2, +0.3%)
 #define KHP_REFILL_WIDE 16
