@@ -277,8 +277,8 @@ constexpr int EXT_WAVES = KHP_EXT_WAVES;
 constexpr int EXT_WAVES_W = KHP_EXT_WAVES_W;  // k_extend over the two-level records (80 VGPRs: 6 waves)
 // k_extend's refill threshold per instance (bounce 0 / 64-B loop / two-level
 // loop), default KHP_EXT_REFILL for each; 16 and 32 measured for each
-#ifndef KHP_REFILL_CAM
-#define KHP_REFILL_CAM KHP_EXT_REFILL
+#ifndef KHP_REFILL_CAM   // 28 in round 5 (bounce 0: 4.56 against 4.72 ms per frame, +0.5%)
+#define KHP_REFILL_CAM 28
 #endif
 #ifndef KHP_REFILL_NARROW   // 28 in round 5 (bounce 1: 7.17 against 7.21-7.25 ms per frame, +0.2%)
 #define KHP_REFILL_NARROW 28
