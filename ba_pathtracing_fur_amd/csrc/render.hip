@@ -192,14 +192,16 @@ __device__ __forceinline__ T wave_sum(T v) {
 // Camera ray and RNG key of path pid.  k_generate writes them to the bounce-0
 // queue; with Wave::cam0 set, k_extend and k_shade compute them in place at
 // bounce 0 instead (queue slot = path there), the same operations.
-__device__ __forceinline__ Ray camera_path(const DevScene& S, const Wave& Wv, uint32_t pid, uint32_t& key) {
+__device__ __forceinline__ Ray camera_path(const DevScene& S, const Wave& Wv, uint32_t pid, uint32_t& key,
+                                           uint32_t s_off = 0u) {
     // the samples of one pixel are adjacent paths (path_coords), so a wave traces
-    // a few neighbouring pixels x all their samples (cache reuse)
+    // a few neighbouring pixels x all their samples (cache reuse); s_off: the
+    // render-ahead set's sample offset (k_path)
     uint32_t fr, p_local, s_local;
     path_coords(Wv, pid, fr, p_local, s_local);
     const uint32_t pixel = Wv.pix[Wv.p_off + p_local];
     const uint32_t x = pixel % Wv.W, y = pixel / Wv.W;
-    key = path_key(Wv.seed, pixel, Wv.fsample0[fr] + s_local);
+    key = path_key(Wv.seed, pixel, Wv.fsample0[fr] + s_local + s_off);
     const float u1 = draw_u01(key, dim_of(0, P_CAM_X)), u2 = draw_u01(key, dim_of(0, P_CAM_Y));
     const khp_camera& cam = S.cam;
     const float s1 = ((float)x + u1) * cam.pixel_size, s2 = ((float)y + u2) * cam.pixel_size;
@@ -1528,6 +1530,75 @@ struct PathLanes {
     float4* col[8];
 };
 
+// ---- render-ahead (khp_ctx_params.render_ahead, ABI 13) ---------------------------------------
+// KIRK's GUI calls PathTracer::render once per pass and waits for it
+// (CPU_PathTracer.cpp:17-52); a synchronous k_path launch ends with the drain
+// of its longest paths, ~45% of a 1-spp call with most lanes idle (DESIGN.md
+// §5b).  With render-ahead the launch of call k renders the paths of sample
+// set k ("own") and, once every own path is claimed, lets its idle lanes claim
+// the camera paths of the set the NEXT matching call will ask for ("ahead":
+// the same pixels, samples [first_sample + spp, first_sample + 2 spp)).  An
+// ahead path that ends writes its colour to the ahead set's column; the
+// launch ends as soon as every own path has ended (a counter that the waves
+// poll), and each lane still holding an ahead path parks it: the path state
+// at the start of its current traversal (the 8 PathLanes columns, the ray,
+// the query kind) goes to a park record and the traversal is redone later.
+// Call k+1 resumes the parked paths first, claims its unclaimed paths from
+// the cursors call k advanced, and accumulates the colour column call k
+// filled.  Paths are independent and deterministic functions of (scene,
+// camera, parameters, pixel, sample), so each call's colours -- and its
+// accumulate, texture and framebuffer -- are those of rendering it alone.
+// The host drops the ahead set on any change of scene, camera, parameters,
+// size or first_sample (AheadSet).
+constexpr uint32_t AHEAD_BIT = 0x80000000u;   // PathLanes col[2].w: the path belongs to the ahead set
+constexpr uint32_t PARK_F4 = 10;              // float4 per park record: 8 columns, (o, t_max), (d, any)
+struct alignas(128) AheadState {
+    uint32_t fetch[2][NSEG * 32];   // per set parity: claim cursors (one 128-B line each)
+    uint32_t done[2][32];           // paths of the set that have ended
+    uint32_t park_n[2][32];         // records parked for the set
+    uint32_t take[2][32];           // resume cursor over them
+};
+struct Ahead {
+    uint32_t on;           // 0: a plain synchronous launch (the fields below unused)
+    uint32_t npaths;       // paths per set (= the launch's own paths)
+    uint32_t s_off;        // ahead camera paths: sample offset from the own set's
+    const uint32_t* park_n_own;   // records parked for the own set by the previous launch
+    float4* ck;            // the ahead set's colour column (Wave::CK is the own set's)
+    uint32_t* fetch_own;   // the own set's claim cursors (advanced by the previous launch's ahead claims)
+    uint32_t* fetch_ahead; // the ahead set's (zero at launch)
+    uint32_t* done_own;
+    uint32_t* done_ahead;
+    uint32_t* park_n_ahead;
+    uint32_t* take_own;
+    const float4* park_own;  // the previous launch's park records (own set)
+    float4* park_ahead;      // this launch's park records
+};
+// Ends a path: its colour to its set's column; 1 for an own path, 2 for an ahead path.
+__device__ __forceinline__ uint32_t end_path(const Wave& Wv, const Ahead& A, uint32_t pw, float4 cko) {
+    if (pw & AHEAD_BIT) {
+        A.ck[pw & ~AHEAD_BIT] = cko;
+        return 2u;
+    }
+    Wv.CK[pw] = cko;
+    return 1u;
+}
+// Every own path of the launch has ended (render-ahead; wave-uniform).
+__device__ __forceinline__ bool own_set_done(const Ahead& A) {
+    const uint32_t d = __hip_atomic_load(A.done_own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(d) >= A.npaths;
+}
+__global__ void k_ahead_reset(AheadState* a, int q, int both) {
+    for (int p = 0; p < 2; ++p) {
+        if (p != q && !both) continue;
+        for (uint32_t i = threadIdx.x; i < NSEG * 32; i += blockDim.x) a->fetch[p][i] = 0;
+        if (threadIdx.x == 0) {
+            a->done[p][0] = 0;
+            a->park_n[p][0] = 0;
+            a->take[p][0] = 0;
+        }
+    }
+}
+
 // k_shade's per-hit operations without the light-path variant (KIRK's traceRay
 // light test, EnvironmentShader / LightShader / SimpleShader /
 // MarschnerHairShader): the path state after bounce `bounce` and, when the NEE
@@ -1699,10 +1770,15 @@ __device__ uint32_t g_wprof_n;
 #endif
 
 template <bool TEX, bool WIDE, uint32_t KINDS>
-__global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wave Wv, SpillArea spill, PathLanes L) {
+__global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wave Wv, SpillArea spill, PathLanes L, Ahead A) {
     extern __shared__ uint32_t lds[];
     const uint32_t npaths = Wv.P * Wv.n_samples * Wv.n_frames;
     const uint32_t g = blockIdx.x * TRAV_BLOCK + threadIdx.x;
+    if (A.on && own_set_done(A)) return;   // render-ahead: the previous launch finished this whole set
+    // render-ahead (wave-uniform): parked own paths may remain / the ahead set has unclaimed paths
+    const uint32_t park_n_own = A.on ? __builtin_amdgcn_readfirstlane(*A.park_n_own) : 0u;
+    bool res_left = park_n_own > 0u, ahead_left = A.on != 0u, stop = false;
+    uint32_t poll_it = 0;
     LdsStack<PATH_RING, false> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0, 0};
@@ -1715,8 +1791,9 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     uint32_t mode = 0u, state = PS_NEW, n_ext = 0, n_sh = 0;
     bool any = false, occ = false, exhausted = false;
     float tmax_any = 0.0f;
-    Claimer cl;
-    cl.init(Wv.cnt->fetch_ext, npaths, 0u, npaths);
+    Claimer cl, cl2;   // own set, ahead set (render-ahead)
+    cl.init(A.on ? A.fetch_own : Wv.cnt->fetch_ext, npaths, 0u, npaths);
+    cl2.init(A.on ? A.fetch_ahead : Wv.cnt->fetch_ext, npaths, 0u, npaths);
 #ifdef KHP_PATH_PROFILE   // diagnostic builds: launch timeline (100 MHz wall clock): first start, last
     // claim exhaustion seen, last end, longest drain of one wave (its end - its exhaustion)
     const unsigned long long pc_start = wall_clock64();
@@ -1731,12 +1808,18 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
             pw_ntrav_exh = (uint32_t)__popcll(__ballot(state == PS_TRAV || state == PS_FIN || state == PS_BEGIN));
         }
 #endif
+        // render-ahead: once every own path has ended, park the ahead paths (below) and leave
+        if (stop || (A.on && exhausted && !res_left && own_set_done(A))) {
+            stop = true;
+            break;
+        }
         // ---- service: shade finished extension rays, finish shadow rays, claim camera
         //      paths, start traversals -- until every lane traverses or has no work left
         for (;;) {
             Ray sray;          // the ray a lane starts next (PS_BEGIN)
             bool sany = false;
             float stmax = 0.0f;
+            uint32_t ended = 0u;   // 1: an own path ended here, 2: an ahead path (render-ahead)
             sray.o = sray.d = mk(0, 0, 0);
             if (state == PS_FIN) {
                 const Ray fr = tr.r;
@@ -1770,7 +1853,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                         sray = o.nr;
                         state = PS_BEGIN;
                     } else {
-                        Wv.CK[bits_from_f(f2.w)] = cko;
+                        ended = end_path(Wv, A, bits_from_f(f2.w), cko);
                         state = PS_NEW;
                     }
                 } else {  // k_shadow_finish
@@ -1788,30 +1871,77 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                         sray.d = mk(f3.x, f3.y, f3.z);
                         state = PS_BEGIN;
                     } else {
-                        Wv.CK[bits_from_f(f2.w)] = cko;
+                        ended = end_path(Wv, A, bits_from_f(f2.w), cko);
                         state = PS_NEW;
                     }
                 }
             }
+            if (A.on) {   // render-ahead: ended paths per set
+                const unsigned long long eo = __ballot(ended == 1u), ea = __ballot(ended == 2u);
+                if (lane_id() == 0) {
+                    if (eo) atomicAdd(A.done_own, (uint32_t)__popcll(eo));
+                    if (ea) atomicAdd(A.done_ahead, (uint32_t)__popcll(ea));
+                }
+            }
             const unsigned long long want = __ballot(state == PS_NEW);
             if (want != 0ull) {  // wave-uniform: claim camera paths for the lanes whose path ended
-                uint32_t my = 0, pid = 0;
-                bool got = false;
-                if (!exhausted) got = cl.claim(want, my, exhausted);
-                if (state == PS_NEW) {
-                    if (got && cl.phys(my, pid)) {
-                        uint32_t key;
-                        sray = camera_path(S, Wv, pid, key);
-                        L.col[0][g] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));
-                        L.col[1][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));
-                        L.col[2][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(pid));
-                        L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(0u));
-                        sany = false;
+                if (res_left) {   // render-ahead: this set's paths parked by the previous launch first
+                    const uint32_t slot = wave_alloc(state == PS_NEW, A.take_own);
+                    if (__ballot(state == PS_NEW && slot >= park_n_own) != 0ull) res_left = false;
+                    if (state == PS_NEW && slot < park_n_own) {
+                        const float4* r = A.park_own + (size_t)slot * PARK_F4;
+#pragma unroll 1
+                        for (int k = 0; k < 8; ++k) {   // one record at a time (registers)
+                            float4 v = r[k];
+                            if (k == 2) v.w = f_from_bits(bits_from_f(v.w) & ~AHEAD_BIT);   // now an own path
+                            L.col[k][g] = v;
+                        }
+                        const float4 ro = r[8], rd = r[9];
+                        sray.o = mk(ro.x, ro.y, ro.z);
+                        sray.d = mk(rd.x, rd.y, rd.z);
+                        stmax = ro.w;
+                        sany = bits_from_f(rd.w) != 0u;
                         state = PS_BEGIN;
-                    } else if (exhausted) {
-                        state = PS_DONE;
                     }
                 }
+                // a camera path: the next of this call's set, or (render-ahead, once
+                // they are all claimed) of the next call's set
+                bool cam = false;
+                uint32_t cpid = 0, coff = 0;
+                const unsigned long long want1 = __ballot(state == PS_NEW);
+                if (want1 != 0ull && !exhausted) {
+                    uint32_t my = 0, pid = 0;
+                    const bool got = cl.claim(want1, my, exhausted);
+                    if (state == PS_NEW && got && cl.phys(my, pid)) {
+                        cam = true;
+                        cpid = pid;
+                    }
+                }
+                if (ahead_left && exhausted && !res_left) {
+                    const unsigned long long want2 = __ballot(state == PS_NEW && !cam);
+                    if (want2 != 0ull) {
+                        uint32_t my2 = 0, pid2 = 0;
+                        bool gone = false;
+                        const bool got2 = cl2.claim(want2, my2, gone);
+                        if (gone) ahead_left = false;
+                        if (state == PS_NEW && !cam && got2 && cl2.phys(my2, pid2)) {
+                            cam = true;
+                            cpid = pid2 | AHEAD_BIT;
+                            coff = A.s_off;
+                        }
+                    }
+                }
+                if (cam) {
+                    uint32_t key;
+                    sray = camera_path(S, Wv, cpid & ~AHEAD_BIT, key, coff);
+                    L.col[0][g] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));
+                    L.col[1][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));
+                    L.col[2][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(cpid));
+                    L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(0u));
+                    sany = false;
+                    state = PS_BEGIN;
+                }
+                if (state == PS_NEW && exhausted && !res_left && !ahead_left) state = PS_DONE;
             }
             if (state == PS_BEGIN) {  // k_extend's / k_shadow's ray start
                 TravRay t2;
@@ -1865,9 +1995,26 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
             // refill at REFILL finished lanes; once every path is claimed, as soon as
             // the finished lanes are as many as those still traversing (the drain;
             // servicing at every finished lane there measured 5% slower)
-            const uint32_t thr = exhausted ? (ntrav < PATH_REFILL ? (ntrav > 0u ? ntrav : 1u) : PATH_REFILL)
-                                           : PATH_REFILL;
+            const bool nomore = exhausted && !res_left && !ahead_left;
+            const uint32_t thr = nomore ? (ntrav < PATH_REFILL ? (ntrav > 0u ? ntrav : 1u) : PATH_REFILL)
+                                        : PATH_REFILL;
             if (ntrav == 0u || nfin >= thr) break;
+            // render-ahead: a wave busy with ahead paths looks for the end of the own set
+            if (A.on && exhausted && !res_left && (++poll_it & 31u) == 0u && own_set_done(A)) {
+                stop = true;
+                break;
+            }
+        }
+    }
+    if (stop) {   // render-ahead: the state at the start of each ahead path's current traversal, which is redone
+        bool ah = false;
+        if (state == PS_TRAV || state == PS_FIN) ah = (bits_from_f(L.col[2][g].w) & AHEAD_BIT) != 0u;
+        const uint32_t slot = wave_alloc(ah, A.park_n_ahead);
+        if (ah) {
+            float4* r = A.park_ahead + (size_t)slot * PARK_F4;
+            for (int k = 0; k < 8; ++k) r[k] = L.col[k][g];
+            r[8] = make_float4(tr.r.o.x, tr.r.o.y, tr.r.o.z, tmax_any);
+            r[9] = make_float4(tr.r.d.x, tr.r.d.y, tr.r.d.z, f_from_bits(any ? 1u : 0u));
         }
     }
     const unsigned long long se = wave_sum((unsigned long long)n_ext), ss = wave_sum((unsigned long long)n_sh);
@@ -1902,20 +2049,21 @@ constexpr size_t PATH_LDS = PATH_LDS_BYTES;
 constexpr uint32_t KINDS_ALL = (1u << KHP_BSDF_COUNT) - 1u;
 constexpr uint32_t KINDS_FUR = (1u << KHP_BSDF_LAMBERTIAN_REFLECTION) | (1u << KHP_BSDF_MARSCHNER_HAIR);
 template <bool TEX, bool WIDE, uint32_t K>
-static void launch_path_k(int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp, const PathLanes& L) {
-    hipLaunchKernelGGL((k_path<TEX, WIDE, K>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L);
+static void launch_path_k(int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp, const PathLanes& L,
+                          const Ahead& A) {
+    hipLaunchKernelGGL((k_path<TEX, WIDE, K>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L, A);
 }
 static void launch_path(bool tex, bool wide, bool fur, int grid, hipStream_t s, const DevScene& S, const Wave& W,
-                        SpillArea sp, const PathLanes& L) {
+                        SpillArea sp, const PathLanes& L, const Ahead& A) {
     if (tex) {
-        if (wide) launch_path_k<true, true, KINDS_ALL>(grid, s, S, W, sp, L);
-        else launch_path_k<true, false, KINDS_ALL>(grid, s, S, W, sp, L);
+        if (wide) launch_path_k<true, true, KINDS_ALL>(grid, s, S, W, sp, L, A);
+        else launch_path_k<true, false, KINDS_ALL>(grid, s, S, W, sp, L, A);
     } else if (fur) {
-        if (wide) launch_path_k<false, true, KINDS_FUR>(grid, s, S, W, sp, L);
-        else launch_path_k<false, false, KINDS_FUR>(grid, s, S, W, sp, L);
+        if (wide) launch_path_k<false, true, KINDS_FUR>(grid, s, S, W, sp, L, A);
+        else launch_path_k<false, false, KINDS_FUR>(grid, s, S, W, sp, L, A);
     } else {
-        if (wide) launch_path_k<false, true, KINDS_ALL>(grid, s, S, W, sp, L);
-        else launch_path_k<false, false, KINDS_ALL>(grid, s, S, W, sp, L);
+        if (wide) launch_path_k<false, true, KINDS_ALL>(grid, s, S, W, sp, L, A);
+        else launch_path_k<false, false, KINDS_ALL>(grid, s, S, W, sp, L, A);
     }
 }
 
@@ -2439,6 +2587,19 @@ struct khp_ctx {
     uint64_t lg_stamp[64] = {}, lg_count[64] = {};
     bool lg_taken[64] = {};
     uint64_t lg_seq = 0;
+    // render-ahead (khp_ctx_params.render_ahead, ABI 13; k_path's Ahead): the work a
+    // synchronous path-kernel call did for the next call of its progressive series
+    uint64_t gen = 1;   // bumped by every change of the scene, camera or parameters
+    struct AheadSet {
+        DevMem st, ck[2], park[2];   // AheadState; per set parity: colour column, park records
+        bool valid = false;          // the set of parity `own` belongs to the call `next`
+        int own = 0;
+        khp_render_params next{};
+        uint64_t gen = 0;
+        size_t npaths = 0;
+        uint32_t* hst = nullptr;     // pinned: the own set's finished / parked counts at the call's start
+        bool counted = false;        // hst was filled by the current call
+    } ra;
 };
 constexpr size_t LG_SLOTS = 64;
 
@@ -2611,6 +2772,7 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->path_kernel = 0;       // automatic: k_path for synchronous renders
     out->ray_sort_from = 0;     // automatic: bounces 2.. of large trees, +1.8% on the metric row
     out->lds_nodes = 0;         // the top records in LDS, measured
+    out->render_ahead = 1;      // synchronous path-kernel calls fill their drain with the next call's paths
 }
 
 extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {
@@ -2632,11 +2794,14 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     if (prm->path_order > 2) return fail(KHP_EINVAL, "path_order must be 0, 1 or 2");
     if (prm->path_kernel > 2) return fail(KHP_EINVAL, "path_kernel must be 0, 1 or 2");
     if (prm->lds_nodes != 0 && prm->lds_nodes != TOP_NODES) return fail(KHP_EINVAL, "lds_nodes must be 0 or 7");
+    if (prm->render_ahead > 1) return fail(KHP_EINVAL, "render_ahead must be 0 or 1");
+    if (prm->reserved0 != 0) return fail(KHP_EINVAL, "reserved0 must be 0");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
     if (dr != KHP_OK) return dr;
     c->prm = *prm;
     c->auto_chunk = 0;
+    ++c->gen;
     return KHP_OK;
 }
 
@@ -2668,6 +2833,18 @@ extern "C" khp_status khp_set_bdpt(khp_ctx* c, const khp_bdpt_params* p) {
     khp_status dr = drain(c);  // frames in flight finish with the estimator they started with
     if (dr != KHP_OK) return dr;
     c->bd = *p;
+    ++c->gen;
+    return KHP_OK;
+}
+
+extern "C" khp_status khp_set_camera(khp_ctx* c, const khp_camera* cam) {
+    if (!c || !cam) return fail(KHP_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    khp_status dr = drain(c);  // frames in flight finish with the camera they started with
+    if (dr != KHP_OK) return dr;
+    c->hs.cam = *cam;
+    c->S.cam = *cam;
+    ++c->gen;
     return KHP_OK;
 }
 
@@ -2722,6 +2899,7 @@ extern "C" void khp_destroy(khp_ctx* c) {
     for (auto e : c->sync_pool) (void)hipEventDestroy(e);
     if (c->tm_hl) (void)hipHostFree(c->tm_hl);
     if (c->tm_hm) (void)hipHostFree(c->tm_hm);
+    if (c->ra.hst) (void)hipHostFree(c->ra.hst);
     for (hipEvent_t e : c->tm_ev)
         if (e) (void)hipEventDestroy(e);
     for (auto* v : {&c->snaps, &c->snap_free})
@@ -2779,6 +2957,7 @@ static khp_status set_scene_impl(khp_ctx* c, const khp_scene* s, bool device_ptr
     }
     c->scene_set = false;
     c->built = false;
+    ++c->gen;
     std::string err = flatten_scene(s, c->hs, host);
     if (!err.empty()) return fail(KHP_EINVAL, err);
     c->st.flatten_kernel_ms = 0.0;
@@ -3065,6 +3244,7 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, true, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
     c->grid_path_w = std::min(c->grid_path, std::max(1, nb) * c->n_cu);   // the columns are sized by grid_path
     c->built = true;
+    ++c->gen;
     return KHP_OK;
 }
 
@@ -3214,6 +3394,7 @@ static void report_begin(khp_ctx* c) {
     }
     c->st.frames = 0;
     c->st.extend_busy_ms = 0.0;
+    c->st.ahead_finished = c->st.ahead_resumed = 0;
     c->ext_iv.clear();
     if (!c->report_ref) (void)hipEventCreate(&c->report_ref);
     (void)hipEventRecord(c->report_ref, c->stream);
@@ -3351,6 +3532,67 @@ static khp_status snapshot_now(khp_ctx* c, uint64_t id);
 static khp_status op_now(khp_ctx* c, const PendingOp& o) {
     return o.kind == PendingOp::SNAPSHOT ? snapshot_now(c, o.snap) : gather_now(c, &o.p, o.root);
 }
+// Render-ahead (k_path's Ahead): the call p of npaths paths in one chunk.  When
+// the previous such call rendered ahead for exactly this call (same scene,
+// camera, parameters, pixels, spp, depth, seed; first_sample = its own +
+// spp), its ahead set becomes this call's own set -- its finished colours,
+// claim cursors and parked paths -- otherwise both sets start empty.  The
+// other parity is cleared for this call's ahead set.  Enqueued on s before the
+// launch; ahead_commit records the set once the launch is enqueued.
+static bool ahead_key_equal(const khp_render_params& a, const khp_render_params& b) {
+    return a.width == b.width && a.height == b.height && a.spp == b.spp && a.depth == b.depth && a.seed == b.seed &&
+           a.first_sample == b.first_sample && a.tile_size == b.tile_size && a.tile_rank == b.tile_rank &&
+           a.tile_nranks == b.tile_nranks;
+}
+static khp_status ahead_prepare(khp_ctx* c, const khp_render_params* p, size_t npaths, hipStream_t s, Ahead& A,
+                                float4** ck_own) {
+    khp_ctx::AheadSet& ra = c->ra;
+    const bool match = ra.valid && ra.gen == c->gen && ra.npaths == npaths && ahead_key_equal(ra.next, *p);
+    ra.valid = false;
+    const size_t lanes = (size_t)c->grid_path * TRAV_BLOCK;   // a lane parks at most one path
+    HIPCHK(ra.st.ensure(sizeof(AheadState)));
+    for (int q = 0; q < 2; ++q) {
+        HIPCHK(ra.ck[q].ensure(npaths * sizeof(float4)));
+        HIPCHK(ra.park[q].ensure(lanes * PARK_F4 * sizeof(float4)));
+    }
+    AheadState* st = ra.st.as<AheadState>();
+    if (!match) {
+        hipLaunchKernelGGL(k_ahead_reset, dim3(1), dim3(256), 0, s, st, 0, 1);
+        ra.own = 0;
+    }
+    const int own = ra.own, ah = own ^ 1;
+    hipLaunchKernelGGL(k_ahead_reset, dim3(1), dim3(256), 0, s, st, ah, 0);
+    if (!ra.hst) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&ra.hst), 2 * sizeof(uint32_t), hipHostMallocDefault));
+    HIPCHK(hipMemcpyAsync(&ra.hst[0], &st->done[own][0], sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&ra.hst[1], &st->park_n[own][0], sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    ra.counted = true;
+    A = Ahead{};
+    A.on = 1u;
+    A.npaths = (uint32_t)npaths;
+    A.s_off = p->spp;
+    A.park_n_own = &st->park_n[own][0];
+    A.ck = ra.ck[ah].as<float4>();
+    A.fetch_own = st->fetch[own];
+    A.fetch_ahead = st->fetch[ah];
+    A.done_own = &st->done[own][0];
+    A.done_ahead = &st->done[ah][0];
+    A.park_n_ahead = &st->park_n[ah][0];
+    A.take_own = &st->take[own][0];
+    A.park_own = ra.park[own].as<float4>();
+    A.park_ahead = ra.park[ah].as<float4>();
+    *ck_own = ra.ck[own].as<float4>();
+    return KHP_OK;
+}
+static void ahead_commit(khp_ctx* c, const khp_render_params* p, size_t npaths) {
+    khp_ctx::AheadSet& ra = c->ra;
+    ra.valid = true;
+    ra.own ^= 1;
+    ra.next = *p;
+    ra.next.first_sample = p->first_sample + p->spp;
+    ra.gen = c->gen;
+    ra.npaths = npaths;
+}
+
 static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* out_rgb,
                                  const std::vector<PendingOp>* ops) {
     khp_status s;
@@ -3548,6 +3790,11 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     }
     bool acc_waited = false;
     Wave Wv = wave_view(c, w);
+    // render-ahead (khp_ctx_params.render_ahead): synchronous path-kernel calls of one chunk
+    const bool ahead = use_path && !async && !ops && nf == 1 && c->prm.render_ahead != 0 && P_all > 0 &&
+                       P_chunk >= P_all && S_chunk >= p->spp && call_paths < ((size_t)1 << 31);
+    Ahead AH{};
+    if (ahead) KHPCHK(ahead_prepare(c, p, call_paths, sA, AH, &Wv.CK));
     Wv.pix = c->pix.as<uint32_t>();
     Wv.W = p->width;
     Wv.H = p->height;
@@ -3595,7 +3842,10 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 HIPCHK(hipMemsetAsync(reinterpret_cast<char*>(Wv.cnt) + offsetof(Counters, fetch_ext), 0,
                                       sizeof(Counters::fetch_ext), sA));
                 timed(c, f, 3, true, sA);
-                launch_path(c->S.textured != 0, path_wide, (c->bsdf_kinds & ~KINDS_FUR) == 0u, grid_path, sA, c->S, Wv, sp_path, PL);
+                launch_path(c->S.textured != 0, path_wide, (c->bsdf_kinds & ~KINDS_FUR) == 0u, grid_path, sA, c->S, Wv,
+                            sp_path, PL, AH);
+                HIPCHK(hipGetLastError());
+                if (ahead) ahead_commit(c, p, call_paths);
                 timed(c, f, 3, false, sA);
             }
             timed(c, f, 3, true, sA);
@@ -3832,6 +4082,11 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     s = harvest(c, slot);
     if (s != KHP_OK) return s;
     KHPCHK(wait_stream(c, c->stream, "a synchronous frame"));
+    if (c->ra.counted) {
+        c->st.ahead_finished = c->ra.hst[0];
+        c->st.ahead_resumed = c->ra.hst[1];
+        c->ra.counted = false;
+    }
     c->report_open = false;
     return KHP_OK;
 }

@@ -110,7 +110,8 @@ class Stats(ctypes.Structure):
                 ("flatten_ms", c_double), ("bvh_ms", c_double), ("bvh_kernel_ms", c_double), ("layout_ms", c_double),
                 ("flatten_kernel_ms", c_double), ("layout_kernel_ms", c_double),
                 ("extend_pruned_pops", c_uint64), ("shadow_pruned_pops", c_uint64), ("frames", c_uint64),
-                ("extend_busy_ms", c_double), ("shadow_finish_ms", c_double), ("shadow_launches", c_uint64)]
+                ("extend_busy_ms", c_double), ("shadow_finish_ms", c_double), ("shadow_launches", c_uint64),
+                ("ahead_finished", c_uint64), ("ahead_resumed", c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if not isinstance(getattr(self, k), (int, float)) else getattr(self, k))
@@ -118,14 +119,14 @@ class Stats(ctypes.Structure):
 
 
 class CtxParams(ctypes.Structure):
-    """khp_ctx_params (ABI 12 layout, 56 bytes; path_order since ABI 9, wide_from since
-    ABI 10, path_kernel since ABI 11, ray_sort_from and lds_nodes since ABI 12): scheduling knobs of a
-    context; no value changes any result."""
+    """khp_ctx_params (ABI 13 layout, 64 bytes; path_order since ABI 9, wide_from since
+    ABI 10, path_kernel since ABI 11, ray_sort_from and lds_nodes since ABI 12, render_ahead since
+    ABI 13): scheduling knobs of a context; no value changes any result."""
     _fields_ = [("fuse_frames", c_uint32), ("frames_in_flight", c_uint32), ("chunk_paths", c_uint64),
                 ("heavy_iters", c_uint32), ("dump_bounce", c_int32), ("trace_kernels", c_uint32),
                 ("shade_order", c_uint32), ("serial_stages", c_uint32), ("path_order", c_uint32),
                 ("wide_from", c_uint32), ("path_kernel", c_uint32), ("ray_sort_from", c_uint32),
-                ("lds_nodes", c_uint32)]
+                ("lds_nodes", c_uint32), ("render_ahead", c_uint32), ("reserved0", c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -169,10 +170,10 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params", "khp_debug_shadow_queue",
             "khp_bdpt_params_defaults", "khp_set_bdpt", "khp_get_bdpt", "khp_gather_plan",
             "khp_read_rgba8_async", "khp_snapshot_wait", "khp_comm_init_local", "khp_comm_set_timeout",
-            "khp_tonemap_log_sum"]
+            "khp_tonemap_log_sum", "khp_set_camera"]
 
 # the include/kirk_hip.h this module mirrors (load_library refuses another)
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _lib = None
 
@@ -213,6 +214,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_get_params": (c_int, [c_void_p, P(CtxParams)]),
         "khp_bdpt_params_defaults": (None, [P(BdptParams)]),
         "khp_set_bdpt": (c_int, [c_void_p, P(BdptParams)]),
+        "khp_set_camera": (c_int, [c_void_p, P(Camera)]),
         "khp_get_bdpt": (c_int, [c_void_p, P(BdptParams)]),
         "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
         "khp_read_rgba8": (c_int, [c_void_p, P(Tonemap), P(c_uint8)]),

@@ -171,7 +171,7 @@ class HipContext:
     def set_params(self, **kw) -> dict:
         """khp_set_params with the given fields changed (fuse_frames, frames_in_flight,
         chunk_paths, heavy_iters, dump_bounce, trace_kernels, shade_order, serial_stages,
-        path_order, wide_from, path_kernel, ray_sort_from, lds_nodes); returns the previous values."""
+        path_order, wide_from, path_kernel, ray_sort_from, lds_nodes, render_ahead); returns the previous values."""
         prm = N.CtxParams()
         N.check(self.lib, self.lib.khp_get_params(self.ptr, ctypes.byref(prm)), "khp_get_params")
         old = prm.as_dict()
@@ -181,6 +181,11 @@ class HipContext:
             setattr(prm, k, int(v))
         N.check(self.lib, self.lib.khp_set_params(self.ptr, ctypes.byref(prm)), "khp_set_params")
         return old
+
+    def set_camera(self, camera: "N.Camera"):
+        """khp_set_camera (ABI 13): a new camera for the next render, nothing rebuilt
+        (KIRK's GUI moving the Camera between PathTracer::render calls)."""
+        N.check(self.lib, self.lib.khp_set_camera(self.ptr, ctypes.byref(camera)), "khp_set_camera")
 
     def set_bdpt(self, **kw) -> dict:
         """khp_set_bdpt with the given khp_bdpt_params fields changed (enabled,

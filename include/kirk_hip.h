@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KHP_ABI_VERSION 12
+#define KHP_ABI_VERSION 13
 
 typedef struct khp_ctx khp_ctx;
 
@@ -256,6 +256,10 @@ typedef struct {
      * any-hit (k_shadow) launches */
     double shadow_finish_ms;
     uint64_t shadow_launches;
+    /* ABI 13: render-ahead (khp_ctx_params.render_ahead), last synchronous render:
+     * its paths the previous call had already finished, and those it resumed from
+     * that call's park records (0 when the call had nothing rendered ahead) */
+    uint64_t ahead_finished, ahead_resumed;
 } khp_stats;
 #define KHP_MAX_BOUNCE_STATS 16
 
@@ -324,7 +328,18 @@ typedef struct {
                                     staged in each traversal wave's LDS beside its stack rings (the 64-B
                                     loops of k_extend and k_shadow), the rest fetched from HBM as before.
                                     Same walk, same counts, same frames.  Measured in DESIGN.md §4    */
-} khp_ctx_params;   /* 56 bytes */
+    uint32_t render_ahead;       /* ABI 13: 1 (default) or 0.  A synchronous render that runs the path kernel
+                                    in one chunk lets the lanes that would idle in its launch's drain (its
+                                    longest paths finishing alone) start the paths of the NEXT call of a
+                                    progressive series -- the same pixels, spp, depth and seed, first_sample +
+                                    spp: KIRK's PathTracer::render loop, CPU_PathTracer.cpp:17-52.  The call
+                                    still returns as soon as its own paths end; the next matching call resumes
+                                    the paths parked at that moment and accumulates the colours already
+                                    finished.  Any other call, and any change of scene, camera or parameters,
+                                    drops that work.  Frames, textures and framebuffers are those of each call
+                                    alone, bit for bit.  Measured in DESIGN.md §5b                          */
+    uint32_t reserved0;          /* 0 */
+} khp_ctx_params;   /* 64 bytes */
 
 /* ---- context --------------------------------------------------------------- */
 /* device: HIP device ordinal (one process per GPU). */
@@ -577,6 +592,12 @@ int khp_shader_kind_from_name(const char* name);
 khp_status khp_camera_setup(const float position[3], const float look_at[3], const float up[3],
                             float sensor_w, float sensor_h, float focal_length,
                             uint32_t width, uint32_t height, khp_camera* out);
+
+/* ABI 13: replaces the scene's camera without rebuilding anything (KIRK's GUI
+ * moves the Camera between PathTracer::render calls and restarts the pass
+ * count, CPU_PathTracer.cpp:17-24).  Completes in-flight frames first; the
+ * next render uses the new camera.  Drops render-ahead work. */
+khp_status khp_set_camera(khp_ctx* ctx, const khp_camera* camera);
 
 /* Fur fibers -> cone frusta exactly as CPU_Scene::flattenNode does with
  * m_fiberAsCylinder (CPU_Scene.cpp:121-144): base pulled back by 0.8 % of the

@@ -1,0 +1,17 @@
+#!/bin/bash
+# round-6 GPU steps (usage on the box: bash tools/gpu_r06.sh <step> [tag])
+set -o pipefail
+T=${2:-r06}
+mkdir -p gpurun_out/$T
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
+case "$1" in
+ra)   # render-ahead: its tests, the path-kernel parity tests, then the synchronous-call timings
+  KHP_NO_BUILD=1 timeout -k 10 500 $PYT tests/test_render_ahead.py > gpurun_out/$T/tests_ra.log 2>&1 || exit 1
+  KHP_NO_BUILD=1 timeout -k 10 400 $PYT tests/test_gpu_parity.py -k "path_kernel or edge_sizes or quirk or progressive or tiny or pathtracer_api" > gpurun_out/$T/tests_pk.log 2>&1 || exit 1
+  timeout -k 10 300 python -u tools/sync_calls.py 8 > gpurun_out/$T/sync_calls.jsonl 2> gpurun_out/$T/sync_calls.log || exit 1
+  ;;
+sync)  # synchronous-call timings only ($3: extra env, e.g. KHP_LIB=variants/libkirk_x.so)
+  env $3 timeout -k 10 300 python -u tools/sync_calls.py 8 >> gpurun_out/$T/sync_calls.jsonl 2>> gpurun_out/$T/sync_calls.log || exit 1
+  ;;
+*) echo "unknown step $1"; exit 2 ;;
+esac

@@ -1,6 +1,7 @@
 """Synchronous-call timing at the metric row (dev tool, GPU box): KIRK's GUI call
 (1-spp khp_render + 8-bit texture) and the 8-spp synchronous pass through the
-path kernel (path_kernel 2) and the automatic choice (0), with the library in
+path kernel (path_kernel 2) and the automatic choice (0), with render-ahead on
+(the default) and off, with the library in
 KHP_LIB (tools/build_variant.sh) or the in-tree one.  Prints one JSON line of
 median wall ms per call and the Msamples/s they give.
 usage: [KHP_LIB=variants/libkirk_x.so] python tools/sync_calls.py [calls=8]"""
@@ -21,8 +22,10 @@ scenes.config3_device(ctx, W, H, n_strands=1_000_000)
 ctx.build_accel()
 out = {"lib": os.path.basename(os.environ.get("KHP_LIB", "in-tree"))}
 k = 0
-for name, spp, pk, tex in (("gui", 1, 0, True), ("sync8_pk2", 8, 2, False), ("sync8_auto", 8, 0, False)):
-    ctx.set_params(path_kernel=pk)
+CASES = (("gui", 1, 0, True, 1), ("gui_ra0", 1, 0, True, 0), ("sync8_pk2", 8, 2, False, 1),
+         ("sync8_pk2_ra0", 8, 2, False, 0), ("sync8_auto", 8, 0, False, 1))
+for name, spp, pk, tex, ra in CASES:
+    ctx.set_params(path_kernel=pk, render_ahead=ra)
     ms = []
     for it in range(N + 2):
         t0 = time.perf_counter()
