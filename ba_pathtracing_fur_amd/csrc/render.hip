@@ -813,6 +813,12 @@ __device__ __forceinline__ bool bd_connection(const DevScene& S, const BdptDev& 
 // (the regrouped ray columns and the state indirection).
 constexpr uint32_t RS_LOG = 5;   // cells per axis = 2^RS_LOG (16^3 cells measured the same)
 constexpr uint32_t RS_CELLS = 1u << (3 * RS_LOG);
+// k_rsort_count / k_rsort_scatter privatise the cell histogram in LDS: 2^15 cells
+// are 128 KiB, which only gfx950's 160 KiB per workgroup holds (64 KiB before it)
+static_assert(RS_CELLS * sizeof(uint32_t) <= 160 * 1024, "ray-sort histogram exceeds gfx950's LDS per workgroup");
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "render.hip is written for gfx950 (MI355X): k_rsort_* need 128 KiB of LDS per workgroup (RS_LOG 4 fits 16 KiB)"
+#endif
 __device__ __forceinline__ uint32_t rs_spread(uint32_t v) {   // 5 bits -> every third bit
     v &= 31u;
     v = (v | (v << 8)) & 0x100Fu;
@@ -1536,66 +1542,84 @@ struct PathLanes {
 // of its longest paths, ~45% of a 1-spp call with most lanes idle (DESIGN.md
 // §5b).  With render-ahead the launch of call k renders the paths of sample
 // set k ("own") and, once every own path is claimed, lets its idle lanes claim
-// the camera paths of the set the NEXT matching call will ask for ("ahead":
-// the same pixels, samples [first_sample + spp, first_sample + 2 spp)).  An
-// ahead path that ends writes its colour to the ahead set's column; the
+// the paths of the sets the NEXT calls of the progressive series will ask for
+// (sets k+1 .. k+D: the same pixels, samples first_sample + j*spp ...), set
+// after set.  A path that ends writes its colour to its set's column; the
 // launch ends as soon as every own path has ended (a counter that the waves
-// poll), and each lane still holding an ahead path parks it: the path state
-// at the start of its current traversal (the 8 PathLanes columns, the ray,
-// the query kind) goes to a park record and the traversal is redone later.
-// Call k+1 resumes the parked paths first, claims its unclaimed paths from
-// the cursors call k advanced, and accumulates the colour column call k
-// filled.  Paths are independent and deterministic functions of (scene,
-// camera, parameters, pixel, sample), so each call's colours -- and its
-// accumulate, texture and framebuffer -- are those of rendering it alone.
-// The host drops the ahead set on any change of scene, camera, parameters,
-// size or first_sample (AheadSet).
-constexpr uint32_t AHEAD_BIT = 0x80000000u;   // PathLanes col[2].w: the path belongs to the ahead set
-constexpr uint32_t PARK_F4 = 10;              // float4 per park record: 8 columns, (o, t_max), (d, any)
-struct alignas(128) AheadState {
-    uint32_t fetch[2][NSEG * 32];   // per set parity: claim cursors (one 128-B line each)
-    uint32_t done[2][32];           // paths of the set that have ended
-    uint32_t park_n[2][32];         // records parked for the set
-    uint32_t take[2][32];           // resume cursor over them
-};
+// without an own path poll), and each lane still holding a path of a later set
+// parks it: the path state at the start of its current traversal (the 8
+// PathLanes columns, the ray, the query kind) is appended to its set's park
+// list and the traversal is redone later.  Every launch takes, set by set, the
+// parked paths first, then the set's unclaimed paths from the cursors earlier
+// launches advanced; call k+1 accumulates the colour column of set k+1.  Paths
+// are independent and deterministic functions of (scene, camera, parameters,
+// pixel, sample), so each call's colours -- and its accumulate, texture and
+// framebuffer -- are those of rendering it alone.  The host drops the sets on
+// any change of scene, camera, parameters, size or first_sample (AheadSet).
+// The sets live in a ring of nsets = D + 1 slots; a path carries its set
+// relative to the launch's own set (0 own, 1 next, ...) in the top bits of its
+// PathLanes id.
+constexpr uint32_t RA_MAX_SETS = 4;
+constexpr uint32_t SET_SHIFT = 30;               // PathLanes col[2].w: bits 30-31 = relative set
+constexpr uint32_t PID_MASK = (1u << SET_SHIFT) - 1u;
+constexpr uint32_t PARK_F4 = 10;                 // float4 per park record: 8 columns, (o, t_max), (d, any)
+struct AheadState;
 struct Ahead {
-    uint32_t on;           // 0: a plain synchronous launch (the fields below unused)
-    uint32_t npaths;       // paths per set (= the launch's own paths)
-    uint32_t s_off;        // ahead camera paths: sample offset from the own set's
-    const uint32_t* park_n_own;   // records parked for the own set by the previous launch
-    float4* ck;            // the ahead set's colour column (Wave::CK is the own set's)
-    uint32_t* fetch_own;   // the own set's claim cursors (advanced by the previous launch's ahead claims)
-    uint32_t* fetch_ahead; // the ahead set's (zero at launch)
-    uint32_t* done_own;
-    uint32_t* done_ahead;
-    uint32_t* park_n_ahead;
-    uint32_t* take_own;
-    const float4* park_own;  // the previous launch's park records (own set)
-    float4* park_ahead;      // this launch's park records
+    uint32_t on;         // 0: a plain synchronous launch (the fields below unused)
+    uint32_t npaths;     // paths per set (= the launch's own paths)
+    uint32_t spp;        // set j's camera paths: sample offset j * spp from the own set's
+    uint32_t own;        // ring slot of the own set
+    uint32_t nsets;      // sets in flight: the own set and nsets - 1 later ones (2 .. RA_MAX_SETS)
+    uint32_t park_cap;   // park records per ring slot
+    AheadState* st;
+    float4* ck;          // [ring slot][npaths] colour columns (Wave::CK = the own slot's)
+    float4* park;        // [ring slot][park_cap][PARK_F4] park lists
 };
-// Ends a path: its colour to its set's column; 1 for an own path, 2 for an ahead path.
+struct alignas(128) AheadState {
+    uint32_t fetch[RA_MAX_SETS][NSEG * 32];   // per ring slot: claim cursors (one 128-B line each)
+    uint32_t done[RA_MAX_SETS][32];           // paths of the set that have ended
+    uint32_t park_n[RA_MAX_SETS][32];         // records appended to the set's park list
+    uint32_t park_lim[RA_MAX_SETS][32];       // park_n when the launch was enqueued: the records it may resume
+    uint32_t take[RA_MAX_SETS][32];           // resume cursor over the list
+    uint32_t report[32];                      // at enqueue: the own set's finished paths, its resumable records
+};
+__device__ __forceinline__ uint32_t ra_slot(const Ahead& A, uint32_t j) {
+    const uint32_t s = A.own + j;
+    return s >= A.nsets ? s - A.nsets : s;
+}
+// Ends a path: its colour to its set's column; returns 1 + its relative set.
+template <bool RA>
 __device__ __forceinline__ uint32_t end_path(const Wave& Wv, const Ahead& A, uint32_t pw, float4 cko) {
-    if (pw & AHEAD_BIT) {
-        A.ck[pw & ~AHEAD_BIT] = cko;
-        return 2u;
+    const uint32_t j = RA ? pw >> SET_SHIFT : 0u;
+    if (RA && j != 0u) {
+        A.ck[(size_t)ra_slot(A, j) * A.npaths + (pw & PID_MASK)] = cko;
+        return 1u + j;
     }
-    Wv.CK[pw] = cko;
+    Wv.CK[pw & PID_MASK] = cko;
     return 1u;
 }
 // Every own path of the launch has ended (render-ahead; wave-uniform).
 __device__ __forceinline__ bool own_set_done(const Ahead& A) {
-    const uint32_t d = __hip_atomic_load(A.done_own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t d = __hip_atomic_load(&A.st->done[A.own][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return __builtin_amdgcn_readfirstlane(d) >= A.npaths;
 }
-__global__ void k_ahead_reset(AheadState* a, int q, int both) {
-    for (int p = 0; p < 2; ++p) {
-        if (p != q && !both) continue;
+// Before a render-ahead launch: clears the ring slots in `clear` (bit mask), then
+// fixes every slot's resume limit and the own slot's report.
+__global__ void k_ahead_prep(AheadState* a, uint32_t clear, uint32_t own) {
+    for (uint32_t p = 0; p < RA_MAX_SETS; ++p) {
+        if (!(clear >> p & 1u)) continue;
         for (uint32_t i = threadIdx.x; i < NSEG * 32; i += blockDim.x) a->fetch[p][i] = 0;
         if (threadIdx.x == 0) {
             a->done[p][0] = 0;
             a->park_n[p][0] = 0;
             a->take[p][0] = 0;
         }
+    }
+    __syncthreads();
+    if (threadIdx.x < RA_MAX_SETS) a->park_lim[threadIdx.x][0] = a->park_n[threadIdx.x][0];
+    if (threadIdx.x == 0) {
+        a->report[0] = a->done[own][0];
+        a->report[1] = a->park_n[own][0] > a->take[own][0] ? a->park_n[own][0] - a->take[own][0] : 0u;
     }
 }
 
@@ -1767,18 +1791,41 @@ enum : uint32_t { PS_TRAV = 0u, PS_FIN = 1u, PS_NEW = 2u, PS_BEGIN = 3u, PS_DONE
 #define KHP_WPROF_MAX 65536
 __device__ unsigned long long g_wprof[6 * KHP_WPROF_MAX];
 __device__ uint32_t g_wprof_n;
+// render-ahead: the clock when the last own path ended, ~ when the first wave saw the own set's end
+__device__ unsigned long long g_ra_prof[2];
 #endif
 
-template <bool TEX, bool WIDE, uint32_t KINDS>
+// Render-ahead tuning: a wave adds its ended paths to the set counters in batches
+// of KHP_RA_BATCH (at once for own paths once the own set is all claimed: the end
+// of the set is looked for only then).
+#ifndef KHP_RA_BATCH
+#define KHP_RA_BATCH 1024
+#endif
+#ifndef KHP_RA_MIX   // measured slower: off
+#define KHP_RA_MIX 0
+#endif
+#ifndef KHP_RA_MIX_REFILL
+#define KHP_RA_MIX_REFILL 48
+#endif
+#ifndef KHP_RA_NO_AHEAD   // diagnostic builds: the render-ahead instance with nothing claimed ahead
+#define KHP_RA_NO_AHEAD 0
+#endif
+template <bool TEX, bool WIDE, uint32_t KINDS, bool RA>
 __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wave Wv, SpillArea spill, PathLanes L, Ahead A) {
     extern __shared__ uint32_t lds[];
     const uint32_t npaths = Wv.P * Wv.n_samples * Wv.n_frames;
     const uint32_t g = blockIdx.x * TRAV_BLOCK + threadIdx.x;
-    if (A.on && own_set_done(A)) return;   // render-ahead: the previous launch finished this whole set
-    // render-ahead (wave-uniform): parked own paths may remain / the ahead set has unclaimed paths
-    const uint32_t park_n_own = A.on ? __builtin_amdgcn_readfirstlane(*A.park_n_own) : 0u;
-    bool res_left = park_n_own > 0u, ahead_left = A.on != 0u, stop = false;
-    uint32_t poll_it = 0;
+    if (RA && own_set_done(A)) return;   // render-ahead: earlier launches finished this whole set
+    // render-ahead (wave-uniform): the set the wave claims from (relative: 0 own, 1 the next
+    // call's, ...), its resume limit and whether parked records may remain; ended paths per
+    // set not yet counted; the lanes holding an own path (only a wave without one looks for
+    // the end of the own set: the look is a coherent load, and the waves carrying the call's
+    // last paths never wait for it)
+    const uint32_t nsets = RA ? (KHP_RA_NO_AHEAD ? 1u : A.nsets) : 1u;
+    uint32_t cur = 0u, lim = RA ? __builtin_amdgcn_readfirstlane(A.st->park_lim[A.own][0]) : 0u;
+    bool res_left = lim > 0u, stop = false;
+    uint32_t pend[RA_MAX_SETS] = {0u, 0u, 0u, 0u}, poll_it = 0u;
+    unsigned long long own_lanes = 0ull;
     LdsStack<PATH_RING, false> stk;
     stk.init(lds, spill.base, spill.stride);
     TravStats st{0, 0, 0};
@@ -1791,9 +1838,8 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     uint32_t mode = 0u, state = PS_NEW, n_ext = 0, n_sh = 0;
     bool any = false, occ = false, exhausted = false;
     float tmax_any = 0.0f;
-    Claimer cl, cl2;   // own set, ahead set (render-ahead)
-    cl.init(A.on ? A.fetch_own : Wv.cnt->fetch_ext, npaths, 0u, npaths);
-    cl2.init(A.on ? A.fetch_ahead : Wv.cnt->fetch_ext, npaths, 0u, npaths);
+    Claimer cl;   // the claims of set `cur` (render-ahead), of the launch's paths otherwise
+    cl.init(RA ? A.st->fetch[A.own] : Wv.cnt->fetch_ext, npaths, 0u, npaths);
 #ifdef KHP_PATH_PROFILE   // diagnostic builds: launch timeline (100 MHz wall clock): first start, last
     // claim exhaustion seen, last end, longest drain of one wave (its end - its exhaustion)
     const unsigned long long pc_start = wall_clock64();
@@ -1803,13 +1849,16 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
 #endif
     for (;;) {
 #ifdef KHP_PATH_PROFILE
-        if (exhausted && pc_exh == 0) {
+        if ((RA ? cur > 0u : exhausted) && pc_exh == 0) {
             pc_exh = wall_clock64();
             pw_ntrav_exh = (uint32_t)__popcll(__ballot(state == PS_TRAV || state == PS_FIN || state == PS_BEGIN));
         }
 #endif
-        // render-ahead: once every own path has ended, park the ahead paths (below) and leave
-        if (stop || (A.on && exhausted && !res_left && own_set_done(A))) {
+        // render-ahead: once every own path has ended, park the later sets' paths (below) and leave
+        if (RA && (stop || (cur > 0u && own_lanes == 0ull && own_set_done(A)))) {
+#ifdef KHP_PATH_PROFILE
+            if (lane_id() == 0) atomicMin(&g_ra_prof[1], wall_clock64());
+#endif
             stop = true;
             break;
         }
@@ -1819,7 +1868,8 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
             Ray sray;          // the ray a lane starts next (PS_BEGIN)
             bool sany = false;
             float stmax = 0.0f;
-            uint32_t ended = 0u;   // 1: an own path ended here, 2: an ahead path (render-ahead)
+            uint32_t ended = 0u;   // render-ahead: 1 + the relative set of a path that ended here
+            bool st_own = false;   // render-ahead: an own path started here
             sray.o = sray.d = mk(0, 0, 0);
             if (state == PS_FIN) {
                 const Ray fr = tr.r;
@@ -1853,7 +1903,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                         sray = o.nr;
                         state = PS_BEGIN;
                     } else {
-                        ended = end_path(Wv, A, bits_from_f(f2.w), cko);
+                        ended = end_path<RA>(Wv, A, bits_from_f(f2.w), cko);
                         state = PS_NEW;
                     }
                 } else {  // k_shadow_finish
@@ -1871,69 +1921,79 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                         sray.d = mk(f3.x, f3.y, f3.z);
                         state = PS_BEGIN;
                     } else {
-                        ended = end_path(Wv, A, bits_from_f(f2.w), cko);
+                        ended = end_path<RA>(Wv, A, bits_from_f(f2.w), cko);
                         state = PS_NEW;
                     }
                 }
             }
-            if (A.on) {   // render-ahead: ended paths per set
-                const unsigned long long eo = __ballot(ended == 1u), ea = __ballot(ended == 2u);
-                if (lane_id() == 0) {
-                    if (eo) atomicAdd(A.done_own, (uint32_t)__popcll(eo));
-                    if (ea) atomicAdd(A.done_ahead, (uint32_t)__popcll(ea));
-                }
+            if (RA) {   // render-ahead: ended paths per set
+                const unsigned long long eom = __ballot(ended == 1u);
+                pend[0] += (uint32_t)__popcll(eom);
+                for (uint32_t j = 1; j < RA_MAX_SETS; ++j) pend[j] += (uint32_t)__popcll(__ballot(ended == 1u + j));
+                own_lanes &= ~eom;
+#ifdef KHP_PATH_PROFILE
+                if (eom && lane_id() == 0) atomicMax(&g_ra_prof[0], wall_clock64());
+#endif
             }
-            const unsigned long long want = __ballot(state == PS_NEW);
-            if (want != 0ull) {  // wave-uniform: claim camera paths for the lanes whose path ended
-                if (res_left) {   // render-ahead: this set's paths parked by the previous launch first
-                    const uint32_t slot = wave_alloc(state == PS_NEW, A.take_own);
-                    if (__ballot(state == PS_NEW && slot >= park_n_own) != 0ull) res_left = false;
-                    if (state == PS_NEW && slot < park_n_own) {
-                        const float4* r = A.park_own + (size_t)slot * PARK_F4;
-#pragma unroll 1
-                        for (int k = 0; k < 8; ++k) {   // one record at a time (registers)
-                            float4 v = r[k];
-                            if (k == 2) v.w = f_from_bits(bits_from_f(v.w) & ~AHEAD_BIT);   // now an own path
-                            L.col[k][g] = v;
-                        }
-                        const float4 ro = r[8], rd = r[9];
-                        sray.o = mk(ro.x, ro.y, ro.z);
-                        sray.d = mk(rd.x, rd.y, rd.z);
-                        stmax = ro.w;
-                        sany = bits_from_f(rd.w) != 0u;
-                        state = PS_BEGIN;
-                    }
-                }
-                // a camera path: the next of this call's set, or (render-ahead, once
-                // they are all claimed) of the next call's set
-                bool cam = false;
+            unsigned long long want = __ballot(state == PS_NEW);
+            if (want != 0ull) {  // wave-uniform: claim paths for the lanes whose path ended
+                bool cam = false;   // a camera path starts: path cpid (with its relative set), sample offset coff
                 uint32_t cpid = 0, coff = 0;
-                const unsigned long long want1 = __ballot(state == PS_NEW);
-                if (want1 != 0ull && !exhausted) {
+                if constexpr (RA) {
+                    // set after set (own first): its parked paths, then its unclaimed ones
+                    while (want != 0ull && cur < nsets) {
+                        const uint32_t sl = ra_slot(A, cur);
+                        if (res_left) {
+                            const uint32_t slot = wave_alloc(state == PS_NEW && !cam, &A.st->take[sl][0]);
+                            if (__ballot(state == PS_NEW && !cam && slot >= lim) != 0ull) res_left = false;
+                            if (state == PS_NEW && !cam && slot < lim) {
+                                const float4* r = A.park + ((size_t)sl * A.park_cap + slot) * PARK_F4;
+#pragma unroll 1
+                                for (int k = 0; k < 8; ++k) {   // one record at a time (registers)
+                                    float4 v = r[k];
+                                    if (k == 2) v.w = f_from_bits((bits_from_f(v.w) & PID_MASK) | (cur << SET_SHIFT));
+                                    L.col[k][g] = v;
+                                }
+                                const float4 ro = r[8], rd = r[9];
+                                sray.o = mk(ro.x, ro.y, ro.z);
+                                sray.d = mk(rd.x, rd.y, rd.z);
+                                stmax = ro.w;
+                                sany = bits_from_f(rd.w) != 0u;
+                                state = PS_BEGIN;
+                                st_own = cur == 0u;
+                            }
+                        } else if (!exhausted) {
+                            uint32_t my = 0, pid = 0;
+                            const bool got = cl.claim(want, my, exhausted);
+                            if (state == PS_NEW && !cam && got && cl.phys(my, pid)) {
+                                cam = true;
+                                cpid = pid | (cur << SET_SHIFT);
+                                coff = cur * A.spp;
+                                st_own = cur == 0u;
+                            }
+                        } else if (++cur < nsets) {   // the next set: its cursors and park list
+                            const uint32_t s2 = ra_slot(A, cur);
+                            cl.init(A.st->fetch[s2], npaths, 0u, npaths);
+                            exhausted = false;
+                            lim = __builtin_amdgcn_readfirstlane(A.st->park_lim[s2][0]);
+                            res_left = lim > 0u;
+                        }
+                        want = __ballot(state == PS_NEW && !cam);
+                    }
+                    own_lanes |= __ballot(st_own);
+                    if (state == PS_NEW && cur >= nsets) state = PS_DONE;
+                } else {
                     uint32_t my = 0, pid = 0;
-                    const bool got = cl.claim(want1, my, exhausted);
+                    bool got = false;
+                    if (!exhausted) got = cl.claim(want, my, exhausted);
                     if (state == PS_NEW && got && cl.phys(my, pid)) {
                         cam = true;
                         cpid = pid;
                     }
                 }
-                if (ahead_left && exhausted && !res_left) {
-                    const unsigned long long want2 = __ballot(state == PS_NEW && !cam);
-                    if (want2 != 0ull) {
-                        uint32_t my2 = 0, pid2 = 0;
-                        bool gone = false;
-                        const bool got2 = cl2.claim(want2, my2, gone);
-                        if (gone) ahead_left = false;
-                        if (state == PS_NEW && !cam && got2 && cl2.phys(my2, pid2)) {
-                            cam = true;
-                            cpid = pid2 | AHEAD_BIT;
-                            coff = A.s_off;
-                        }
-                    }
-                }
                 if (cam) {
                     uint32_t key;
-                    sray = camera_path(S, Wv, cpid & ~AHEAD_BIT, key, coff);
+                    sray = camera_path(S, Wv, cpid & PID_MASK, key, coff);
                     L.col[0][g] = make_float4(1.0f, 1.0f, 1.0f, f_from_bits(0u));
                     L.col[1][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(key));
                     L.col[2][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(cpid));
@@ -1941,7 +2001,19 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                     sany = false;
                     state = PS_BEGIN;
                 }
-                if (state == PS_NEW && exhausted && !res_left && !ahead_left) state = PS_DONE;
+                if (!RA && state == PS_NEW && exhausted) state = PS_DONE;
+            }
+            if (RA) {   // render-ahead: add the ended paths to their sets' counters
+                if (pend[0] != 0u && (cur > 0u || pend[0] >= KHP_RA_BATCH)) {
+                    if (lane_id() == 0) atomicAdd(&A.st->done[A.own][0], pend[0]);
+                    pend[0] = 0u;
+                }
+                for (uint32_t j = 1; j < RA_MAX_SETS; ++j) {
+                    if (pend[j] >= KHP_RA_BATCH) {
+                        if (lane_id() == 0) atomicAdd(&A.st->done[ra_slot(A, j)][0], pend[j]);
+                        pend[j] = 0u;
+                    }
+                }
             }
             if (state == PS_BEGIN) {  // k_extend's / k_shadow's ray start
                 TravRay t2;
@@ -1995,26 +2067,41 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
             // refill at REFILL finished lanes; once every path is claimed, as soon as
             // the finished lanes are as many as those still traversing (the drain;
             // servicing at every finished lane there measured 5% slower)
-            const bool nomore = exhausted && !res_left && !ahead_left;
-            const uint32_t thr = nomore ? (ntrav < PATH_REFILL ? (ntrav > 0u ? ntrav : 1u) : PATH_REFILL)
-                                        : PATH_REFILL;
+            const bool nomore = RA ? cur >= nsets : exhausted;
+            uint32_t thr = nomore ? (ntrav < PATH_REFILL ? (ntrav > 0u ? ntrav : 1u) : PATH_REFILL) : PATH_REFILL;
+            if (RA && KHP_RA_MIX && cur > 0u && own_lanes != 0ull) {
+                // render-ahead, a wave carrying own paths beside later sets' ones once the own set is
+                // claimed: an own path that finished its traversal is shaded at once (the call waits
+                // for it), the others wait for KHP_RA_MIX_REFILL finished lanes
+                if (__ballot(state == PS_FIN) & own_lanes) break;
+                thr = nomore ? thr : KHP_RA_MIX_REFILL;
+            }
             if (ntrav == 0u || nfin >= thr) break;
-            // render-ahead: a wave busy with ahead paths looks for the end of the own set
-            if (A.on && exhausted && !res_left && (++poll_it & 31u) == 0u && own_set_done(A)) {
+            // render-ahead: a wave busy with later sets' paths looks for the end of the own set
+            // every 32 iterations too (its lanes may not finish a traversal for long)
+            if (RA && cur > 0u && own_lanes == 0ull && (++poll_it & 31u) == 0u && own_set_done(A)) {
                 stop = true;
                 break;
             }
         }
     }
-    if (stop) {   // render-ahead: the state at the start of each ahead path's current traversal, which is redone
-        bool ah = false;
-        if (state == PS_TRAV || state == PS_FIN) ah = (bits_from_f(L.col[2][g].w) & AHEAD_BIT) != 0u;
-        const uint32_t slot = wave_alloc(ah, A.park_n_ahead);
-        if (ah) {
-            float4* r = A.park_ahead + (size_t)slot * PARK_F4;
-            for (int k = 0; k < 8; ++k) r[k] = L.col[k][g];
-            r[8] = make_float4(tr.r.o.x, tr.r.o.y, tr.r.o.z, tmax_any);
-            r[9] = make_float4(tr.r.d.x, tr.r.d.y, tr.r.d.z, f_from_bits(any ? 1u : 0u));
+    if (RA) {   // render-ahead: the counts not yet added
+        for (uint32_t j = 0; j < RA_MAX_SETS; ++j)
+            if (pend[j] != 0u && lane_id() == 0) atomicAdd(&A.st->done[ra_slot(A, j)][0], pend[j]);
+    }
+    if (RA && stop) {   // render-ahead: later sets' paths are appended to their park lists, each as
+                        // its state at the start of its current traversal, which is redone
+        uint32_t j = 0u;
+        if (state == PS_TRAV || state == PS_FIN) j = bits_from_f(L.col[2][g].w) >> SET_SHIFT;
+        for (uint32_t q = 1; q < nsets; ++q) {
+            const uint32_t sl = ra_slot(A, q);
+            const uint32_t slot = wave_alloc(j == q, &A.st->park_n[sl][0]);
+            if (j == q && slot < A.park_cap) {   // (park_cap holds every lane of nsets - 1 launches)
+                float4* r = A.park + ((size_t)sl * A.park_cap + slot) * PARK_F4;
+                for (int k = 0; k < 8; ++k) r[k] = L.col[k][g];
+                r[8] = make_float4(tr.r.o.x, tr.r.o.y, tr.r.o.z, tmax_any);
+                r[9] = make_float4(tr.r.d.x, tr.r.d.y, tr.r.d.z, f_from_bits(any ? 1u : 0u));
+            }
         }
     }
     const unsigned long long se = wave_sum((unsigned long long)n_ext), ss = wave_sum((unsigned long long)n_sh);
@@ -2051,7 +2138,8 @@ constexpr uint32_t KINDS_FUR = (1u << KHP_BSDF_LAMBERTIAN_REFLECTION) | (1u << K
 template <bool TEX, bool WIDE, uint32_t K>
 static void launch_path_k(int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp, const PathLanes& L,
                           const Ahead& A) {
-    hipLaunchKernelGGL((k_path<TEX, WIDE, K>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L, A);
+    if (A.on) hipLaunchKernelGGL((k_path<TEX, WIDE, K, true>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L, A);
+    else hipLaunchKernelGGL((k_path<TEX, WIDE, K, false>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L, A);
 }
 static void launch_path(bool tex, bool wide, bool fur, int grid, hipStream_t s, const DevScene& S, const Wave& W,
                         SpillArea sp, const PathLanes& L, const Ahead& A) {
@@ -2591,13 +2679,13 @@ struct khp_ctx {
     // synchronous path-kernel call did for the next call of its progressive series
     uint64_t gen = 1;   // bumped by every change of the scene, camera or parameters
     struct AheadSet {
-        DevMem st, ck[2], park[2];   // AheadState; per set parity: colour column, park records
-        bool valid = false;          // the set of parity `own` belongs to the call `next`
-        int own = 0;
+        DevMem st, ck, park;         // AheadState; per ring slot: colour column, park list
+        bool valid = false;          // the ring's slot `own` holds the set of the call `next`
+        uint32_t own = 0, nsets = 0, park_cap = 0;
         khp_render_params next{};
         uint64_t gen = 0;
         size_t npaths = 0;
-        uint32_t* hst = nullptr;     // pinned: the own set's finished / parked counts at the call's start
+        uint32_t* hst = nullptr;     // pinned: AheadState::report of the current call
         bool counted = false;        // hst was filled by the current call
     } ra;
 };
@@ -2772,7 +2860,7 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->path_kernel = 0;       // automatic: k_path for synchronous renders
     out->ray_sort_from = 0;     // automatic: bounces 2.. of large trees, +1.8% on the metric row
     out->lds_nodes = 0;         // the top records in LDS, measured
-    out->render_ahead = 1;      // synchronous path-kernel calls fill their drain with the next call's paths
+    out->render_ahead = 2;      // synchronous path-kernel calls fill their drain with the next 2 calls' paths
 }
 
 extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {
@@ -2794,7 +2882,7 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     if (prm->path_order > 2) return fail(KHP_EINVAL, "path_order must be 0, 1 or 2");
     if (prm->path_kernel > 2) return fail(KHP_EINVAL, "path_kernel must be 0, 1 or 2");
     if (prm->lds_nodes != 0 && prm->lds_nodes != TOP_NODES) return fail(KHP_EINVAL, "lds_nodes must be 0 or 7");
-    if (prm->render_ahead > 1) return fail(KHP_EINVAL, "render_ahead must be 0 or 1");
+    if (prm->render_ahead > RA_MAX_SETS - 1) return fail(KHP_EINVAL, "render_ahead must be 0..3");
     if (prm->reserved0 != 0) return fail(KHP_EINVAL, "reserved0 must be 0");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
@@ -3236,12 +3324,12 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shadow_finish<false>), 256, 0));
     c->grid_fin = std::max(1, nb) * c->n_cu;
     nb = 0;
-    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, false, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
-    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, false, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, false, KINDS_ALL, true>), TRAV_BLOCK, PATH_LDS));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, false, KINDS_ALL, true>), TRAV_BLOCK, PATH_LDS));
     c->grid_path = std::max(1, nb) * c->n_cu;
     nb = 0;
-    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, true, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
-    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, true, KINDS_ALL>), TRAV_BLOCK, PATH_LDS));
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<true, true, KINDS_ALL, true>), TRAV_BLOCK, PATH_LDS));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_path<false, true, KINDS_ALL, true>), TRAV_BLOCK, PATH_LDS));
     c->grid_path_w = std::min(c->grid_path, std::max(1, nb) * c->n_cu);   // the columns are sized by grid_path
     c->built = true;
     ++c->gen;
@@ -3547,46 +3635,48 @@ static bool ahead_key_equal(const khp_render_params& a, const khp_render_params&
 static khp_status ahead_prepare(khp_ctx* c, const khp_render_params* p, size_t npaths, hipStream_t s, Ahead& A,
                                 float4** ck_own) {
     khp_ctx::AheadSet& ra = c->ra;
-    const bool match = ra.valid && ra.gen == c->gen && ra.npaths == npaths && ahead_key_equal(ra.next, *p);
+    const uint32_t nsets = std::min<uint32_t>(c->prm.render_ahead, RA_MAX_SETS - 1) + 1;
+    const bool match = ra.valid && ra.gen == c->gen && ra.npaths == npaths && ra.nsets == nsets &&
+                       ahead_key_equal(ra.next, *p);
     ra.valid = false;
-    const size_t lanes = (size_t)c->grid_path * TRAV_BLOCK;   // a lane parks at most one path
+    // a lane parks at most one path per launch, and a set is parked by the nsets - 1
+    // launches before the one it belongs to
+    const size_t lanes = (size_t)c->grid_path * TRAV_BLOCK;
+    const size_t cap = (nsets - 1) * lanes;
     HIPCHK(ra.st.ensure(sizeof(AheadState)));
-    for (int q = 0; q < 2; ++q) {
-        HIPCHK(ra.ck[q].ensure(npaths * sizeof(float4)));
-        HIPCHK(ra.park[q].ensure(lanes * PARK_F4 * sizeof(float4)));
-    }
-    AheadState* st = ra.st.as<AheadState>();
-    if (!match) {
-        hipLaunchKernelGGL(k_ahead_reset, dim3(1), dim3(256), 0, s, st, 0, 1);
+    HIPCHK(ra.ck.ensure(nsets * npaths * sizeof(float4)));
+    HIPCHK(ra.park.ensure(nsets * cap * PARK_F4 * sizeof(float4)));
+    uint32_t clear;
+    if (match) {   // the previous call's next set is this call's own set; its own slot takes the farthest set
+        clear = 1u << ra.own;
+        ra.own = (ra.own + 1) % nsets;
+    } else {
+        clear = (1u << RA_MAX_SETS) - 1u;
         ra.own = 0;
     }
-    const int own = ra.own, ah = own ^ 1;
-    hipLaunchKernelGGL(k_ahead_reset, dim3(1), dim3(256), 0, s, st, ah, 0);
-    if (!ra.hst) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&ra.hst), 2 * sizeof(uint32_t), hipHostMallocDefault));
-    HIPCHK(hipMemcpyAsync(&ra.hst[0], &st->done[own][0], sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&ra.hst[1], &st->park_n[own][0], sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    ra.counted = true;
+    ra.nsets = nsets;
+    ra.park_cap = (uint32_t)cap;
+    AheadState* st = ra.st.as<AheadState>();
     A = Ahead{};
     A.on = 1u;
     A.npaths = (uint32_t)npaths;
-    A.s_off = p->spp;
-    A.park_n_own = &st->park_n[own][0];
-    A.ck = ra.ck[ah].as<float4>();
-    A.fetch_own = st->fetch[own];
-    A.fetch_ahead = st->fetch[ah];
-    A.done_own = &st->done[own][0];
-    A.done_ahead = &st->done[ah][0];
-    A.park_n_ahead = &st->park_n[ah][0];
-    A.take_own = &st->take[own][0];
-    A.park_own = ra.park[own].as<float4>();
-    A.park_ahead = ra.park[ah].as<float4>();
-    *ck_own = ra.ck[own].as<float4>();
+    A.spp = p->spp;
+    A.own = ra.own;
+    A.nsets = nsets;
+    A.park_cap = (uint32_t)cap;
+    A.st = st;
+    A.ck = ra.ck.as<float4>();
+    A.park = ra.park.as<float4>();
+    hipLaunchKernelGGL(k_ahead_prep, dim3(1), dim3(256), 0, s, st, clear, ra.own);
+    if (!ra.hst) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&ra.hst), 2 * sizeof(uint32_t), hipHostMallocDefault));
+    HIPCHK(hipMemcpyAsync(ra.hst, st->report, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    ra.counted = true;
+    *ck_own = ra.ck.as<float4>() + (size_t)ra.own * npaths;
     return KHP_OK;
 }
 static void ahead_commit(khp_ctx* c, const khp_render_params* p, size_t npaths) {
     khp_ctx::AheadSet& ra = c->ra;
     ra.valid = true;
-    ra.own ^= 1;
     ra.next = *p;
     ra.next.first_sample = p->first_sample + p->spp;
     ra.gen = c->gen;
@@ -3792,7 +3882,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     Wave Wv = wave_view(c, w);
     // render-ahead (khp_ctx_params.render_ahead): synchronous path-kernel calls of one chunk
     const bool ahead = use_path && !async && !ops && nf == 1 && c->prm.render_ahead != 0 && P_all > 0 &&
-                       P_chunk >= P_all && S_chunk >= p->spp && call_paths < ((size_t)1 << 31);
+                       P_chunk >= P_all && S_chunk >= p->spp && call_paths <= (size_t)PID_MASK + 1;
     Ahead AH{};
     if (ahead) KHPCHK(ahead_prepare(c, p, call_paths, sA, AH, &Wv.CK));
     Wv.pix = c->pix.as<uint32_t>();
@@ -3908,6 +3998,9 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                 }
                 if (!prepped) hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, Wb.shq, cur);
                 prepped = false;
+#ifdef KHP_LEAF_REUSE
+                if (stats) HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_reuse_b), &b, sizeof(b), 0, hipMemcpyHostToDevice, sA));
+#endif
                 timed(c, f, 0, true, sA);
                 const bool cam = b == 0 && Wv.cam0;
                 const bool wide = c->S.wide != nullptr && b >= c->prm.wide_from;
@@ -3944,7 +4037,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                         HIPCHK(w.rs_hist.ensure(2 * RS_CELLS * sizeof(uint32_t)));
                         uint32_t* hist = w.rs_hist.as<uint32_t>();
                         Wave Wn = Wv;   // the next queue (parity cur ^ 1) as shade wrote it
-                        timed(c, f, 1, true, sA);
+                        timed(c, f, 3, true, sA);   // under "other": shade_ms stays k_shade's alone
                         HIPCHK(hipMemsetAsync(hist, 0, RS_CELLS * sizeof(uint32_t), sA));
                         const uint32_t rs_per_cu = std::max(1u, std::min(2048u / RS_THREADS, 163840u / (RS_CELLS * 4u)));
                         const dim3 rs_grid((c->n_cu > 0 ? (uint32_t)c->n_cu : 256u) * rs_per_cu);   // resident blocks
@@ -3955,7 +4048,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                                            w.rs_keys.as<uint32_t>(), hist + RS_CELLS, w.rs_cols.as<float>(),
                                            w.rs_qsrc.as<uint32_t>());
                         HIPCHK(hipGetLastError());
-                        timed(c, f, 1, false, sA);
+                        timed(c, f, 3, false, sA);
                     }
                     return KHP_OK;
                 };
@@ -4448,10 +4541,17 @@ extern "C" khp_status khp_read_rgba8(khp_ctx* c, const khp_tonemap* tm, uint8_t*
             if (bounded_waits(c)) {
                 KHPCHK(wait_event(c, c->tm_ev[ch], "the 8-bit texture's log luminances"));
             } else {
-                for (;;) {
+                // spin briefly (a chunk usually lands within ~0.1 ms), then yield, then
+                // block: no core burnt for a long copy, no endless spin on a hung device
+                for (int spins = 0;; ++spins) {
                     const hipError_t q = hipEventQuery(c->tm_ev[ch]);
                     if (q == hipSuccess) break;
                     if (q != hipErrorNotReady) HIPCHK(q);
+                    if (spins >= 4096) {
+                        HIPCHK(hipEventSynchronize(c->tm_ev[ch]));
+                        break;
+                    }
+                    if (spins >= 256) std::this_thread::yield();
                 }
             }
             const uint32_t a = std::min(n, ch * per), b = std::min(n, a + per);
@@ -4834,6 +4934,17 @@ extern "C" khp_status khp_debug_wave_profile(khp_ctx* c, unsigned long long* out
     *n = cnt;
     return KHP_OK;
 }
+// render-ahead timeline of the last launch: the 100 MHz clock when its last own path
+// ended and when the first wave saw that (~0ull: none); read and reset
+extern "C" khp_status khp_debug_ahead_profile(khp_ctx* c, unsigned long long* out) {
+    if (!c || !out) return fail(KHP_EINVAL, "null argument");
+    KHPCHK(drain(c));
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ra_prof), 2 * sizeof(unsigned long long)));
+    const unsigned long long init[2] = {0ull, ~0ull};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_ra_prof), init, sizeof(init)));
+    return KHP_OK;
+}
 #endif
 
 // ---- RCCL ---------------------------------------------------------------------------------
@@ -5188,3 +5299,17 @@ static khp_status gather_now(khp_ctx* c, const khp_render_params* p, int root) {
     c->fb_evt = c->gather_evt;
     return KHP_OK;
 }
+
+#ifdef KHP_LEAF_REUSE
+// Diagnostic builds: the leaf-record reuse histograms of the instrumented k_extend
+// launches since the last call (traverse.h leaf_reuse), 16 bounces x 8; read and reset.
+extern "C" khp_status khp_debug_leaf_reuse(khp_ctx* c, unsigned long long* out) {
+    if (!c || !out) return fail(KHP_EINVAL, "null argument");
+    KHPCHK(drain(c));
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_leaf_hist), 16 * 8 * sizeof(unsigned long long)));
+    static const unsigned long long zero[16 * 8] = {};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_leaf_hist), zero, sizeof(zero)));
+    return KHP_OK;
+}
+#endif

@@ -505,6 +505,34 @@ __device__ __forceinline__ bool candidate_rt(float4 p0, float4 p1, float4 p2, fl
     return cone_quadratic(p0, p1, p2, p3, r, any, 0.0f, tMax, t);
 }
 
+#ifdef KHP_LEAF_REUSE
+// Diagnostic builds: how many lanes of a wave fetch the SAME
+// candidate (cone / triangle) record in one traversal iteration of the instrumented
+// closest-hit kernels.  Per bounce (g_reuse_b, set by the host before each launch),
+// the leaf-record fetches are binned by the size of their group of lanes fetching the
+// same record: 1, 2, 3-4, 5-8, 9-16, 17-32, 33-64 (weighted by lanes), and slot 7
+// counts the distinct records fetched.  Read by khp_debug_leaf_reuse.
+__device__ unsigned long long g_leaf_hist[16 * 8];
+__device__ uint32_t g_reuse_b;
+__device__ __forceinline__ void leaf_reuse(bool in_leaf, uint32_t slot) {
+    unsigned long long m = __ballot(in_leaf);
+    const uint32_t b = g_reuse_b < 16u ? g_reuse_b : 15u;
+    const uint32_t lane = threadIdx.x & 63u;
+    while (m) {
+        const int leader = __ffsll((long long)m) - 1;
+        const uint32_t s = (uint32_t)__shfl((int)slot, leader);
+        const unsigned long long same = __ballot(in_leaf && slot == s) & m;
+        const uint32_t n = (uint32_t)__popcll(same);
+        const uint32_t k = n == 1u ? 0u : n == 2u ? 1u : n <= 4u ? 2u : n <= 8u ? 3u : n <= 16u ? 4u : n <= 32u ? 5u : 6u;
+        if (lane == (uint32_t)leader) {
+            atomicAdd(&g_leaf_hist[b * 8 + k], (unsigned long long)n);
+            atomicAdd(&g_leaf_hist[b * 8 + 7], 1ull);
+        }
+        m &= ~same;
+    }
+}
+#endif
+
 // One wave iteration of one lane (mode != M_IDLE).  KIND 1: any-hit with the
 // fixed limit tlimit = the ray's tMax; KIND 0: closest hit, tlimit = h.t;
 // KIND 2: the lane's any_rt decides (the path kernel).  Returns true when the
@@ -517,6 +545,9 @@ __device__ __forceinline__ bool iter2k(const DevScene& S, const TravRay& tr, Hit
     const bool in_leaf = mode == M_LEAF;
     const bool fetch = in_leaf || mode == M_NODE;
     const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : reinterpret_cast<const float4*>(S.nodes + c.ref);
+#ifdef KHP_LEAF_REUSE
+    if (STATS && KIND == 0) leaf_reuse(in_leaf, lf.slot);
+#endif
     float4 q0, q1, q2, q3;
     if (Stack::kTop && fetch && !in_leaf && (c.ref & TOP_REF) != 0u) {   // a staged top record (LDS)
         const float4* t = stk.top() + 4 * (c.ref & 0xFFu);
@@ -686,6 +717,9 @@ __device__ __forceinline__ bool iterwk(const DevScene& S, const TravRay& tr, Hit
     const bool node = mode == M_NODE;
     const bool fetch = in_leaf || node;
     const float4* p = in_leaf ? S.prims + 4 * (size_t)lf.slot : S.wide + 8 * (size_t)c.ref;
+#ifdef KHP_LEAF_REUSE
+    if (STATS && KIND == 0) leaf_reuse(in_leaf, lf.slot);
+#endif
     float4 q0, q1, q2, q3, q4, q5, q6, q7;
     if (fetch) {
         q0 = p[0];

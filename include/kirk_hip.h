@@ -280,7 +280,9 @@ typedef struct {
     uint64_t chunk_paths;        /* paths per wavefront chunk, >= 4096; 0 (default): the smaller of
                                     2^27 and what fits in half the free HBM                         */
     uint32_t heavy_iters;        /* longest-first queues: a path whose last traversal took more
-                                    iterations has its next rays claimed first (default 160)        */
+                                    iterations has its next rays claimed first (default 160).  No
+                                    effect on the extension rays of bounces regrouped by ray_sort_from
+                                    (their claim order is the cell order; shadow rays keep it)      */
     int32_t dump_bounce;         /* debug: keep the extension rays of this bounce of the next
                                     synchronous render for khp_debug_queue (-1: off, default)       */
     uint32_t trace_kernels;      /* khp_trace_closest / khp_trace_any run on 0: one-ray-per-thread
@@ -328,16 +330,18 @@ typedef struct {
                                     staged in each traversal wave's LDS beside its stack rings (the 64-B
                                     loops of k_extend and k_shadow), the rest fetched from HBM as before.
                                     Same walk, same counts, same frames.  Measured in DESIGN.md §4    */
-    uint32_t render_ahead;       /* ABI 13: 1 (default) or 0.  A synchronous render that runs the path kernel
+    uint32_t render_ahead;       /* ABI 13: 0..3 (default 2).  A synchronous render that runs the path kernel
                                     in one chunk lets the lanes that would idle in its launch's drain (its
-                                    longest paths finishing alone) start the paths of the NEXT call of a
-                                    progressive series -- the same pixels, spp, depth and seed, first_sample +
-                                    spp: KIRK's PathTracer::render loop, CPU_PathTracer.cpp:17-52.  The call
-                                    still returns as soon as its own paths end; the next matching call resumes
-                                    the paths parked at that moment and accumulates the colours already
-                                    finished.  Any other call, and any change of scene, camera or parameters,
-                                    drops that work.  Frames, textures and framebuffers are those of each call
-                                    alone, bit for bit.  Measured in DESIGN.md §5b                          */
+                                    longest paths finishing alone) start the paths of the next render_ahead
+                                    calls of a progressive series -- the same pixels, spp, depth and seed,
+                                    first_sample + spp, + 2 spp, ...: KIRK's PathTracer::render loop,
+                                    CPU_PathTracer.cpp:17-52.  A call still returns as soon as its own
+                                    paths end (at once when earlier calls finished them all); the paths of
+                                    later calls in flight then are parked and resumed by later calls, which
+                                    accumulate the colours already finished.  Any other call, and any change
+                                    of scene, camera or parameters, drops that work.  Frames, textures and
+                                    framebuffers are those of each call alone, bit for bit.  Measured in
+                                    DESIGN.md §5b                                                          */
     uint32_t reserved0;          /* 0 */
 } khp_ctx_params;   /* 64 bytes */
 

@@ -283,6 +283,17 @@ except N.KhpError as e:
     assert e.status in (N.KHP_ENOTREADY, N.KHP_EINVAL), e
 img = ctx.render(32, 24, 1, 5)          # the context is still usable
 assert img.shape == (24, 32, 3)
+# VERDICT r05 item 5 (ADVICE r04, the two-GPU test_rccl_abort_then_local_group_waits_unbounded
+# on one GPU): after the abort, a 1 ms bound and a move into a one-member local group, a
+# render that takes far longer than the bound completes normally
+from ba_pathtracing_fur_amd.pathtracer import comm_init_local
+ctx.comm_set_timeout(1)
+t1 = time.time()
+big = ctx.render(384, 288, 16, 5)       # ~tens of ms of device work
+assert big.shape == (288, 384, 3)
+comm_init_local([ctx])
+big2 = ctx.render(384, 288, 16, 5, first_sample=16)
+assert big2.shape == (288, 384, 3) and time.time() - t1 > 0.002
 ctx.close()                             # khp_destroy with the abandoned init thread still blocked in RCCL
 # the abandoned helper thread stays blocked inside ncclCommInitRankConfig (RCCL
 # 2.27.7 does not return while a peer is missing): it holds only its own job, so a
@@ -303,8 +314,10 @@ def test_rccl_init_without_peer_fails_with_a_status():
     """A forced RCCL failure: rank 0 of 2 initialises while rank 1 never joins.
     The non-blocking init is polled against the context's timeout and returns
     KHP_EDEVICE naming the rank (it used to block in ncclCommInitRank forever).
-    Run in a child process with its own time limit, so a regression cannot
-    hang the test run."""
+    After the abort, with a 1 ms bound and the context moved into a local group,
+    renders far longer than the bound complete (the one-GPU form of
+    test_rccl_abort_then_local_group_waits_unbounded).  Run in a child process
+    with its own time limit, so a regression cannot hang the test run."""
     r = subprocess.run([sys.executable, "-c", _NO_PEER % {"root": ROOT}], capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0 and "NO_PEER_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

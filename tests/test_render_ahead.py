@@ -59,18 +59,19 @@ SCENES = [("config2", dict(n_strands=2000), 64, 48, 5), ("zoo", dict(n_strands=4
 
 
 @pytest.mark.parametrize("name,kw,w,h,depth", SCENES, ids=[s[0] for s in SCENES])
-@pytest.mark.parametrize("spp,wide", [(1, 2), (2, 0), (3, 2)])
-def test_progressive_calls_match_oracle(name, kw, w, h, depth, spp, wide):
+@pytest.mark.parametrize("spp,wide,ahead_sets", [(1, 2, 2), (2, 0, 1), (3, 2, 3)])
+def test_progressive_calls_match_oracle(name, kw, w, h, depth, spp, wide, ahead_sets):
     """Synchronous calls first_sample = 0, spp, 2 spp, ...: every call's
     framebuffer and texture are the oracle's, and from the second call on the
-    call found work rendered ahead for it (khp_stats.ahead_*)."""
+    call found work rendered ahead for it (khp_stats.ahead_*), with 1, 2 and 3
+    later calls' sets rendered ahead."""
     sd = S.build_config(name, width=w, height=h, **kw)
     ser = _Series(sd, w, h, depth)
     ctx = HipContext(0)
     try:
         ctx.set_scene(sd)
         ctx.build_accel()
-        ctx.set_params(path_kernel=2, wide_from=wide, render_ahead=1)
+        ctx.set_params(path_kernel=2, wide_from=wide, render_ahead=ahead_sets)
         ahead = []
         for k in range(6):
             ctx.render(w, h, spp, depth, first_sample=k * spp, readback=False)
@@ -79,8 +80,11 @@ def test_progressive_calls_match_oracle(name, kw, w, h, depth, spp, wide):
             ser.call(spp, k * spp)
             _check(ctx, ser, w, h, f"call {k}")
         assert ahead[0] == 0
-        # a small image: the whole next set is claimed in the drain of each call
-        assert all(a > 0 for a in ahead[1:]), ahead
+        # each later call found work rendered ahead for it -- unless the previous call
+        # had found ITS whole set finished: that call returns at once and renders nothing ahead
+        n = w * h * spp
+        assert all(ahead[k] > 0 or ahead[k - 1] == n for k in range(1, 6)), ahead
+        assert max(ahead[1:]) > 0, ahead
     finally:
         ctx.close()
 
@@ -147,7 +151,7 @@ def test_render_ahead_off_and_validation(hip_ctx):
         got = hip_ctx.read_framebuffer(w, h)
         assert_parity(got, oracle_ffi.Oracle(sd).render(w, h, 3, depth, threads=16), exact=True)
         with pytest.raises(N.KhpError):
-            hip_ctx.set_params(render_ahead=2)
+            hip_ctx.set_params(render_ahead=4)
     finally:
         hip_ctx.set_params(**old)
 
@@ -174,8 +178,9 @@ def metric_scene_oracle():
 def test_gui_calls_full_size(metric_scene_oracle):
     """The metric scene at 1080p, KIRK's GUI call (1 spp + texture) four times
     with render-ahead (the default): each call's framebuffer equals the same
-    calls without it bit for bit, the later calls resume parked paths, and
-    every 27th row of the last frame is the oracle's."""
+    calls without it bit for bit, the later calls found paths finished ahead
+    (and, unless their whole set was, parked ones), and every 27th row of the
+    last frame is the oracle's."""
     W, H, D = 1920, 1080, 5
     frames = {}
     counts = []
@@ -200,7 +205,7 @@ def test_gui_calls_full_size(metric_scene_oracle):
         assert np.array_equal(frames[1][0][k].view(np.uint32), frames[0][0][k].view(np.uint32)), k
         assert np.array_equal(frames[1][1][k], frames[0][1][k]), k
     assert counts[0] == (0, 0)
-    assert all(f > 0 and r > 0 for f, r in counts[1:]), counts
+    assert all(f > 0 and (r > 0 or f == W * H) for f, r in counts[1:]), counts
     rows = (13, 1080, 27)
     want = np.zeros((H, W, 3), np.float32)
     for k in range(4):

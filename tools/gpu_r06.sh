@@ -13,5 +13,19 @@ ra)   # render-ahead: its tests, the path-kernel parity tests, then the synchron
 sync)  # synchronous-call timings only ($3: extra env, e.g. KHP_LIB=variants/libkirk_x.so)
   env $3 timeout -k 10 300 python -u tools/sync_calls.py 8 >> gpurun_out/$T/sync_calls.jsonl 2>> gpurun_out/$T/sync_calls.log || exit 1
   ;;
+probe)  # tools/ra_probe.py over the in-tree library and variants/libkirk_<v>.so for v in $3; $4: render_ahead list
+  for v in base $3; do
+    if [ $v = base ]; then L=""; else L="KHP_LIB=variants/libkirk_$v.so"; fi
+    env $L timeout -k 10 300 python -u tools/ra_probe.py 12 1,8 ${4:-1,0} >> gpurun_out/$T/ra_probe.jsonl 2>> gpurun_out/$T/ra_probe.log || exit 1
+  done
+  ;;
+drain)  # per-wave k_path timelines with render-ahead on and off (variants/libkirk_prof.so)
+  for ra in 1 0; do
+    KHP_LIB=variants/libkirk_prof.so timeout -k 10 300 python -u tools/path_drain_probe.py 3 path_kernel=2 render_ahead=$ra >> gpurun_out/$T/drain.jsonl 2>> gpurun_out/$T/drain.log || exit 1
+  done
+  ;;
+leaf)   # leaf-record reuse inside a wave (variants/libkirk_leafreuse.so)
+  KHP_LIB=variants/libkirk_leafreuse.so timeout -k 10 300 python -u tools/leaf_reuse.py 8 > gpurun_out/$T/leaf_reuse.json 2> gpurun_out/$T/leaf_reuse.log || exit 1
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac

@@ -41,6 +41,18 @@ scenes.config3_device(ctx, W, H, n_strands=1_000_000)
 ctx.build_accel()
 
 
+RA = (ctypes.c_uint64 * 2)()
+
+
+def read_ahead():
+    """khp_debug_ahead_profile: clock of the last own path's end, of the first wave seeing it."""
+    if not hasattr(lib, "khp_debug_ahead_profile"):
+        return None
+    lib.khp_debug_ahead_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    native.check(lib, lib.khp_debug_ahead_profile(ctx.ptr, RA), "khp_debug_ahead_profile")
+    return RA[0], RA[1]
+
+
 def read_waves():
     lib.khp_debug_wave_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     native.check(lib, lib.khp_debug_wave_profile(ctx.ptr, buf, MAXW, ctypes.byref(nw)), "khp_debug_wave_profile")
@@ -54,12 +66,14 @@ for _ in range(2):  # warmup
     ctx.render(W, H, 8, D, first_sample=k, readback=False)
     k += 8
 read_waves()
+read_ahead()
 for name, spp in (("gui", 1), ("sync8", 8)):
     for call in range(N):
         ctx.render(W, H, spp, D, first_sample=k, readback=False)
         k += spp
         st = ctx.stats()
         rec = read_waves()
+        ra = read_ahead()
         if not rec:
             continue
         t0 = min(r[0] for r in rec)
@@ -79,7 +93,13 @@ for name, spp in (("gui", 1), ("sync8", 8)):
                        "us_per_drain_iter": round(dms * 1e3 / dit, 3) if dit else None,
                        "lanes_per_drain_iter": round(r[4] / dit, 2) if dit else None,
                        "lanes_at_exh": r[5] & 0xFFFFFFFF})
+        ra_line = None
+        if ra and ra[0]:
+            ra_line = {"own_end_ms": round((ra[0] - t0) / 1e5, 3),
+                       "stop_seen_ms": round((ra[1] - t0) / 1e5, 3) if ra[1] != 2 ** 64 - 1 else None,
+                       "ahead_finished": st["ahead_finished"], "ahead_resumed": st["ahead_resumed"]}
         print(json.dumps({"pattern": name, "call": call, "waves": len(rec), "device_ms": round(st["render_ms"], 3),
+                          "ahead": ra_line,
                           "first_exh_ms": round((min(exh) - t0) / 1e5, 3), "exh_ms": round((last_exh - t0) / 1e5, 3),
                           "end_ms": round((end - t0) / 1e5, 3), "alive_after_exh": alive, "longest": lw}), flush=True)
 ctx.close()
