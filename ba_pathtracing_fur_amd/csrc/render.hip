@@ -379,6 +379,15 @@ struct Claimer {
         tried = 0;
         res_lo = res_hi = 0;
     }
+    // The same claim geometry over another cursor array (render-ahead: the next set,
+    // which has the same number of paths).
+    __device__ __forceinline__ void retarget(uint32_t* f) {
+        fetch = f;
+        rseg = 0;
+        sg = (blockIdx.x % 8u) * SEG_PER_XCD + (blockIdx.x / 8u) % SEG_PER_XCD;
+        tried = 0;
+        res_lo = res_hi = 0;
+    }
     __device__ __forceinline__ uint32_t hlo(uint32_t g) const { return (uint32_t)((uint64_t)nf * g / NSEG); }
     __device__ __forceinline__ uint32_t llo(uint32_t g) const { return (uint32_t)((uint64_t)nl * g / NSEG); }
     __device__ __forceinline__ uint32_t lo(uint32_t g) const { return CB_LOG ? g * (sf + sl) : hlo(g) + llo(g); }
@@ -1973,7 +1982,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                             }
                         } else if (++cur < nsets) {   // the next set: its cursors and park list
                             const uint32_t s2 = ra_slot(A, cur);
-                            cl.init(A.st->fetch[s2], npaths, 0u, npaths);
+                            cl.retarget(A.st->fetch[s2]);
                             exhausted = false;
                             lim = __builtin_amdgcn_readfirstlane(A.st->park_lim[s2][0]);
                             res_left = lim > 0u;

@@ -87,7 +87,7 @@ def parse():
     ap.add_argument("--fuse", type=int, default=None, help="khp_ctx_params.fuse_frames (default: the library's)")
     ap.add_argument("--chunk-paths", type=int, default=None, help="khp_ctx_params.chunk_paths")
     ap.add_argument("--frames-in-flight", type=int, default=None, help="khp_ctx_params.frames_in_flight")
-    ap.add_argument("--gui-steps", type=int, default=8,
+    ap.add_argument("--gui-steps", type=int, default=12,
                     help="KIRK GUI calls timed: 1 spp per synchronous render + 8-bit texture read (0: skip)")
     ap.add_argument("--iso-steps", type=int, default=8,
                     help="fused passes re-run with serial_stages=1 for the isolated per-kernel rooflines (0: skip)")
@@ -457,19 +457,29 @@ def main():
     # then reads the 8-bit texture (drawTexture -> Texture::setPixel)
     gui_line = None
     if args.gui_steps > 0 and rank == 0 and world == 1:
-        ctx.render(W, H, 1, depth, first_sample=k * spp, readback=False)
-        ctx.read_rgba8(W, H)
+        for g in range(2):   # the series' first calls (render-ahead fills up), untimed
+            ctx.render(W, H, 1, depth, first_sample=k * spp + g, readback=False)
+            ctx.read_rgba8(W, H)
+        calls, ahead = [], []
         t1 = time.perf_counter()
         for g in range(args.gui_steps):
-            ctx.render(W, H, 1, depth, first_sample=k * spp + 1 + g, readback=False)
+            tc = time.perf_counter()
+            ctx.render(W, H, 1, depth, first_sample=k * spp + 2 + g, readback=False)
             ctx.read_rgba8(W, H)
+            calls.append(round((time.perf_counter() - tc) * 1e3, 3))
+            st_g = ctx.stats()
+            ahead.append(st_g["ahead_finished"])
         gui_el = time.perf_counter() - t1
         gui_line = {"value": round(args.gui_steps * W * H / gui_el / 1e6, 3),
                     "ms_per_call": round(gui_el / args.gui_steps * 1e3, 3), "calls": args.gui_steps,
+                    "call_ms": calls, "paths_finished_ahead": ahead,
                     "def": "KIRK GUI render() calls: one synchronous khp_render of 1 spp + khp_read_rgba8 "
-                           "(8-bit texture to the host) per call; synchronous renders run the path kernel "
-                           f"(khp_ctx_params.path_kernel = {params['path_kernel']}, 0 = automatic)"}
-        k += 1   # those samples belong to the pass slot after the last timed one
+                           "(8-bit texture to the host) per call, consecutive first_sample; synchronous renders run "
+                           f"the path kernel (khp_ctx_params.path_kernel = {params['path_kernel']}, 0 = automatic) "
+                           f"with render_ahead = {params.get('render_ahead', 0)} (a call's drain starts the paths of "
+                           "the next calls; each call returns when its own paths end; call_ms: each call, "
+                           "paths_finished_ahead: its paths found finished by earlier calls)"}
+        k += (args.gui_steps + 2 + spp - 1) // spp   # those samples belong to the pass slots after the last timed one
         # the same calls pipelined (ABI 8): render() enqueues its 1-spp pass and an
         # asynchronous texture read, the viewer shows textures as they complete;
         # consecutive passes fuse, each texture is taken between two accumulates
