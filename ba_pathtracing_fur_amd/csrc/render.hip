@@ -1625,7 +1625,16 @@ __global__ void k_ahead_prep(AheadState* a, uint32_t clear, uint32_t own) {
         }
     }
     __syncthreads();
-    if (threadIdx.x < RA_MAX_SETS) a->park_lim[threadIdx.x][0] = a->park_n[threadIdx.x][0];
+    // A resume claim takes a wave's whole request from `take`, also past the limit
+    // (those lanes get nothing), so take can end a launch beyond park_lim while the
+    // records from park_lim on -- parked by that same launch -- were never resumed:
+    // the next launch resumes from park_lim there.
+    if (threadIdx.x < RA_MAX_SETS) {
+        const uint32_t p = threadIdx.x;
+        if (a->take[p][0] > a->park_lim[p][0]) a->take[p][0] = a->park_lim[p][0];
+        a->park_lim[p][0] = a->park_n[p][0];
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         a->report[0] = a->done[own][0];
         a->report[1] = a->park_n[own][0] > a->take[own][0] ? a->park_n[own][0] - a->take[own][0] : 0u;

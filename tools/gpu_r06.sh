@@ -27,5 +27,29 @@ drain)  # per-wave k_path timelines with render-ahead on and off (variants/libki
 leaf)   # leaf-record reuse inside a wave (variants/libkirk_leafreuse.so)
   KHP_LIB=variants/libkirk_leafreuse.so timeout -k 10 300 python -u tools/leaf_reuse.py 8 > gpurun_out/$T/leaf_reuse.json 2> gpurun_out/$T/leaf_reuse.log || exit 1
   ;;
+full)   # the whole GPU suite, then the driver's bench command
+  KHP_NO_BUILD=1 timeout -k 10 1000 $PYT tests > gpurun_out/$T/gpu_tests.log 2>&1 || exit 1
+  timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver_cmd.json 2> gpurun_out/$T/bench.log || exit 1
+  ;;
+bench)  # the driver's bench command only
+  timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench_driver_cmd.json 2> gpurun_out/$T/bench.log || exit 1
+  ;;
+vars)   # the driver's bench shape (fused passes only), in-tree vs variants/libkirk_<v>.so for v in $3, alternated twice
+  for r in 1 2; do
+    for v in base $3; do
+      if [ $v = base ]; then L=""; else L="KHP_LIB=variants/libkirk_$v.so"; fi
+      env $L timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --sync-check-steps 0 --gui-steps 0 --iso-steps 0 > gpurun_out/$T/v_${v}_$r.json 2> gpurun_out/$T/v_${v}_$r.log || exit 1
+    done
+  done
+  python - $T base $3 <<'PY'
+import json, sys
+t = sys.argv[1]
+for r in (1, 2):
+    for v in sys.argv[2:]:
+        d = json.loads(open(f"gpurun_out/{t}/v_{v}_{r}.json").read().strip().splitlines()[-1])
+        rl = d["roofline"]
+        print(r, v, d["value"], "frac", rl["frac"], "b-ms", [b["ms_per_frame"] for b in rl["per_bounce"]])
+PY
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
