@@ -598,9 +598,10 @@ khp_status khp_camera_setup(const float position[3], const float look_at[3], con
                             uint32_t width, uint32_t height, khp_camera* out);
 
 /* ABI 13: replaces the scene's camera without rebuilding anything (KIRK's GUI
- * moves the Camera between PathTracer::render calls and restarts the pass
- * count, CPU_PathTracer.cpp:17-24).  Completes in-flight frames first; the
- * next render uses the new camera.  Drops render-ahead work. */
+ * moves the Camera between PathTracer::render calls and resets the pass
+ * count, after which render() restarts its buffers, CPU_PathTracer.cpp:17-19).
+ * Completes in-flight frames first; the next render uses the new camera.
+ * Drops render-ahead work. */
 khp_status khp_set_camera(khp_ctx* ctx, const khp_camera* camera);
 
 /* Fur fibers -> cone frusta exactly as CPU_Scene::flattenNode does with

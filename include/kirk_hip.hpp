@@ -155,6 +155,8 @@ class Context {
         check(khp_set_scene(c_, &v), "khp_set_scene");
     }
     void build_accel() { check(khp_build_accel(c_), "khp_build_accel"); }
+    // ABI 13: a moved camera for the next render, nothing rebuilt
+    void set_camera(const khp_camera& cam) { check(khp_set_camera(c_, &cam), "khp_set_camera"); }
     // scheduling parameters (ABI 6); never change results
     khp_ctx_params params() {
         khp_ctx_params p{};
