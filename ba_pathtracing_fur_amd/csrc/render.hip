@@ -91,6 +91,7 @@ struct Wave {
     uint32_t pix_major;   // path numbering (khp_ctx_params.path_order): 0 frame-major, else pixel-major
     uint8_t* pixheavy;    // path_order 2: per image pixel, its last camera ray took > heavy_T iterations (null: off)
     uint32_t cam0;        // bounce 0 computes camera rays in place (no k_generate queue)
+    uint32_t q_cur, q_bounce;   // k_path from the queue (hybrid batches): the queue's parity and bounce
     uint32_t fsample0[KHP_MAX_FUSE];  // per fused frame: global sample index of chunk sample 0
     uint32_t depth;
     uint8_t* heavy;       // per queue slot: the ray's traversal took more than heavy_T iterations
@@ -1819,6 +1820,9 @@ __device__ unsigned long long g_ra_prof[2];
 #ifndef KHP_RA_BATCH
 #define KHP_RA_BATCH 1024
 #endif
+#ifndef KHP_RA_PROTECT   // only waves without an own path claim later sets' paths
+#define KHP_RA_PROTECT 0
+#endif
 #ifndef KHP_RA_MIX   // measured slower: off
 #define KHP_RA_MIX 0
 #endif
@@ -1828,7 +1832,12 @@ __device__ unsigned long long g_ra_prof[2];
 #ifndef KHP_RA_NO_AHEAD   // diagnostic builds: the render-ahead instance with nothing claimed ahead
 #define KHP_RA_NO_AHEAD 0
 #endif
-template <bool TEX, bool WIDE, uint32_t KINDS, bool RA>
+// QS (hybrid batches, khp_ctx_params.path_from): the launch takes its paths from the
+// wavefront's queue of bounce Wv.q_bounce (parity Wv.q_cur) -- each entry's ray and
+// path state (TFq / CKq, moved as k_shade and the shadow finish left them) -- and
+// carries them through the remaining bounces; paths of a chunk that ended earlier
+// already wrote their colour.
+template <bool TEX, bool WIDE, uint32_t KINDS, bool RA, bool QS = false>
 __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wave Wv, SpillArea spill, PathLanes L, Ahead A) {
     extern __shared__ uint32_t lds[];
     const uint32_t npaths = Wv.P * Wv.n_samples * Wv.n_frames;
@@ -1857,7 +1866,8 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
     bool any = false, occ = false, exhausted = false;
     float tmax_any = 0.0f;
     Claimer cl;   // the claims of set `cur` (render-ahead), of the launch's paths otherwise
-    cl.init(RA ? A.st->fetch[A.own] : Wv.cnt->fetch_ext, npaths, 0u, npaths);
+    if (QS) cl.init(Wv.cnt->fetch_ext, Wv.cnt->nq[Wv.q_cur], Wv.cnt->nqb[Wv.q_cur], Wv.cap);
+    else cl.init(RA ? A.st->fetch[A.own] : Wv.cnt->fetch_ext, npaths, 0u, npaths);
 #ifdef KHP_PATH_PROFILE   // diagnostic builds: launch timeline (100 MHz wall clock): first start, last
     // claim exhaustion seen, last end, longest drain of one wave (its end - its exhaustion)
     const unsigned long long pc_start = wall_clock64();
@@ -1949,6 +1959,9 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                 pend[0] += (uint32_t)__popcll(eom);
                 for (uint32_t j = 1; j < RA_MAX_SETS; ++j) pend[j] += (uint32_t)__popcll(__ballot(ended == 1u + j));
                 own_lanes &= ~eom;
+                // KHP_RA_PROTECT: a wave that idled lanes while it carried own paths takes
+                // later sets' paths again once they have all ended
+                if (KHP_RA_PROTECT && own_lanes == 0ull && cur > 0u && cur < nsets && state == PS_DONE) state = PS_NEW;
 #ifdef KHP_PATH_PROFILE
                 if (eom && lane_id() == 0) atomicMax(&g_ra_prof[0], wall_clock64());
 #endif
@@ -1959,7 +1972,8 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                 uint32_t cpid = 0, coff = 0;
                 if constexpr (RA) {
                     // set after set (own first): its parked paths, then its unclaimed ones
-                    while (want != 0ull && cur < nsets) {
+                    while (want != 0ull && cur < nsets &&
+                           !(KHP_RA_PROTECT && cur > 0u && (own_lanes | __ballot(st_own)) != 0ull)) {
                         const uint32_t sl = ra_slot(A, cur);
                         if (res_left) {
                             const uint32_t slot = wave_alloc(state == PS_NEW && !cam, &A.st->take[sl][0]);
@@ -1999,7 +2013,24 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
                         want = __ballot(state == PS_NEW && !cam);
                     }
                     own_lanes |= __ballot(st_own);
-                    if (state == PS_NEW && cur >= nsets) state = PS_DONE;
+                    if (state == PS_NEW && (cur >= nsets || (KHP_RA_PROTECT && cur > 0u && own_lanes != 0ull)))
+                        state = PS_DONE;
+                } else if constexpr (QS) {   // the next queue entry: its ray and path state
+                    uint32_t my = 0, slot = 0;
+                    bool got = false;
+                    if (!exhausted) got = cl.claim(want, my, exhausted);
+                    if (state == PS_NEW && got && cl.phys(my, slot)) {
+                        const uint32_t qc = Wv.q_cur;
+                        const uint32_t src = Wv.qsrc ? Wv.qsrc[slot] : slot;   // regrouped rays: state slot
+                        L.col[0][g] = Wv.TFq[qc][src];
+                        L.col[1][g] = Wv.CKq[qc][src];
+                        L.col[2][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(Wv.qpid[qc][slot]));
+                        L.col[3][g] = make_float4(0.0f, 0.0f, 0.0f, f_from_bits(Wv.q_bounce));
+                        sray.o = mk(Wv.qo[qc][0][slot], Wv.qo[qc][1][slot], Wv.qo[qc][2][slot]);
+                        sray.d = mk(Wv.qd[qc][0][slot], Wv.qd[qc][1][slot], Wv.qd[qc][2][slot]);
+                        sany = false;
+                        state = PS_BEGIN;
+                    }
                 } else {
                     uint32_t my = 0, pid = 0;
                     bool got = false;
@@ -2085,7 +2116,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, PATH_WAVES) void k_path(DevScene S, Wav
             // refill at REFILL finished lanes; once every path is claimed, as soon as
             // the finished lanes are as many as those still traversing (the drain;
             // servicing at every finished lane there measured 5% slower)
-            const bool nomore = RA ? cur >= nsets : exhausted;
+            const bool nomore = RA ? (cur >= nsets || (KHP_RA_PROTECT && cur > 0u && own_lanes != 0ull)) : exhausted;
             uint32_t thr = nomore ? (ntrav < PATH_REFILL ? (ntrav > 0u ? ntrav : 1u) : PATH_REFILL) : PATH_REFILL;
             if (RA && KHP_RA_MIX && cur > 0u && own_lanes != 0ull) {
                 // render-ahead, a wave carrying own paths beside later sets' ones once the own set is
@@ -2155,21 +2186,25 @@ constexpr uint32_t KINDS_ALL = (1u << KHP_BSDF_COUNT) - 1u;
 constexpr uint32_t KINDS_FUR = (1u << KHP_BSDF_LAMBERTIAN_REFLECTION) | (1u << KHP_BSDF_MARSCHNER_HAIR);
 template <bool TEX, bool WIDE, uint32_t K>
 static void launch_path_k(int grid, hipStream_t s, const DevScene& S, const Wave& W, SpillArea sp, const PathLanes& L,
-                          const Ahead& A) {
+                          const Ahead& A, bool qs) {
+    if (qs) {
+        hipLaunchKernelGGL((k_path<TEX, WIDE, K, false, true>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L, A);
+        return;
+    }
     if (A.on) hipLaunchKernelGGL((k_path<TEX, WIDE, K, true>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L, A);
     else hipLaunchKernelGGL((k_path<TEX, WIDE, K, false>), dim3(grid), dim3(TRAV_BLOCK), PATH_LDS, s, S, W, sp, L, A);
 }
 static void launch_path(bool tex, bool wide, bool fur, int grid, hipStream_t s, const DevScene& S, const Wave& W,
-                        SpillArea sp, const PathLanes& L, const Ahead& A) {
+                        SpillArea sp, const PathLanes& L, const Ahead& A, bool qs = false) {
     if (tex) {
-        if (wide) launch_path_k<true, true, KINDS_ALL>(grid, s, S, W, sp, L, A);
-        else launch_path_k<true, false, KINDS_ALL>(grid, s, S, W, sp, L, A);
+        if (wide) launch_path_k<true, true, KINDS_ALL>(grid, s, S, W, sp, L, A, qs);
+        else launch_path_k<true, false, KINDS_ALL>(grid, s, S, W, sp, L, A, qs);
     } else if (fur) {
-        if (wide) launch_path_k<false, true, KINDS_FUR>(grid, s, S, W, sp, L, A);
-        else launch_path_k<false, false, KINDS_FUR>(grid, s, S, W, sp, L, A);
+        if (wide) launch_path_k<false, true, KINDS_FUR>(grid, s, S, W, sp, L, A, qs);
+        else launch_path_k<false, false, KINDS_FUR>(grid, s, S, W, sp, L, A, qs);
     } else {
-        if (wide) launch_path_k<false, true, KINDS_ALL>(grid, s, S, W, sp, L, A);
-        else launch_path_k<false, false, KINDS_ALL>(grid, s, S, W, sp, L, A);
+        if (wide) launch_path_k<false, true, KINDS_ALL>(grid, s, S, W, sp, L, A, qs);
+        else launch_path_k<false, false, KINDS_ALL>(grid, s, S, W, sp, L, A, qs);
     }
 }
 
@@ -2901,7 +2936,7 @@ extern "C" khp_status khp_set_params(khp_ctx* c, const khp_ctx_params* prm) {
     if (prm->path_kernel > 2) return fail(KHP_EINVAL, "path_kernel must be 0, 1 or 2");
     if (prm->lds_nodes != 0 && prm->lds_nodes != TOP_NODES) return fail(KHP_EINVAL, "lds_nodes must be 0 or 7");
     if (prm->render_ahead > RA_MAX_SETS - 1) return fail(KHP_EINVAL, "render_ahead must be 0..3");
-    if (prm->reserved0 != 0) return fail(KHP_EINVAL, "reserved0 must be 0");
+    if (prm->path_from > 64) return fail(KHP_EINVAL, "path_from must be 0..64");
     HIPCHK(hipSetDevice(c->device));
     khp_status dr = drain(c);  // frames in flight finish with the parameters they started with
     if (dr != KHP_OK) return dr;
@@ -3851,16 +3886,23 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     const bool use_path = path_ok && (c->prm.path_kernel == 2 ||
                                       (c->prm.path_kernel == 0 && !async && call_paths <= PATH_AUTO_MAX));
     const bool path_wide = use_path && c->S.wide != nullptr && c->prm.wide_from == 0;
+    // hybrid batches (khp_ctx_params.path_from): a wavefront render hands the paths still
+    // alive at bounce path_from to one k_path launch, which carries them through the
+    // remaining bounces without a barrier per bounce (not with the light-path variant,
+    // hit sorting, instrumented renders or queue dumps)
+    const uint32_t hyb_from = (!use_path && path_ok && c->prm.path_from > 0 && c->prm.path_from < p->depth)
+                              ? c->prm.path_from : 0u;
+    const bool hyb_wide = hyb_from > 0 && c->S.wide != nullptr && hyb_from >= c->prm.wide_from;
     PathLanes PL{};
     SpillArea sp_path{nullptr, 0};
-    if (use_path) {
+    if (use_path || hyb_from > 0) {
         const size_t lanes = (size_t)c->grid_path * TRAV_BLOCK;
         HIPCHK(w.plane.ensure(lanes * 8 * sizeof(float4)));
         HIPCHK(w.pspill.ensure(lanes * STACK_MAX * sizeof(int4)));
         for (int k = 0; k < 8; ++k) PL.col[k] = w.plane.as<float4>() + (size_t)k * lanes;
         sp_path = SpillArea{w.pspill.as<int4>(), (uint32_t)lanes};
     }
-    const int grid_path = std::max(1, (path_wide ? c->grid_path_w : c->grid_path) / G);
+    const int grid_path = std::max(1, ((path_wide || hyb_wide) ? c->grid_path_w : c->grid_path) / G);
     if (stats) {
         const size_t chunks = (size_t)((P_all + P_chunk - 1) / P_chunk) * ((p->spp + S_chunk - 1) / S_chunk);
         HIPCHK(c->snap.ensure(std::max<size_t>(1, chunks * p->depth) * sizeof(Counters)));
@@ -3984,7 +4026,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
             hipEvent_t done_b = nullptr;  // shadow stage of the previous bounce finished (B)
             bool sorted = false;          // this bounce's queue was regrouped by origin cell (rs_*)
             bool prepped = false;         // this bounce's k_prep was enqueued before the previous fork
-            for (uint32_t b = 0; b < (use_path ? 0u : p->depth); ++b) {
+            const uint32_t b_stop = use_path ? 0u : hyb_from > 0 ? hyb_from : p->depth;   // wavefront bounces
+            for (uint32_t b = 0; b < b_stop; ++b) {
                 const int cur = b & 1;
                 c->cur_bounce = (int)b;
                 Wave Wb = Wv;
@@ -4121,6 +4164,30 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                                           hipMemcpyDeviceToDevice, sA));
                     f.snaps.push_back(Snap{b});
                 }
+            }
+            if (hyb_from > 0) {   // the remaining bounces of the paths in the bounce-hyb_from queue
+                const int cur = hyb_from & 1;
+                Wave Wq = Wv;
+                if (sorted) {   // regrouped: ray columns and state slots as k_extend would take them
+                    const size_t cp = w.cap;
+                    for (int k = 0; k < 3; ++k) {
+                        Wq.qo[cur][k] = w.rs_cols.as<float>() + k * cp;
+                        Wq.qd[cur][k] = w.rs_cols.as<float>() + (3 + k) * cp;
+                    }
+                    Wq.qpid[cur] = w.rs_cols.as<uint32_t>() + 6 * cp;
+                    Wq.qsrc = w.rs_qsrc.as<uint32_t>();
+                }
+                Wq.q_cur = (uint32_t)cur;
+                Wq.q_bounce = hyb_from;
+                if (done_b && sB != sA) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));   // the deferred colour adds
+                if (!prepped) hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, sA, Wv.cnt, w.shqb.as<ShadowQ>() + cur, cur);
+                prepped = false;
+                c->cur_bounce = (int)hyb_from;
+                timed(c, f, 3, true, sA);
+                launch_path(c->S.textured != 0, hyb_wide, (c->bsdf_kinds & ~KINDS_FUR) == 0u, grid_path, sA, c->S, Wq,
+                            sp_path, PL, Ahead{}, true);
+                HIPCHK(hipGetLastError());
+                timed(c, f, 3, false, sA);
             }
             c->cur_bounce = -1;
             if (done_b) HIPCHK(hipStreamWaitEvent(sA, done_b, 0));

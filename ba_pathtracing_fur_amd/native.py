@@ -126,7 +126,7 @@ class CtxParams(ctypes.Structure):
                 ("heavy_iters", c_uint32), ("dump_bounce", c_int32), ("trace_kernels", c_uint32),
                 ("shade_order", c_uint32), ("serial_stages", c_uint32), ("path_order", c_uint32),
                 ("wide_from", c_uint32), ("path_kernel", c_uint32), ("ray_sort_from", c_uint32),
-                ("lds_nodes", c_uint32), ("render_ahead", c_uint32), ("reserved0", c_uint32)]
+                ("lds_nodes", c_uint32), ("render_ahead", c_uint32), ("path_from", c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

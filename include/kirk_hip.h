@@ -342,7 +342,12 @@ typedef struct {
                                     of scene, camera or parameters, drops that work.  Frames, textures and
                                     framebuffers are those of each call alone, bit for bit.  Measured in
                                     DESIGN.md §5b                                                          */
-    uint32_t reserved0;          /* 0 */
+    uint32_t path_from;          /* ABI 13: 0 (default) or b >= 1: a wavefront render hands the paths still
+                                    alive at bounce b to ONE path-kernel launch (k_path), which carries them
+                                    through the remaining bounces without a barrier per bounce -- the last
+                                    bounces' launches are short and end with their slowest ray.  Not with the
+                                    light-path variant, hit sorting, instrumented renders or queue dumps;
+                                    >= depth: off.  No value changes a pixel.  Measured in DESIGN.md §5d   */
 } khp_ctx_params;   /* 64 bytes */
 
 /* ---- context --------------------------------------------------------------- */
