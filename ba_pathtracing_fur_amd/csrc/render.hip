@@ -5097,6 +5097,60 @@ extern "C" khp_status khp_comm_set_timeout(khp_ctx* c, uint32_t timeout_ms) {
     return KHP_OK;
 }
 
+// khp_debug_comm_wait's gate: one wave spins (sleeping) until the host sets *flag,
+// or for at most max_ticks of the 100 MHz clock, so it always ends.
+__global__ void k_gate(const volatile uint32_t* flag, unsigned long long max_ticks) {
+    const unsigned long long t0 = wall_clock64();
+    while (*flag == 0u && wall_clock64() - t0 < max_ticks) __builtin_amdgcn_s_sleep(64);
+}
+
+extern "C" khp_status khp_debug_comm_wait(khp_ctx* c, int scenario, uint32_t bound_ms, uint32_t release_ms,
+                                          double* waited_ms) {
+    if (!c || !waited_ms || scenario < 0 || scenario > 2 || bound_ms == 0) return fail(KHP_EINVAL, "bad arguments");
+    if (c->comm) return fail(KHP_EINVAL, "khp_debug_comm_wait: the context has a communicator");
+    HIPCHK(hipSetDevice(c->device));
+    KHPCHK(drain(c));
+    uint32_t* flag = nullptr;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&flag), sizeof(uint32_t), hipHostMallocCoherent));
+    *flag = 0u;
+    const std::string dead_before = c->comm_dead;
+    const uint32_t bound_before = c->comm_timeout_ms;
+    c->comm_dead = "khp_debug_comm_wait";   // waits are bounded as after a communicator's abort
+    c->comm_timeout_ms = bound_ms;
+    auto gate = [&]() { hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, c->stream, flag, 1000000000ull); };
+    hipError_t e = hipSuccess;
+    if (scenario == 0) {
+        gate();
+        e = comm_op_begin(c);
+        if (e == hipSuccess) e = comm_op_end(c);
+    } else if (scenario == 1) {
+        e = comm_op_begin(c);
+        gate();
+        if (e == hipSuccess) e = comm_op_end(c);
+    } else {
+        e = comm_op_begin(c);
+        gate();
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    std::thread rel([flag, release_ms] {
+        std::this_thread::sleep_for(std::chrono::milliseconds(release_ms));
+        __atomic_store_n(flag, 1u, __ATOMIC_RELEASE);
+    });
+    khp_status st = e == hipSuccess ? wait_stream(c, c->stream, "the test gate")
+                                    : fail(KHP_EDEVICE, std::string("hipEventRecord: ") + hipGetErrorString(e));
+    *waited_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const std::string msg = st == KHP_OK ? std::string() : last_error();
+    rel.join();
+    (void)hipStreamSynchronize(c->stream);   // the gate has ended (released)
+    while (comm_op_pending(c)) {}            // every bracket completed: retire them
+    c->comm_ops.clear();
+    c->comm_dead = dead_before;
+    c->comm_timeout_ms = bound_before;
+    (void)hipHostFree(flag);
+    if (st != KHP_OK) return fail(st, msg);
+    return KHP_OK;
+}
+
 static void leave_local_group(khp_ctx* c) {
     if (c->lgroup)
         for (auto& m : *c->lgroup)

@@ -170,7 +170,7 @@ EXPORTED = ["khp_create", "khp_destroy", "khp_last_error", "khp_abi_version", "k
             "khp_sync", "khp_ctx_params_defaults", "khp_set_params", "khp_get_params", "khp_debug_shadow_queue",
             "khp_bdpt_params_defaults", "khp_set_bdpt", "khp_get_bdpt", "khp_gather_plan",
             "khp_read_rgba8_async", "khp_snapshot_wait", "khp_comm_init_local", "khp_comm_set_timeout",
-            "khp_tonemap_log_sum", "khp_set_camera"]
+            "khp_tonemap_log_sum", "khp_set_camera", "khp_debug_comm_wait"]
 
 # the include/kirk_hip.h this module mirrors (load_library refuses another)
 ABI_VERSION = 13
@@ -215,6 +215,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         "khp_bdpt_params_defaults": (None, [P(BdptParams)]),
         "khp_set_bdpt": (c_int, [c_void_p, P(BdptParams)]),
         "khp_set_camera": (c_int, [c_void_p, P(Camera)]),
+        "khp_debug_comm_wait": (c_int, [c_void_p, c_int, c_uint32, c_uint32, P(c_double)]),
         "khp_get_bdpt": (c_int, [c_void_p, P(BdptParams)]),
         "khp_read_framebuffer": (c_int, [c_void_p, P(c_float)]),
         "khp_read_rgba8": (c_int, [c_void_p, P(Tonemap), P(c_uint8)]),

@@ -587,6 +587,18 @@ khp_status khp_debug_queue(khp_ctx* ctx, uint32_t* n, float* orig, float* dir);
 /* The same render's shadow rays of bounce b as k_shadow traces them (after the
  * zero-colour skip): origin, direction ([n][3]) and t_max ([n]). */
 khp_status khp_debug_shadow_queue(khp_ctx* ctx, uint32_t* n, float* orig, float* dir, float* tmax);
+/* ABI 13, test hook for the bounded device waits of a rank: builds
+ * one RCCL-operation bracket (events `pre` / `post`, as around an ncclSend /
+ * ncclRecv) on the context stream around a gate kernel that spins until
+ * `release_ms` after the call starts (or 10 s), then waits for the stream with
+ * the bound `bound_ms` as khp_sync would on a rank.  scenario 0: the gate
+ * before `pre` (the operation never became runnable: no timeout); 1: the gate
+ * between `pre` and `post` (runnable, not completing: KHP_EDEVICE after the
+ * bound); 2: `pre` only, no `post` (retired once `pre` completes, then no
+ * timeout).  *waited_ms: the wait's wall time.  The context keeps no
+ * communicator state afterwards.  No RCCL call is made. */
+khp_status khp_debug_comm_wait(khp_ctx* ctx, int scenario, uint32_t bound_ms, uint32_t release_ms,
+                               double* waited_ms);
 
 /* ---- registries / host helpers --------------------------------------------- */
 /* BsdfFactory::getBsdf / ShaderFactory::getShader by KIRK name; -1 if unknown

@@ -323,6 +323,33 @@ def test_rccl_init_without_peer_fails_with_a_status():
     assert r.returncode == 0 and "NO_PEER_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
 
 
+def test_bounded_waits_count_only_runnable_rccl_time(hip_ctx):
+    """ADVICE r05 (comm_op_pending / poll_wait, ADVICE r04's rule): a rank's device
+    wait is bounded only by the time its oldest RCCL operation has been runnable
+    without completing.  khp_debug_comm_wait brackets a gate kernel (released by
+    the host after `release` ms) with an operation's pre/post events: an operation
+    whose `pre` is still pending never times out; a runnable one whose `post` does
+    not complete fails after the bound; one with no `post` is retired once `pre`
+    completes, and the wait on the compute behind it is not bounded."""
+    import ctypes
+    from ba_pathtracing_fur_amd import native as N
+    lib, waited = hip_ctx.lib, ctypes.c_double(0.0)
+
+    def run(scenario, bound, release):
+        return lib.khp_debug_comm_wait(hip_ctx.ptr, scenario, bound, release, ctypes.byref(waited))
+
+    assert run(0, 20, 200) == N.KHP_OK and waited.value >= 150, waited.value     # pending pre: no timeout
+    st = run(1, 20, 400)                                                          # runnable, not completing
+    assert st == N.KHP_EDEVICE and 15 <= waited.value < 300, (st, waited.value)
+    assert "not complete" in (lib.khp_last_error() or b"").decode() or "still running" in (
+        lib.khp_last_error() or b"").decode()
+    assert run(2, 20, 200) == N.KHP_OK and waited.value >= 150, waited.value     # no post: retired at pre
+    sd = S.config2(32, 24, n_strands=100)                                         # the context still renders
+    hip_ctx.set_scene(sd)
+    hip_ctx.build_accel()
+    assert hip_ctx.render(32, 24, 1, 5).shape == (24, 32, 3)
+
+
 def test_local_group_refuses_out_of_order_gathers():
     """khp_comm_init_local's stamped ring slots (ABI 11): a root gather enqueued
     before its sender's returns KHP_ENOTREADY and can be repeated; a sender 64
