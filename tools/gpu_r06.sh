@@ -51,5 +51,17 @@ for r in (1, 2):
         print(r, v, d["value"], "frac", rl["frac"], "b-ms", [b["ms_per_frame"] for b in rl["per_bounce"]])
 PY
   ;;
+knobs)  # the driver's bench shape with bench.py flag sets $3.. (each a quoted string), alternated twice
+  shift 2
+  for r in 1 2; do
+    i=0
+    for k in "$@"; do
+      timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --sync-check-steps 0 --gui-steps 0 --iso-steps 0 $k > gpurun_out/$T/k${i}_$r.json 2> gpurun_out/$T/k${i}_$r.log || exit 1
+      d=$(python -c "import json,sys; d=json.loads(open('gpurun_out/$T/k${i}_$r.json').read().strip().splitlines()[-1]); rl=d['roofline']; print(d['value'], rl['frac'], [b['ms_per_frame'] for b in rl['per_bounce']])")
+      echo "$r [$k] $d" | tee -a gpurun_out/$T/knobs.txt
+      i=$((i+1))
+    done
+  done
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
