@@ -2741,6 +2741,22 @@ struct khp_ctx {
         uint32_t* hst = nullptr;     // pinned: AheadState::report of the current call
         bool counted = false;        // hst was filled by the current call
     } ra;
+    // render-ahead through fusion (the wavefront's synchronous calls): a call that
+    // continues its progressive series renders the next render_ahead calls' passes in
+    // the same fused batch; their colours stay in ps[0]'s colour column until those
+    // calls accumulate them (wave_ahead_hit).  Any other use of ps[0] drops the batch.
+    struct WaveAhead {
+        bool valid = false;
+        khp_render_params next{};    // the call whose pass is the batch's next frame
+        uint64_t gen = 0;
+        Wave Wv{};                   // the batch's view: colour column, pixel list, frames' first samples
+        uint32_t nf = 0, used = 0;   // frames in the batch, frames accumulated so far
+    } wa;
+    struct {   // the last synchronous single-pass call, first_sample advanced by its spp
+        bool valid = false;
+        khp_render_params next{};
+        uint64_t gen = 0;
+    } series;
 };
 constexpr size_t LG_SLOTS = 64;
 
@@ -3736,6 +3752,43 @@ static void ahead_commit(khp_ctx* c, const khp_render_params* p, size_t npaths) 
     ra.npaths = npaths;
 }
 
+// Render-ahead through fusion: the synchronous call p is the next frame of the
+// batch an earlier call of its series rendered (same scene, camera, parameters,
+// pixels, spp, depth, seed; first_sample = that call's + j spp).  Its paths are
+// done; the call only folds their colours into the running mean (k_accumulate
+// of frame j, the kernel a fused batch runs per frame) -- the framebuffer is the
+// one the call renders alone, bit for bit.
+static khp_status wave_ahead_hit(khp_ctx* c, const khp_render_params* p, float* out_rgb) {
+    khp_ctx::WaveAhead& wa = c->wa;
+    const uint32_t P = wa.Wv.P;
+    hipEvent_t e0 = next_event(c), e1 = next_event(c);
+    (void)hipEventRecord(e0, c->stream);
+    if (c->fb_evt) HIPCHK(hipStreamWaitEvent(c->stream, c->fb_evt, 0));
+    hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, c->stream, wa.Wv, c->fb.as<float>(), wa.used);
+    HIPCHK(hipGetLastError());
+    (void)hipEventRecord(e1, c->stream);
+    ++wa.used;
+    wa.next.first_sample = p->first_sample + p->spp;
+    if (wa.used >= wa.nf) wa.valid = false;
+    if (out_rgb && !(p->flags & KHP_RENDER_NO_READBACK)) {
+        hipMemcpyKind kind = (p->flags & KHP_RENDER_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        HIPCHK(hipMemcpyAsync(out_rgb, c->fb.p, (size_t)p->width * p->height * 3 * sizeof(float), kind, c->stream));
+    }
+    KHPCHK(wait_stream(c, c->stream, "a synchronous frame"));
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) c->st.render_ms = ms;
+    c->st.other_ms = ms;
+    c->ev_next = 0;
+    c->st.frames = 1;
+    c->st.ahead_finished = (uint64_t)P * p->spp;
+    c->report_open = false;
+    c->series.valid = true;
+    c->series.next = *p;
+    c->series.next.first_sample = p->first_sample + p->spp;
+    c->series.gen = c->gen;
+    return KHP_OK;
+}
+
 static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* out_rgb,
                                  const std::vector<PendingOp>* ops) {
     khp_status s;
@@ -3749,7 +3802,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     } else {
         fs0.push_back(p->first_sample);
     }
-    const uint32_t nf = (uint32_t)fs0.size();
+    uint32_t nf = (uint32_t)fs0.size();
     const size_t npix = (size_t)p->width * p->height;
     uint32_t T = p->tile_size ? p->tile_size : 64;
     uint32_t nranks = p->tile_nranks > 1 ? p->tile_nranks : 1;
@@ -3766,6 +3819,15 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     }
     if (!async) report_begin(c);
     else if (!c->report_open) report_begin(c);
+    // render-ahead through fusion (c->wa): a synchronous single pass that an earlier
+    // call already rendered only accumulates; every other render drops the batch
+    const bool sync1 = !async && !ops && nf == 1;
+    const bool continues = sync1 && c->series.valid && c->series.gen == c->gen && ahead_key_equal(c->series.next, *p);
+    c->series.valid = false;
+    if (sync1 && !stats && c->wa.valid && c->wa.gen == c->gen && ahead_key_equal(c->wa.next, *p) && c->fb.p &&
+        c->fbW == p->width && c->fbH == p->height)
+        return wave_ahead_hit(c, p, out_rgb);
+    c->wa.valid = false;
     if (c->fbW != p->width || c->fbH != p->height || !c->fb.p) {
         HIPCHK(c->fb.ensure(npix * 3 * sizeof(float)));
         HIPCHK(hipMemsetAsync(c->fb.p, 0, npix * 3 * sizeof(float), c->stream));
@@ -3794,7 +3856,6 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     f.sync_next = 0;
     f.launches.clear();
     f.snaps.clear();
-    f.nf = nf;
     const int G = async ? F : 1;
     const int grid_ext = std::max(1, c->grid_ext / G), grid_sh = std::max(1, c->grid_sh / G);
     const int grid_sh_w = std::max(1, c->grid_sh_w / G);
@@ -3807,6 +3868,30 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     const bool bdm = c->bd.enabled != 0 && c->S.n_lights > 0;
     const uint32_t sh_per_path = bdm ? c->bd.vertices : 1u;
     const size_t cap_paths = std::max<size_t>(4096 / sh_per_path, chunk_paths(c) / sh_per_path);
+    const int dump_b = (!async && !ops) ? c->prm.dump_bounce : -1;
+    // the path kernel (khp_ctx_params.path_kernel): automatic for synchronous renders of at
+    // most PATH_AUTO_MAX paths.  At the metric row a synchronous call of s spp takes
+    // 8.0 / 12.5 / 16.7 / 20.8 / 29.4 / 37.6 ms through it for s = 1 / 2 / 3 / 4 / 6 / 8
+    // against 14.0 / 17.9 / 21.4 / 24.7 / 31.2 / 37.2 through the wavefront
+    // (profiles/r04aa_sync_spp.json): the wavefront's better steady rate wins from ~7.5 spp
+    constexpr size_t PATH_AUTO_MAX = (size_t)14 << 20;
+    const bool path_ok = !stats && !bdm && c->prm.shade_order == 0 && dump_b < 0;
+    // render-ahead through fusion: a synchronous wavefront call that continues its series
+    // (the previous synchronous call was its pass with first_sample - spp) renders itself and
+    // the next render_ahead calls' passes as one fused batch of one chunk, accumulates its own
+    // frame and leaves the others' colours for those calls (8-spp calls at the metric row:
+    // a batch of 3 passes costs 28.6 ms per pass against 36.8 alone, tools/fuse_probe.py)
+    uint32_t wa_frames = 1;
+    if (continues && c->prm.render_ahead != 0 && !stats && !bdm && dump_b < 0 && P_all > 0) {
+        const size_t one = (size_t)P_all * p->spp;
+        const bool wavefront = !(path_ok && (c->prm.path_kernel == 2 ||
+                                             (c->prm.path_kernel == 0 && one <= PATH_AUTO_MAX)));
+        const uint32_t F = 1u + std::min<uint32_t>(c->prm.render_ahead, RA_MAX_SETS - 1);
+        if (wavefront && one * F <= cap_paths && F <= KHP_MAX_FUSE) wa_frames = F;
+    }
+    for (uint32_t q = 1; q < wa_frames; ++q) fs0.push_back(p->first_sample + q * p->spp);
+    nf = (uint32_t)fs0.size();
+    f.nf = nf;
     uint32_t P_chunk, S_chunk;
     if (nf > 1) {
         P_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(std::max<uint32_t>(1, P_all),
@@ -3849,7 +3934,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     // first full batch does not allocate
     // (automatic chunks may reach 5/4 of the cap, see above)
     size_t want = (size_t)P_chunk * S_chunk * nf;
-    if (nf > 1) {
+    if (ops && nf > 1) {
         const uint32_t fuse = std::max<uint32_t>(1, std::min<uint32_t>(c->prm.fuse_frames, KHP_MAX_FUSE));
         want = std::max(want, std::min<size_t>(chunk_most(c) / sh_per_path, (size_t)P_all * S_chunk * fuse));
     }
@@ -3874,14 +3959,6 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         }
         HIPCHK(w.lvb.ensure(lv_bytes));
     }
-    const int dump_b = (!async && !ops) ? c->prm.dump_bounce : -1;
-    // the path kernel (khp_ctx_params.path_kernel): automatic for synchronous renders of at
-    // most PATH_AUTO_MAX paths.  At the metric row a synchronous call of s spp takes
-    // 8.0 / 12.5 / 16.7 / 20.8 / 29.4 / 37.6 ms through it for s = 1 / 2 / 3 / 4 / 6 / 8
-    // against 14.0 / 17.9 / 21.4 / 24.7 / 31.2 / 37.2 through the wavefront
-    // (profiles/r04aa_sync_spp.json): the wavefront's better steady rate wins from ~7.5 spp
-    constexpr size_t PATH_AUTO_MAX = (size_t)14 << 20;
-    const bool path_ok = !stats && !bdm && c->prm.shade_order == 0 && dump_b < 0;
     const size_t call_paths = (size_t)P_all * p->spp * nf;
     const bool use_path = path_ok && (c->prm.path_kernel == 2 ||
                                       (c->prm.path_kernel == 0 && !async && call_paths <= PATH_AUTO_MAX));
@@ -4199,7 +4276,9 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
             bool only_renders = true;
             if (ops)
                 for (const PendingOp& o : *ops) only_renders = only_renders && o.kind == PendingOp::RENDER;
-            if ((!ops || only_renders) && ns <= ACC_MAX_SAMPLES) {
+            if (wa_frames > 1) {   // this call's frame; the later frames wait for their calls
+                hipLaunchKernelGGL(k_accumulate, dim3((P + 255) / 256), dim3(256), 0, sA, Wv, c->fb.as<float>(), 0u);
+            } else if ((!ops || only_renders) && ns <= ACC_MAX_SAMPLES) {
                 hipLaunchKernelGGL(k_accumulate_all, dim3((P + ACC_PIX - 1) / ACC_PIX), dim3(ACC_PIX),
                                    ACC_PIX * (ns + 1) * sizeof(float4), sA, Wv, c->fb.as<float>());
             } else if (!ops) {
@@ -4241,6 +4320,15 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         }
         if (c->fb_evt) HIPCHK(hipStreamWaitEvent(sA, c->fb_evt, 0));
     }
+    if (wa_frames > 1) {
+        c->wa.valid = true;
+        c->wa.next = *p;
+        c->wa.next.first_sample = p->first_sample + p->spp;
+        c->wa.gen = c->gen;
+        c->wa.Wv = Wv;
+        c->wa.nf = wa_frames;
+        c->wa.used = 1;
+    }
     // join: the batch is done when its last chunk has accumulated
     hipEvent_t e_end = slot_event(f.sync_pool, f.sync_next, true);
     HIPCHK(hipEventRecord(e_end, sA));
@@ -4266,6 +4354,12 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
         c->ra.counted = false;
     }
     c->report_open = false;
+    if (sync1) {
+        c->series.valid = true;
+        c->series.next = *p;
+        c->series.next.first_sample = p->first_sample + p->spp;
+        c->series.gen = c->gen;
+    }
     return KHP_OK;
 }
 
@@ -4890,6 +4984,7 @@ static khp_status trace_persistent_run(khp_ctx* c, uint32_t n, const float* orig
                                        uint8_t* hit_out) {
     const bool shadow = hit_out != nullptr;
     PathSet& w = c->ps[0];
+    c->wa.valid = false;   // the batch query API reuses ps[0]
     khp_status s = ensure_wave(c, w, n);
     if (s != KHP_OK) return s;
     DevMem o, d, tm, t, ob, uv;

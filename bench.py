@@ -16,7 +16,10 @@ framebuffer stays in HBM.  Steps are enqueued asynchronously (KHP_RENDER_ASYNC)
 and consecutive passes with equal parameters are fused into one wavefront
 (khp_ctx_params.fuse_frames, default 32); the timed region ends with khp_sync +
 a barrier, so every pass is complete.  `sync_steps` in the JSON line is the
-same workload with a host wait after every pass (no fusion, no overlap).
+same workload with a host wait after every pass (KIRK's synchronous call):
+one untimed call starts the series, then 12 calls are timed (with render-ahead
+a call renders its pass and the next two as one batch and the two later calls
+only accumulate, so 12 calls are 4 whole batches).
 
 --gpus N: one process per GPU.  Under torchrun (WORLD_SIZE set) each rank
 renders the 64x64 tiles t with t % N == rank and every step ends with the RCCL
@@ -82,8 +85,9 @@ def parse():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--tile", type=int, default=64)
-    ap.add_argument("--sync-check-steps", type=int, default=4,
-                    help="passes timed with a host wait after each (the sync_steps field; 0: skip)")
+    ap.add_argument("--sync-check-steps", type=int, default=12,
+                    help="passes timed with a host wait after each (the sync_steps field; 0: skip), after one "
+                         "untimed call that starts the series")
     ap.add_argument("--fuse", type=int, default=None, help="khp_ctx_params.fuse_frames (default: the library's)")
     ap.add_argument("--chunk-paths", type=int, default=None, help="khp_ctx_params.chunk_paths")
     ap.add_argument("--frames-in-flight", type=int, default=None, help="khp_ctx_params.frames_in_flight")
@@ -439,18 +443,28 @@ def main():
     # the same workload with a host wait after every pass (no fusion, no overlap)
     sync_line = None
     if args.sync_check_steps > 0:
+        step(async_=False)   # the series' first call (untimed): render-ahead starts with the second
+        frame.sync()
         frame.barrier()
+        calls, ahead = [], []
         t1 = time.perf_counter()
         for _ in range(args.sync_check_steps):
+            tc = time.perf_counter()
             step(async_=False)
+            ahead.append(ctx.stats()["ahead_finished"])   # before khp_sync opens a new report
             frame.sync()
+            calls.append(round((time.perf_counter() - tc) * 1e3, 3))
         frame.barrier()
         sync_el = frame.max_over_ranks(time.perf_counter() - t1)
         sync_line = {"value": round(args.sync_check_steps * samples_per_step / sync_el / 1e6, 3),
                      "ms_per_step": round(sync_el / args.sync_check_steps * 1e3, 3), "steps": args.sync_check_steps,
-                     "def": "one synchronous khp_render per pass (+ gather), no frame fusion; synchronous renders "
-                            f"run the path kernel up to 14 x 2^20 paths per call and the wavefront above "
-                            f"(khp_ctx_params.path_kernel = {params['path_kernel']}, 0 = automatic)"}
+                     "call_ms": calls, "paths_finished_ahead": ahead,
+                     "def": "one synchronous khp_render per pass (+ gather), consecutive first_sample, after one "
+                            "untimed call; synchronous renders run the path kernel up to 14 x 2^20 paths per call "
+                            f"and the wavefront above (khp_ctx_params.path_kernel = {params['path_kernel']}, "
+                            f"0 = automatic), render_ahead = {params.get('render_ahead', 0)} (a wavefront call "
+                            "that continues the series renders its pass and the next render_ahead passes as one "
+                            "fused batch; those calls only accumulate: call_ms, paths_finished_ahead)"}
 
     # KIRK's GUI pattern (CPU_PathTracer.cpp:17-52): every
     # render() call adds ONE sample to every pixel synchronously and the viewer

@@ -257,8 +257,9 @@ typedef struct {
     double shadow_finish_ms;
     uint64_t shadow_launches;
     /* ABI 13: render-ahead (khp_ctx_params.render_ahead), last synchronous render:
-     * its paths the previous call had already finished, and those it resumed from
-     * that call's park records (0 when the call had nothing rendered ahead) */
+     * its paths earlier calls had already finished (all of them when an earlier
+     * wavefront call's fused batch held its pass), and those it resumed from park
+     * records (0 when the call had nothing rendered ahead) */
     uint64_t ahead_finished, ahead_resumed;
 } khp_stats;
 #define KHP_MAX_BOUNCE_STATS 16
@@ -339,9 +340,12 @@ typedef struct {
                                     paths end (at once when earlier calls finished them all); the paths of
                                     later calls in flight then are parked and resumed by later calls, which
                                     accumulate the colours already finished.  Any other call, and any change
-                                    of scene, camera or parameters, drops that work.  Frames, textures and
-                                    framebuffers are those of each call alone, bit for bit.  Measured in
-                                    DESIGN.md §5b                                                          */
+                                    of scene, camera or parameters, drops that work.  A synchronous render
+                                    that runs the wavefront (one chunk) and continues the series of the
+                                    previous synchronous call renders its own pass and the next render_ahead
+                                    calls' passes as one fused batch; those calls then only accumulate.
+                                    Frames, textures and framebuffers are those of each call alone, bit for
+                                    bit.  Measured in DESIGN.md §5c                                        */
     uint32_t path_from;          /* ABI 13: 0 (default) or b >= 1: a wavefront render hands the paths still
                                     alive at bounce b to ONE path-kernel launch (k_path), which carries them
                                     through the remaining bounces without a barrier per bounce -- the last

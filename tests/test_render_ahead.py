@@ -212,3 +212,125 @@ def test_gui_calls_full_size(metric_scene_oracle):
         metric_scene_oracle.render(W, H, 1, D, first_sample=k, threads=16, rows=rows, out=want)
     idx = list(range(*rows))
     assert_parity(frames[1][0][3][idx], want[idx], exact=True)
+
+
+# ---- render-ahead through fusion: the wavefront's synchronous calls -------------------------
+
+
+@pytest.mark.parametrize("name,kw,w,h,depth", SCENES, ids=[s[0] for s in SCENES])
+@pytest.mark.parametrize("spp,ahead_sets", [(2, 2), (3, 1), (1, 3)])
+def test_wavefront_series_match_oracle(name, kw, w, h, depth, spp, ahead_sets):
+    """Synchronous wavefront calls (path_kernel 1) first_sample = 0, spp, ...:
+    the series' second call renders itself and the next ahead_sets calls' passes
+    as one fused batch, those calls only accumulate (khp_stats.ahead_finished =
+    all their paths), then the next call renders a batch again -- and every
+    call's framebuffer and texture are the oracle's progressive ones."""
+    sd = S.build_config(name, width=w, height=h, **kw)
+    ser = _Series(sd, w, h, depth)
+    ctx = HipContext(0)
+    try:
+        ctx.set_scene(sd)
+        ctx.build_accel()
+        ctx.set_params(path_kernel=1, render_ahead=ahead_sets)
+        ahead = []
+        calls = 2 + 2 * (ahead_sets + 1)
+        for k in range(calls):
+            ctx.render(w, h, spp, depth, first_sample=k * spp, readback=False)
+            ahead.append(ctx.stats()["ahead_finished"])
+            ser.call(spp, k * spp)
+            _check(ctx, ser, w, h, f"call {k}")
+        n = w * h * spp
+        group = [0] + [n] * ahead_sets
+        assert ahead == [0] + group * 2 + [0], ahead
+    finally:
+        ctx.close()
+
+
+def test_wavefront_changes_between_calls_drop_the_batch():
+    """Between wavefront calls whose batch holds later passes: a camera move, a
+    parameter change, a skipped and a repeated first_sample, another spp, a
+    fused asynchronous pass, a path-kernel call and a batch ray query (which
+    reuses the batch's path set) -- each call's frame is the oracle's series,
+    which a stale batch would break."""
+    w, h, depth = 64, 48, 5
+    sd = S.config2(w, h, n_strands=2000)
+    ser = _Series(sd, w, h, depth)
+    ctx = HipContext(0)
+    rng = np.random.default_rng(7)
+    try:
+        ctx.set_scene(sd)
+        ctx.build_accel()
+        ctx.set_params(path_kernel=1, trace_kernels=2, render_ahead=3)
+        plan = [("call", 2, 0), ("call", 2, 2), ("call", 2, 4), ("camera", (0.05, 0.0, -0.1)), ("call", 2, 6),
+                ("call", 2, 8), ("call", 2, 10), ("params", dict(wide_from=0)), ("call", 2, 12), ("call", 2, 14),
+                ("call", 2, 16), ("call", 2, 20), ("call", 2, 22), ("call", 2, 24), ("call", 2, 24), ("call", 2, 26),
+                ("call", 2, 28), ("call", 1, 30), ("call", 2, 31), ("call", 2, 33), ("async", 2, 35), ("call", 2, 37),
+                ("call", 2, 39), ("call", 2, 41), ("pathk", 2, 43), ("call", 2, 45), ("call", 2, 47), ("call", 2, 49),
+                ("query",), ("call", 2, 51), ("call", 2, 53), ("call", 2, 55)]
+        hits = 0
+        for step in plan:
+            kind = step[0]
+            if kind == "camera":
+                cam = _moved(sd.cam, step[1])
+                ctx.set_camera(cam)
+                ser.camera(cam)
+                continue
+            if kind == "params":
+                ctx.set_params(**step[1])
+                continue
+            if kind == "query":
+                o = np.tile(np.asarray(sd.cam.position, np.float32), (4096, 1))
+                d = rng.normal(size=(4096, 3)).astype(np.float32)
+                d /= np.linalg.norm(d, axis=1, keepdims=True)
+                ctx.trace_closest(o, d)
+                continue
+            spp, fs = step[1], step[2]
+            if kind == "async":
+                ctx.render(w, h, spp, depth, first_sample=fs, async_=True)
+                ctx.sync()
+            elif kind == "pathk":
+                ctx.set_params(path_kernel=2)
+                ctx.render(w, h, spp, depth, first_sample=fs, readback=False)
+                ctx.set_params(path_kernel=1)
+            else:
+                ctx.render(w, h, spp, depth, first_sample=fs, readback=False)
+                hits += ctx.stats()["ahead_finished"] == w * h * spp
+            ser.call(spp, fs)
+            _check(ctx, ser, w, h, str(step))
+        assert hits >= 4, hits
+    finally:
+        ctx.close()
+
+
+def test_wavefront_calls_full_size(metric_scene_oracle):
+    """The metric scene at 1080p, 8-spp synchronous calls (the automatic choice
+    runs them through the wavefront): six calls with render-ahead (the default)
+    equal the same calls without it bit for bit, calls 2 and 3 found their pass
+    in call 1's batch, and every 54th row of the last frame is the oracle's."""
+    W, H, D, SPP = 1920, 1080, 5, 8
+    frames, ahead = {}, []
+    for ra in (2, 0):
+        ctx = HipContext(0)
+        try:
+            S.config3_device(ctx, W, H, n_strands=1_000_000)
+            ctx.build_accel()
+            ctx.set_params(render_ahead=ra)
+            fbs = []
+            for k in range(6):
+                ctx.render(W, H, SPP, D, first_sample=k * SPP, readback=False)
+                if ra:
+                    ahead.append(ctx.stats()["ahead_finished"])
+                fbs.append(ctx.read_framebuffer(W, H))
+            frames[ra] = fbs
+        finally:
+            ctx.close()
+    for k in range(6):
+        assert np.array_equal(frames[2][k].view(np.uint32), frames[0][k].view(np.uint32)), k
+    n = W * H * SPP
+    assert ahead == [0, 0, n, n, 0, n], ahead
+    rows = (13, 1080, 54)
+    want = np.zeros((H, W, 3), np.float32)
+    for k in range(6):
+        metric_scene_oracle.render(W, H, SPP, D, first_sample=k * SPP, threads=16, rows=rows, out=want)
+    idx = list(range(*rows))
+    assert_parity(frames[2][5][idx], want[idx], exact=True)

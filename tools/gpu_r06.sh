@@ -63,5 +63,15 @@ knobs)  # the driver's bench shape with bench.py flag sets $3.. (each a quoted s
     done
   done
   ;;
+fuse)   # fused-batch rate of F consecutive 8-spp passes (tools/fuse_probe.py), twice
+  for r in 1 2; do
+    timeout -k 10 300 python -u tools/fuse_probe.py 6 ${3:-1,2,3,4} >> gpurun_out/$T/fuse_probe.jsonl 2>> gpurun_out/$T/fuse_probe.log || exit 1
+  done
+  ;;
+wra)    # render-ahead through fusion: its tests, the synchronous-call parity tests, then the bench's sync line
+  KHP_NO_BUILD=1 timeout -k 10 700 $PYT tests/test_render_ahead.py > gpurun_out/$T/tests_ra.log 2>&1 || exit 1
+  KHP_NO_BUILD=1 timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "progressive or ray_sorting or wide_records or chunked or fused" > gpurun_out/$T/tests_par.log 2>&1 || exit 1
+  timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --gui-steps 0 --iso-steps 0 > gpurun_out/$T/bench_sync.json 2> gpurun_out/$T/bench_sync.log || exit 1
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
