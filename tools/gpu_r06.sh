@@ -68,6 +68,11 @@ fuse)   # fused-batch rate of F consecutive 8-spp passes (tools/fuse_probe.py), 
     timeout -k 10 300 python -u tools/fuse_probe.py 6 ${3:-1,2,3,4} >> gpurun_out/$T/fuse_probe.jsonl 2>> gpurun_out/$T/fuse_probe.log || exit 1
   done
   ;;
+fuse1)  # the GUI call's pass (1 spp): fused batches through the path kernel and the wavefront, and single calls
+  timeout -k 10 200 python -u tools/fuse_probe.py 8 1 1 2 2 >> gpurun_out/$T/fuse1.jsonl 2>> gpurun_out/$T/fuse1.log || exit 1
+  timeout -k 10 200 python -u tools/fuse_probe.py 8 1,2,3,4,6,8 1 2 0 >> gpurun_out/$T/fuse1.jsonl 2>> gpurun_out/$T/fuse1.log || exit 1
+  timeout -k 10 200 python -u tools/fuse_probe.py 8 3,4,6,8 1 1 0 >> gpurun_out/$T/fuse1.jsonl 2>> gpurun_out/$T/fuse1.log || exit 1
+  ;;
 wra)    # render-ahead through fusion: its tests, the synchronous-call parity tests, then the bench's sync line
   KHP_NO_BUILD=1 timeout -k 10 700 $PYT tests/test_render_ahead.py > gpurun_out/$T/tests_ra.log 2>&1 || exit 1
   KHP_NO_BUILD=1 timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "progressive or ray_sorting or wide_records or chunked or fused" > gpurun_out/$T/tests_par.log 2>&1 || exit 1
