@@ -73,6 +73,22 @@ fuse1)  # the GUI call's pass (1 spp): fused batches through the path kernel and
   timeout -k 10 200 python -u tools/fuse_probe.py 8 1,2,3,4,6,8 1 2 0 >> gpurun_out/$T/fuse1.jsonl 2>> gpurun_out/$T/fuse1.log || exit 1
   timeout -k 10 200 python -u tools/fuse_probe.py 8 3,4,6,8 1 1 0 >> gpurun_out/$T/fuse1.jsonl 2>> gpurun_out/$T/fuse1.log || exit 1
   ;;
+envab)  # the driver's bench shape with environment settings $3.. (each a quoted string, "-" = none), alternated twice
+  shift 2
+  for r in 1 2; do
+    i=0
+    for e in "$@"; do
+      E=$e; [ "$E" = "-" ] && E=""
+      env $E timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --sync-check-steps 0 --gui-steps 0 --iso-steps 0 > gpurun_out/$T/e${i}_$r.json 2> gpurun_out/$T/e${i}_$r.log || exit 1
+      d=$(python -c "import json,sys; d=json.loads(open('gpurun_out/$T/e${i}_$r.json').read().strip().splitlines()[-1]); rl=d['roofline']; fr=d['frame']; print(d['value'], rl['frac'], [b['ms_per_frame'] for b in rl['per_bounce']], fr['device_ms'], fr['shade_ms'])")
+      echo "$r [$e] $d" | tee -a gpurun_out/$T/envab.txt
+      i=$((i+1))
+    done
+  done
+  ;;
+partests)  # the wavefront/path-kernel parity suites (render-ahead, hybrid, parity)
+  KHP_NO_BUILD=1 timeout -k 10 900 $PYT tests/test_gpu_parity.py tests/test_render_ahead.py tests/test_hybrid_batches.py > gpurun_out/$T/tests_par.log 2>&1 || exit 1
+  ;;
 wra)    # render-ahead through fusion: its tests, the synchronous-call parity tests, then the bench's sync line
   KHP_NO_BUILD=1 timeout -k 10 700 $PYT tests/test_render_ahead.py > gpurun_out/$T/tests_ra.log 2>&1 || exit 1
   KHP_NO_BUILD=1 timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "progressive or ray_sorting or wide_records or chunked or fused" > gpurun_out/$T/tests_par.log 2>&1 || exit 1
