@@ -2929,7 +2929,8 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->path_kernel = 0;       // automatic: k_path for synchronous renders
     out->ray_sort_from = 0;     // automatic: bounces 2.. of large trees, +1.8% on the metric row
     out->lds_nodes = 0;         // the top records in LDS, measured
-    out->render_ahead = 2;      // synchronous path-kernel calls fill their drain with the next 2 calls' paths
+    out->render_ahead = 3;      // a synchronous path-kernel call fills its drain with the next 3 calls' paths,
+                                // a wavefront call that continues its series renders the next 3 passes in its batch
 }
 
 extern "C" khp_status khp_get_params(khp_ctx* c, khp_ctx_params* out) {

@@ -103,6 +103,8 @@ def parse():
     ap.add_argument("--ray-sort-from", type=int, default=None,
                     help="khp_ctx_params.ray_sort_from (first bounce whose rays are regrouped by origin cell; "
                          "0: automatic, >= depth: never)")
+    ap.add_argument("--render-ahead", type=int, default=None,
+                    help="khp_ctx_params.render_ahead (later calls of a synchronous series rendered ahead, 0..3)")
     ap.add_argument("--lds-nodes", type=int, default=None,
                     help="khp_ctx_params.lds_nodes (0 or 7: the tree's top records staged in LDS)")
     ap.add_argument("--heavy-iters", type=int, default=None,
@@ -403,7 +405,7 @@ def main():
                                ("frames_in_flight", args.frames_in_flight), ("shade_order", args.shade_order),
                                ("heavy_iters", args.heavy_iters), ("path_order", args.path_order),
                                ("wide_from", args.wide_from), ("ray_sort_from", args.ray_sort_from),
-                               ("lds_nodes", args.lds_nodes))
+                               ("lds_nodes", args.lds_nodes), ("render_ahead", args.render_ahead))
              if v is not None}
     if knobs:
         ctx.set_params(**knobs)

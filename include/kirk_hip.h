@@ -331,7 +331,7 @@ typedef struct {
                                     staged in each traversal wave's LDS beside its stack rings (the 64-B
                                     loops of k_extend and k_shadow), the rest fetched from HBM as before.
                                     Same walk, same counts, same frames.  Measured in DESIGN.md §4    */
-    uint32_t render_ahead;       /* ABI 13: 0..3 (default 2).  A synchronous render that runs the path kernel
+    uint32_t render_ahead;       /* ABI 13: 0..3 (default 3).  A synchronous render that runs the path kernel
                                     in one chunk lets the lanes that would idle in its launch's drain (its
                                     longest paths finishing alone) start the paths of the next render_ahead
                                     calls of a progressive series -- the same pixels, spp, depth and seed,

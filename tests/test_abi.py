@@ -148,5 +148,5 @@ def test_ctx_params_struct_matches_header():
     assert prm.as_dict() == {"fuse_frames": 32, "frames_in_flight": 1, "chunk_paths": 0, "heavy_iters": 160,
                              "dump_bounce": -1, "trace_kernels": 0, "shade_order": 0, "serial_stages": 0, "path_order": 1,
                              "wide_from": 2, "path_kernel": 0, "ray_sort_from": 0, "lds_nodes": 0,
-                             "render_ahead": 2, "path_from": 0}
+                             "render_ahead": 3, "path_from": 0}
     assert ctypes.sizeof(N.CtxParams) == 64  # 15 fields: 8 + 8 + 12 x 4 bytes

@@ -37,8 +37,8 @@ def test_bench_gpus_n_orchestration(gpus):
     assert line["n_gpus"] == gpus and line["value"] > 0 and line["steps"] == 3
     assert line["config"]["ctx_factory"].endswith("OracleBenchCtx") and line["data"].startswith("STAND-IN")
     chk = line["gather_check"]
-    # warmup + instrumented pass + timed + sync-check + isolated passes, all gathered
-    assert chk["passes"] == 1 + 1 + 3 + 1 + 1 and chk["pixels"] == 40 * 24
+    # warmup + instrumented pass + timed + (series start + sync-check) + isolated passes, all gathered
+    assert chk["passes"] == 1 + 1 + 3 + (1 + 1) + 1 and chk["pixels"] == 40 * 24
     assert chk["bit_exact"] and chk["mismatched_pixels"] == 0
 
 

@@ -86,6 +86,20 @@ envab)  # the driver's bench shape with environment settings $3.. (each a quoted
     done
   done
   ;;
+guiab)  # bench's GUI and sync lines with environment settings $3.. ("-" = none), alternated twice
+  shift 2
+  for r in 1 2; do
+    i=0
+    for e in "$@"; do
+      E=""; A=""
+      for t in $e; do case $t in -) ;; *=*) E="$E $t" ;; *) A="$A $t" ;; esac; done
+      env $E timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --iso-steps 0 $A > gpurun_out/$T/g${i}_$r.json 2> gpurun_out/$T/g${i}_$r.log || exit 1
+      d=$(python -c "import json,sys; d=json.loads(open('gpurun_out/$T/g${i}_$r.json').read().strip().splitlines()[-1]); g=d['gui_steps']; s=d['sync_steps']; print('gui', g['value'], g['ms_per_call'], 'sync', s['value'], 'gui_calls', g['call_ms'])")
+      echo "$r [$e] $d" | tee -a gpurun_out/$T/guiab.txt
+      i=$((i+1))
+    done
+  done
+  ;;
 partests)  # the wavefront/path-kernel parity suites (render-ahead, hybrid, parity)
   KHP_NO_BUILD=1 timeout -k 10 900 $PYT tests/test_gpu_parity.py tests/test_render_ahead.py tests/test_hybrid_batches.py > gpurun_out/$T/tests_par.log 2>&1 || exit 1
   ;;
