@@ -410,4 +410,4 @@ def test_bench_two_ranks_on_one_gpu():
     assert out.returncode == 0, out.stderr[-3000:]
     line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0
-    assert line["gather_check"]["bit_exact"] and line["gather_check"]["passes"] == 1 + 1 + 3 + 1 + 1
+    assert line["gather_check"]["bit_exact"] and line["gather_check"]["passes"] == 1 + 1 + 3 + (1 + 1) + 1
