@@ -18,8 +18,8 @@ and consecutive passes with equal parameters are fused into one wavefront
 a barrier, so every pass is complete.  `sync_steps` in the JSON line is the
 same workload with a host wait after every pass (KIRK's synchronous call):
 one untimed call starts the series, then 12 calls are timed (with render-ahead
-a call renders its pass and the next two as one batch and the two later calls
-only accumulate, so 12 calls are 4 whole batches).
+a call renders its pass and the next three as one batch and the three later calls
+only accumulate, so 12 calls are 3 whole batches).
 
 --gpus N: one process per GPU.  Under torchrun (WORLD_SIZE set) each rank
 renders the 64x64 tiles t with t % N == rank and every step ends with the RCCL
