@@ -100,6 +100,17 @@ guiab)  # bench's GUI and sync lines with environment settings $3.. ("-" = none)
     done
   done
   ;;
+tiles)  # rank-of-N projection (tools/scale_probe.py, the driver's 20 passes) per tile size $3..
+  shift 2
+  for t in "$@"; do
+    timeout -k 10 300 python -u tools/scale_probe.py --nranks 1 8 --steps 20 --tile $t > gpurun_out/$T/scale_tile$t.txt 2>&1 || exit 1
+  done
+  ;;
+fif)    # rank-of-8 projection with two batches in flight (fuse 10) and 8 hardware queues, vs the default
+  timeout -k 10 300 python -u tools/scale_probe.py --nranks 1 8 --steps 20 > gpurun_out/$T/scale_base.txt 2>&1 || exit 1
+  GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python -u tools/scale_probe.py --nranks 1 8 --steps 20 --set frames_in_flight=2 fuse_frames=10 > gpurun_out/$T/scale_fif2.txt 2>&1 || exit 1
+  GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python -u tools/scale_probe.py --nranks 1 8 --steps 20 --set frames_in_flight=2 fuse_frames=5 > gpurun_out/$T/scale_fif2f5.txt 2>&1 || exit 1
+  ;;
 partests)  # the wavefront/path-kernel parity suites (render-ahead, hybrid, parity)
   KHP_NO_BUILD=1 timeout -k 10 900 $PYT tests/test_gpu_parity.py tests/test_render_ahead.py tests/test_hybrid_batches.py > gpurun_out/$T/tests_par.log 2>&1 || exit 1
   ;;
