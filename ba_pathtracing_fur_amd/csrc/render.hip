@@ -78,7 +78,11 @@ struct Wave {
     float4* CK;          // per path: the final colour, written when the path ends (k_accumulate reads it)
     uint8_t* vis;        // shadow-ray occlusion flag per shadow record (this parity)
     ShadowQ* shq;        // shadow queue of this parity
-    float4* sh;          // 6 float4 per shadow record
+    float4* sh;          // shs float4 per shadow record
+    // float4 per shadow record: 4 for the next-event records of k_shade (o + t_max,
+    // d + state destination, the colour add if unoccluded, the add if occluded), 6 for
+    // the light-path variant's connection records and the batch ray queries
+    uint32_t shs;
     Counters* cnt;
     const uint32_t* pix;  // owned pixel ids (y*W+x)
     uint32_t P;           // pixels in this chunk
@@ -771,7 +775,7 @@ __global__ __launch_bounds__(256) void k_img_connect(DevScene S, Wave Wv) {
                 ++nv;
                 continue;
             }
-            float4* rec = Wv.sh + 6 * (size_t)o++;
+            float4* rec = Wv.sh + Wv.shs * (size_t)o++;
             rec[0] = make_float4(sensor.x, sensor.y, sensor.z, t);
             rec[1] = make_float4(dir.x, dir.y, dir.z, f_from_bits(pid));
             rec[2] = make_float4(cj.x, cj.y, cj.z, 0.0f);
@@ -1256,7 +1260,7 @@ __global__ __launch_bounds__(KHP_SHADE_BLOCK, KHP_SHADE_WAVES) void k_shade(DevS
                             if (!bd_connection(S, bd, lv, j, S.lights[li], s, loc, r.d, bounce, sh, tm, cj) ||
                                 (cj.x == 0.0f && cj.y == 0.0f && cj.z == 0.0f))
                                 continue;
-                            float4* rec = Wv.sh + 6 * (size_t)o++;
+                            float4* rec = Wv.sh + Wv.shs * (size_t)o++;
                             rec[0] = make_float4(sh.o.x, sh.o.y, sh.o.z, tm);
                             rec[1] = make_float4(sh.d.x, sh.d.y, sh.d.z, f_from_bits(pid));
                             rec[2] = make_float4(cj.x, cj.y, cj.z, has_emit ? 1.0f : 0.0f);
@@ -1312,15 +1316,23 @@ __global__ __launch_bounds__(KHP_SHADE_BLOCK, KHP_SHADE_WAVES) void k_shade(DevS
             Wv.CK[pid] = cko;
         }
         if (emit_sh) {
-            float4* rec = Wv.sh + 6 * (size_t)si;
+            // The finish adds one of two values: the light's term if the shadow ray is
+            // unoccluded, none if it is -- both computed here with the finish's own
+            // operations (lc * (occ ? 0 : 1), then (0 + dl * Told) + AT [+ ET]), so the
+            // record is 64 B instead of 96 and the finish reads one of them
+            float4* rec = Wv.sh + Wv.shs * (size_t)si;
             rec[0] = make_float4(shr.o.x, shr.o.y, shr.o.z, sh_tmax);
-            rec[1] = make_float4(shr.d.x, shr.d.y, shr.d.z, f_from_bits(pid));
-            rec[2] = make_float4(lc.x, lc.y, lc.z, has_emit ? 1.0f : 0.0f);
-            rec[3] = make_float4(Told.x, Told.y, Told.z, 0.0f);
-            rec[4] = make_float4(AT.x, AT.y, AT.z, f_from_bits(dest));
-            if (has_emit) rec[5] = make_float4(ET.x, ET.y, ET.z, 0.0f);
+            rec[1] = make_float4(shr.d.x, shr.d.y, shr.d.z, f_from_bits(dest));
+            const v3 dl_u = mk(0, 0, 0) + lc * 1.0f, dl_o = mk(0, 0, 0) + lc * 0.0f;
+            v3 add_u = (mk(0, 0, 0) + dl_u * Told) + AT, add_o = (mk(0, 0, 0) + dl_o * Told) + AT;
+            if (has_emit) {
+                add_u = add_u + ET;
+                add_o = add_o + ET;
+            }
+            rec[2] = make_float4(add_u.x, add_u.y, add_u.z, 0.0f);
+            rec[3] = make_float4(add_o.x, add_o.y, add_o.z, 0.0f);
         }
-        if (BD && bd_head != 0xFFFFFFFFu) Wv.sh[6 * (size_t)bd_head + 4] = make_float4(AT.x, AT.y, AT.z, f_from_bits(dest));
+        if (BD && bd_head != 0xFFFFFFFFu) Wv.sh[Wv.shs * (size_t)bd_head + 4] = make_float4(AT.x, AT.y, AT.z, f_from_bits(dest));
     }
 }
 
@@ -1335,49 +1347,40 @@ __device__ __forceinline__ float4* state_dest(const Wave& Wv, int nxt, uint32_t 
 }
 
 __device__ __forceinline__ void shadow_finish_one(const DevScene& S, const Wave& Wv, int nxt, uint32_t i, bool occ) {
-    {
-        const float4* rec = Wv.sh + 6 * (size_t)i;
-        float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3], e = rec[4];
-        uint32_t pid = bits_from_f(b.w);
+    const float4* rec = Wv.sh + Wv.shs * (size_t)i;
+    const float4 b = rec[1];
+    if (!occ) {   // KIRK's light occlusion loop (the any-hit result came from k_shadow)
+        const float4 a = rec[0];
         Ray r;
         r.o = mk(a.x, a.y, a.z);
         r.d = mk(b.x, b.y, b.z);
         const float tmax = a.w;
-        if (!occ) {
-            for (int li = 0; li < S.n_lights; ++li) {
-                float t;
-                if (light_isect(S.lights[li], r, t) && (t < tmax)) {
-                    occ = true;
-                    break;
-                }
+        for (int li = 0; li < S.n_lights; ++li) {
+            float t;
+            if (light_isect(S.lights[li], r, t) && (t < tmax)) {
+                occ = true;
+                break;
             }
         }
-        v3 lc = mk(c.x, c.y, c.z) * (occ ? 0.0f : 1.0f);
-        v3 dl = mk(0, 0, 0) + lc;
-        v3 acc = (mk(0, 0, 0) + dl * mk(d.x, d.y, d.z)) + mk(e.x, e.y, e.z);
-        if (c.w != 0.0f) {
-            float4 f = rec[5];
-            acc = acc + mk(f.x, f.y, f.z);
-        }
-        (void)pid;
-        float4* dst = state_dest(Wv, nxt, bits_from_f(e.w));
-        const float4 ck = *dst;
-        *dst = make_float4(ck.x + acc.x, ck.y + acc.y, ck.z + acc.z, ck.w);
     }
+    const float4 acc = rec[occ ? 3 : 2];   // k_shade's precomputed add for this outcome
+    float4* dst = state_dest(Wv, nxt, bits_from_f(b.w));
+    const float4 ck = *dst;
+    *dst = make_float4(ck.x + acc.x, ck.y + acc.y, ck.z + acc.z, ck.w);
 }
 
 // BD: the records of a light-path connection group (one path, one bounce) are
 // consecutive in the front part; the head (rec[3].w = group size) adds the
 // unoccluded contributions in vertex order (the oracle's bdpt_connect).
 __device__ __forceinline__ void connection_group_finish(const DevScene& S, const Wave& Wv, int nxt, uint32_t i) {
-    const float4* rec = Wv.sh + 6 * (size_t)i;
+    const float4* rec = Wv.sh + Wv.shs * (size_t)i;
     const float4 d = rec[3];
     if (d.w == 0.0f) return;  // not a group head
     const uint32_t nv = (uint32_t)d.w;
     const uint32_t pid = bits_from_f(rec[1].w);
     v3 dl = mk(0, 0, 0);
     for (uint32_t m = 0; m < nv; ++m) {
-        const float4* q = rec + 6 * (size_t)m;
+        const float4* q = rec + Wv.shs * (size_t)m;
         const float4 a = q[0], b = q[1], c = q[2];
         bool occ = Wv.vis[i + m] != 0;
         if (!occ) {
@@ -1442,7 +1445,7 @@ __global__ __launch_bounds__(TRAV_BLOCK, TRAV_WAVES) void k_shadow(DevScene S, W
             uint32_t my;
             const bool got = cl.claim(idle, my, exhausted);
             if (!has && got && cl.phys(my, idx)) {
-                const float4* rec = Wv.sh + 6 * (size_t)idx;
+                const float4* rec = Wv.sh + Wv.shs * (size_t)idx;
                 float4 a = rec[0], b = rec[1];
                 Ray r;
                 r.o = mk(a.x, a.y, a.z);
@@ -2582,7 +2585,8 @@ struct PathSet {
     hipStream_t sA = nullptr, sB = nullptr;
 };
 // Device bytes per path of a PathSet (ensure_wave): 2 x 7 queue columns, hit
-// t/slot, TF + CK records, heavy flag, 2 x (occlusion flag + 96-B shadow record).
+// t/slot, TF + CK records, heavy flag, 2 x (occlusion flag + 96-B shadow record: the
+// light-path variant's size; next-event records use 64 of it).
 constexpr size_t PATH_BYTES = 2 * 7 * 4 + 2 * 4 + 5 * 16 + 1 + 2 * (1 + 6 * 16) + 4 + 1;
 
 #ifndef KHP_MAX_INFLIGHT
@@ -3461,6 +3465,7 @@ static Wave wave_view(const khp_ctx* c, PathSet& w) {
     Wv.CK = w.CKb.as<float4>();
     Wv.vis = w.visb[0].as<uint8_t>();
     Wv.sh = w.shb[0].as<float4>();
+    Wv.shs = 6;
     Wv.shq = w.shqb.as<ShadowQ>();
     Wv.cnt = w.cnt.as<Counters>();
     Wv.heavy = w.heavyb.as<uint8_t>();
@@ -4043,6 +4048,7 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     // variant (its image-plane connections add to the queued bounce-0 state) nor
     // when bounce 0's queue is dumped
     Wv.cam0 = (!bdm && dump_b != 0) ? 1u : 0u;
+    Wv.shs = bdm ? 6u : 4u;   // next-event records are 64 B; the light-path variant's connection records 96
     Wv.bd = BdptDev{bdm ? 1u : 0u, c->bd.light_paths, (uint32_t)c->S.n_lights, c->bd.vertices, c->bd.bias,
                     c->bd.bounce_bias, c->bd.min_pdf, c->bd.image_plane,
                     bdm ? w.lvb.as<float4>() : nullptr};
@@ -4212,15 +4218,16 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     KHPCHK(wait_stream(c, sA, "the queue dump"));
                     ShadowQ hq;
                     HIPCHK(hipMemcpy(&hq, Wb.shq, sizeof(ShadowQ), hipMemcpyDeviceToHost));
-                    std::vector<float4> rec(6 * ((size_t)hq.nsh + hq.nshb));
+                    const size_t R = Wv.shs;   // float4 per record
+                    std::vector<float4> rec(R * ((size_t)hq.nsh + hq.nshb));
                     if (hq.nsh)
-                        HIPCHK(hipMemcpy(rec.data(), Wb.sh, 6 * sizeof(float4) * hq.nsh, hipMemcpyDeviceToHost));
+                        HIPCHK(hipMemcpy(rec.data(), Wb.sh, R * sizeof(float4) * hq.nsh, hipMemcpyDeviceToHost));
                     if (hq.nshb)
-                        HIPCHK(hipMemcpy(rec.data() + 6 * (size_t)hq.nsh, Wb.sh + 6 * (Wv.cap - hq.nshb),
-                                         6 * sizeof(float4) * hq.nshb, hipMemcpyDeviceToHost));
+                        HIPCHK(hipMemcpy(rec.data() + R * (size_t)hq.nsh, Wb.sh + R * (Wv.cap - hq.nshb),
+                                         R * sizeof(float4) * hq.nshb, hipMemcpyDeviceToHost));
                     c->dump_sh.resize(7 * ((size_t)hq.nsh + hq.nshb));
                     for (size_t k = 0; k < (size_t)hq.nsh + hq.nshb; ++k) {
-                        const float4 a = rec[6 * k], d = rec[6 * k + 1];
+                        const float4 a = rec[R * k], d = rec[R * k + 1];
                         const float v[7] = {a.x, a.y, a.z, d.x, d.y, d.z, a.w};
                         memcpy(c->dump_sh.data() + 7 * k, v, sizeof(v));
                     }
@@ -4948,8 +4955,8 @@ __global__ void k_load_rays(uint32_t n, const float* orig, const float* dir, Wav
     if (i >= n) return;
     Ray r = make_ray(ld3(orig + 3 * (size_t)i), ld3(dir + 3 * (size_t)i));
     if (as_shadow) {
-        Wv.sh[6 * (size_t)i] = make_float4(r.o.x, r.o.y, r.o.z, tmax[i]);
-        Wv.sh[6 * (size_t)i + 1] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
+        Wv.sh[Wv.shs * (size_t)i] = make_float4(r.o.x, r.o.y, r.o.z, tmax[i]);
+        Wv.sh[Wv.shs * (size_t)i + 1] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
     } else {
         Wv.qo[0][0][i] = r.o.x; Wv.qo[0][1][i] = r.o.y; Wv.qo[0][2][i] = r.o.z;
         Wv.qd[0][0][i] = r.d.x; Wv.qd[0][1][i] = r.d.y; Wv.qd[0][2][i] = r.d.z;
