@@ -2922,7 +2922,7 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     *out = khp_ctx_params{};
     out->fuse_frames = 32;      // 8 -> 470, 16 -> 485, 32 -> 497 Msamples/s
     out->frames_in_flight = 1;  // with fusion one batch at a time is fastest
-    out->chunk_paths = 0;       // min(2^27, fits in half the free HBM)
+    out->chunk_paths = 0;       // min(2^28, fits in half the free HBM)
     out->heavy_iters = 160;
     out->dump_bounce = -1;
     out->trace_kernels = 0;
@@ -3489,19 +3489,20 @@ static khp_status prepare_pixels(khp_ctx* c, const khp_render_params* p) {
     return KHP_OK;
 }
 
-// Paths per wavefront chunk.  A chunk's path state is PATH_BYTES (~300 B) per
-// path, 40 GB at 2^27; at the metric row a 32-frame batch is four such chunks
-// (16-frame batches: 2^26 four chunks 1.2% slower, 2^28 one chunk 1% slower,
-// as its last shadow launch and accumulate then overlap no other chunk).  By
-// default the smaller of 2^27 and the largest power of two whose path sets
-// (one per batch in flight) fit in half the free HBM.
+// Paths per wavefront chunk.  A chunk's path state is PATH_BYTES (~350 B) per
+// path, ~95 GB at 2^28.  By default the smaller of 2^28 and the largest power of
+// two whose path sets (one per batch in flight) fit in half the free HBM; with
+// the 5/4 rule of chunk_most the driver's 20 fused 8-spp passes at the metric
+// row (332M paths) are then ONE chunk: each launch's tail is paid once per 20
+// frames, +1.8% against two chunks of 166M under the round-5 cap of 2^27
+// (profiles/r06zi_one_chunk_ab.txt).
 // Decided once per context (and again after khp_set_params), before the path
 // sets themselves take memory, so the chunking stays the same frame to frame.
 static size_t chunk_paths(khp_ctx* c) {
     if (c->prm.chunk_paths) return (size_t)c->prm.chunk_paths;
     if (c->auto_chunk) return c->auto_chunk;
     size_t free_b = 0, total_b = 0;
-    size_t cap = (size_t)1 << 27;
+    size_t cap = (size_t)1 << 28;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
         const size_t fit = free_b / 2 / (PATH_BYTES * (size_t)std::max<uint32_t>(1, c->prm.frames_in_flight));
         while (cap > ((size_t)1 << 16) && cap > fit) cap >>= 1;

@@ -279,7 +279,7 @@ typedef struct {
                                     1..32 (default 32)                                               */
     uint32_t frames_in_flight;   /* batches in flight at once, 1..3 (default 1)                     */
     uint64_t chunk_paths;        /* paths per wavefront chunk, >= 4096; 0 (default): the smaller of
-                                    2^27 and what fits in half the free HBM                         */
+                                    2^28 (2^27 before round 6) and what fits in half the free HBM    */
     uint32_t heavy_iters;        /* longest-first queues: a path whose last traversal took more
                                     iterations has its next rays claimed first (default 160).  No
                                     effect on the extension rays of bounces regrouped by ray_sort_from

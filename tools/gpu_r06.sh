@@ -111,6 +111,15 @@ fif)    # rank-of-8 projection with two batches in flight (fuse 10) and 8 hardwa
   GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python -u tools/scale_probe.py --nranks 1 8 --steps 20 --set frames_in_flight=2 fuse_frames=10 > gpurun_out/$T/scale_fif2.txt 2>&1 || exit 1
   GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python -u tools/scale_probe.py --nranks 1 8 --steps 20 --set frames_in_flight=2 fuse_frames=5 > gpurun_out/$T/scale_fif2f5.txt 2>&1 || exit 1
   ;;
+chunks)  # default 32 passes and the driver's 20 with the automatic chunk cap vs an explicit 2^27 (round 5's), alternated
+  for r in 1 2; do
+    for c in 0 134217728; do
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline --sync-check-steps 0 --gui-steps 0 --iso-steps 0 --chunk-paths $c > gpurun_out/$T/c32_${c}_$r.json 2> gpurun_out/$T/c32_${c}_$r.log || exit 1
+      timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --sync-check-steps 0 --gui-steps 0 --iso-steps 0 --chunk-paths $c > gpurun_out/$T/c20_${c}_$r.json 2> gpurun_out/$T/c20_${c}_$r.log || exit 1
+      python -c "import json; f=lambda n: json.loads(open(n).read().strip().splitlines()[-1]); a=f('gpurun_out/$T/c32_${c}_$r.json'); b=f('gpurun_out/$T/c20_${c}_$r.json'); print($r, 'chunk_paths', $c, '32 passes', a['value'], a['frame']['extend_launches'] if 'extend_launches' in a['frame'] else '', '20 passes', b['value'], b['roofline']['frac'])" | tee -a gpurun_out/$T/chunks.txt
+    done
+  done
+  ;;
 partests)  # the wavefront/path-kernel parity suites (render-ahead, hybrid, parity)
   KHP_NO_BUILD=1 timeout -k 10 900 $PYT tests/test_gpu_parity.py tests/test_render_ahead.py tests/test_hybrid_batches.py > gpurun_out/$T/tests_par.log 2>&1 || exit 1
   ;;
