@@ -295,8 +295,9 @@ def cpu_baseline(sd, args, budget_s):
 def _pmc_profile(config: str, frames_per_launch: float | None = None):
     """The committed PMC profile of k_extend for this workload (tools/summarize_prof.py):
     among the newest round's profiles, the one whose launches carried the number of
-    fused frames nearest this run's (the driver's 20 passes: 10 per launch; the
-    default 32: 8), else the newest.  Returns (file name, contents) or (None, None)."""
+    fused frames nearest this run's (since round 6 the driver's 20 passes: 20 per
+    launch; the default 32: 16), else the newest.  Returns (file name, contents) or
+    (None, None)."""
     def tag_order(f):   # r05p < r05z < r05aa: a round's tags run a..z, then aa, ab, ...
         t = os.path.basename(f)[len("pmc_extend_"):].split(".")[0].split("_")[0]
         return (t[:3], len(t), t, f)
