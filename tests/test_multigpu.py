@@ -123,6 +123,59 @@ def test_local_group_gather_with_empty_ranks(async_):
             c.close()
 
 
+def test_local_group_config5_stated_form_eight_ranks():
+    """BASELINE config 5 in its stated form -- 1M strands + 500x500x2-triangle
+    torus + glass icosphere at 3840x2160, 32 spp, tiled over 8 ranks -- with the
+    8 ranks as contexts of this process (khp_comm_init_local): four synchronous
+    8-spp passes per rank (KIRK's progressive calls) with a gather after each.
+    Rank 0's frame equals one context's frame of the same passes bit for bit
+    over all 8.3M pixels, and every 54th row (plus row 860, which holds a NaN
+    pixel) is the oracle's 32-spp frame.
+    Only the transport differs from the RCCL path (device copies instead of
+    ncclSend/ncclRecv)."""
+    from ba_pathtracing_fur_amd.pathtracer import HipContext, comm_init_local
+    W, H, SPP, PASSES, TILE, world = 3840, 2160, 8, 4, 64, 8
+    one = HipContext(0)
+    try:
+        S.config5_device(one, W, H, n_strands=1_000_000)
+        one.build_accel()
+        for k in range(PASSES):
+            one.render(W, H, SPP, 5, first_sample=k * SPP, readback=False)
+        want = one.read_framebuffer(W, H)
+    finally:
+        one.close()
+    ctxs = [HipContext(0) for _ in range(world)]
+    try:
+        for c in ctxs:
+            S.config5_device(c, W, H, n_strands=1_000_000)
+            c.build_accel()
+        comm_init_local(ctxs)
+        for k in range(PASSES):
+            for r in reversed(range(world)):   # senders enqueue their k-th gather before the root
+                ctxs[r].render(W, H, SPP, 5, first_sample=k * SPP, tile_size=TILE, tile_rank=r, tile_nranks=world,
+                               readback=False)
+                ctxs[r].gather_framebuffer(W, H, SPP, 5, TILE, world, r, 0)
+        for c in ctxs[1:]:
+            c.sync()
+        ctxs[0].sync()
+        got = ctxs[0].read_framebuffer(W, H)
+    finally:
+        for c in ctxs:
+            c.close()
+    # a rank's 8-spp call (1M pixels) runs the path kernel, the whole frame's the
+    # wavefront: the same values bit for bit; pixel (860, 2057) turns NaN at
+    # sample 16 in both and in the oracle (KIRK's own arithmetic), with a
+    # different NaN encoding on each (tests/_util.py)
+    assert_parity(got, want, exact=True)
+    assert np.isnan(got[860, 2057]).all()
+    host = S.config5(W, H, n_strands=1_000_000)
+    orc = oracle_ffi.Oracle(host)
+    rows = list(range(11, H, 54)) + [860]
+    ref = orc.render(W, H, SPP * PASSES, 5, threads=16, rows=(11, H, 54))
+    ref = orc.render(W, H, SPP * PASSES, 5, threads=16, rows=(860, 861, 1), out=ref)
+    assert_parity(got[rows], ref[rows], exact=True)
+
+
 def test_local_group_driver_batch_two_ranks():
     """The driver's 2-GPU bench at the metric size, on one GPU: each of 2 ranks
     renders its tiles of 20 fused 8-spp passes with a gather after every pass
