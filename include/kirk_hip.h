@@ -243,9 +243,11 @@ typedef struct {
     double layout_kernel_ms;         /* device layout: GPU time of its kernels  */
     /* stack entries popped only to fail the prune test (instrumented renders) */
     uint64_t extend_pruned_pops, shadow_pruned_pops;
-    /* ABI 5: frames this report covers -- 1 after a synchronous khp_render; after
-     * khp_sync, every asynchronous frame completed since the previous report, with
-     * timings (extend_ms, extend_launches, ...) and counters summed over them */
+    /* ABI 5: frames this report covers -- 1 after a synchronous khp_render (1 +
+     * render_ahead when the call rendered the next calls' passes in its fused
+     * batch, whose timings and counters it then reports); after khp_sync, every
+     * asynchronous frame completed since the previous report, with timings
+     * (extend_ms, extend_launches, ...) and counters summed over them */
     uint64_t frames;
     /* ABI 5: wall time during which at least one k_extend launch of the report
      * was running (union of the launches' HIP-event intervals); equals extend_ms
