@@ -3887,7 +3887,8 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
     // (the previous synchronous call was its pass with first_sample - spp) renders itself and
     // the next render_ahead calls' passes as one fused batch of one chunk, accumulates its own
     // frame and leaves the others' colours for those calls (8-spp calls at the metric row:
-    // a batch of 3 passes costs 28.6 ms per pass against 36.8 alone, tools/fuse_probe.py)
+    // a batch of 3 / 4 passes costs 28.6 / 27.5 ms per pass against 36.8 alone,
+    // profiles/r06t_fuse_probe.jsonl)
     uint32_t wa_frames = 1;
     if (continues && c->prm.render_ahead != 0 && !stats && !bdm && dump_b < 0 && P_all > 0) {
         const size_t one = (size_t)P_all * p->spp;
