@@ -235,10 +235,12 @@ def test_wavefront_series_match_oracle(name, kw, w, h, depth, spp, ahead_sets):
         ahead = []
         calls = 2 + 2 * (ahead_sets + 1)
         for k in range(calls):
-            ctx.render(w, h, spp, depth, first_sample=k * spp, readback=False)
+            out = ctx.render(w, h, spp, depth, first_sample=k * spp, readback=(k == 2))   # call 2 only accumulates
             ahead.append(ctx.stats()["ahead_finished"])
             ser.call(spp, k * spp)
             _check(ctx, ser, w, h, f"call {k}")
+            if k == 2:   # the readback of a call whose pass was rendered ahead
+                assert_parity(out, ser.fb, exact=True)
         n = w * h * spp
         group = [0] + [n] * ahead_sets
         assert ahead == [0] + group * 2 + [0], ahead
