@@ -1035,20 +1035,31 @@ __device__ __forceinline__ void block_alloc2(bool p0, bool p1, uint32_t* c0, uin
 // k_shade's block: 512 threads (8 waves).  Its queue allocation is one device atomic
 // per output kind per block iteration; 512-thread blocks halve those against 256 and
 // measured +1.4% (default bench) / +1.6% (driver's command) on the whole frame; 128
-// threads doubled them and lost 4% (profiles/r04ah_shade_block.json).
+// threads doubled them and lost 4% (profiles/r04ah_shade_block.json).  Round 6:
+// 1024 threads for the untextured instances without the light-path variant (101 /
+// 105 VGPRs, no scratch) -- a block's surviving rays then fill one run of the next
+// queue from 16 pixels' paths, and bounce 1's k_extend takes 6.85 instead of 7.06
+// ms per frame (+0.3% on the driver's command, profiles/r06zx_shade_block_1024_ab.txt);
+// the textured and light-path instances would spill at 1024 and keep 512.
 #ifndef KHP_SHADE_BLOCK
 #define KHP_SHADE_BLOCK 512
 #endif
-constexpr uint32_t SHADE_BLOCK = KHP_SHADE_BLOCK, SHADE_NW = KHP_SHADE_BLOCK / 64;
+#ifndef KHP_SHADE_BLOCK_PLAIN
+#define KHP_SHADE_BLOCK_PLAIN 1024
+#endif
+template <bool TEX, bool BD>
+constexpr uint32_t shade_block() { return (!TEX && !BD) ? KHP_SHADE_BLOCK_PLAIN : KHP_SHADE_BLOCK; }
 // Four outputs (next-bounce rays and shadow rays, each front or back): a lane
 // sets at most one of p0/p1 and one of p2/p3; i01 / i23 is its index in the
 // queue it was counted in.
+template <uint32_t NW>   // waves per block
 struct BlockAlloc4 {
-    uint32_t wcnt[4][SHADE_NW];
+    uint32_t wcnt[4][NW];
     uint32_t base[4];
 };
+template <uint32_t NW>
 __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3, uint32_t* c0, uint32_t* c1,
-                                             uint32_t* c2, uint32_t* c3, BlockAlloc4& sh, uint32_t& i01,
+                                             uint32_t* c2, uint32_t* c3, BlockAlloc4<NW>& sh, uint32_t& i01,
                                              uint32_t& i23) {
     const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
     const unsigned long long m[4] = {__ballot(p0), __ballot(p1), __ballot(p2), __ballot(p3)};
@@ -1059,7 +1070,7 @@ __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3,
     if (threadIdx.x < 4) {
         const uint32_t q = threadIdx.x;
         uint32_t tot = 0;
-        for (uint32_t w = 0; w < SHADE_NW; ++w) tot += sh.wcnt[q][w];
+        for (uint32_t w = 0; w < NW; ++w) tot += sh.wcnt[q][w];
         uint32_t* ctr = q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : c3;
         sh.base[q] = tot ? atomicAdd(ctr, tot) : 0u;
     }
@@ -1078,12 +1089,12 @@ __device__ __forceinline__ void block_alloc4(bool p0, bool p1, bool p2, bool p3,
 #define KHP_SHADE_WAVES 1   // min waves per SIMD for k_shade's register budget (1: unconstrained)
 #endif
 template <bool TEX, bool BD, uint32_t KINDS = 0xFFFFFFFFu>
-__global__ __launch_bounds__(KHP_SHADE_BLOCK, KHP_SHADE_WAVES) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
+__global__ __launch_bounds__((shade_block<TEX, BD>()), KHP_SHADE_WAVES) void k_shade(DevScene S, Wave Wv, int cur, uint32_t bounce) {
     const uint32_t nf = Wv.cnt->nq[cur], n = nf + Wv.cnt->nqb[cur];
     const int nxt = cur ^ 1;
     const bool last = bounce + 1 >= Wv.depth;
     const uint32_t stride = gridDim.x * blockDim.x;
-    __shared__ BlockAlloc4 balloc;
+    __shared__ BlockAlloc4<shade_block<TEX, BD>() / 64> balloc;
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {
         const uint32_t iv = base + threadIdx.x;
         bool active = iv < n;
@@ -2685,6 +2696,7 @@ struct khp_ctx {
     std::vector<TimedLaunch> launches;
     int grid_ext = 0, grid_ext_w = 0, grid_ext_cam = 0, grid_sh = 0, grid_shade = 0;  // k_extend: 64-B, wide, bounce 0
     int grid_fin = 0;    // k_shadow_finish
+    int grid_shade_bd = 0;   // k_shade with the light-path variant (512-thread blocks)
     int grid_sh_w = 0;     // k_shadow on the two-level records
     int grid_path = 0, grid_path_w = 0;   // k_path (64-B / two-level records)
     uint32_t bsdf_kinds = 0;              // the BSDF kinds the scene's materials use (bit per khp_bsdf_kind)
@@ -3387,11 +3399,15 @@ extern "C" khp_status khp_build_accel(khp_ctx* c) {
     for (const khp_material& m : hs.mats)
         c->bsdf_kinds |= (m.bsdf >= 0 && m.bsdf < KHP_BSDF_COUNT) ? (1u << m.bsdf) : KINDS_ALL;
     nb = 0;
-    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<true, false>), SHADE_BLOCK, 0));
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<true, false>), shade_block<true, false>(), 0));
     else if ((c->bsdf_kinds & ~KINDS_FUR) == 0u)
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false, KINDS_FUR>), SHADE_BLOCK, 0));
-    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false>), SHADE_BLOCK, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false, KINDS_FUR>), shade_block<false, false>(), 0));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, false>), shade_block<false, false>(), 0));
     c->grid_shade = std::max(1, nb) * c->n_cu;
+    nb = 0;
+    if (S.textured) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<true, true>), shade_block<true, true>(), 0));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<false, true>), shade_block<false, true>(), 0));
+    c->grid_shade_bd = std::max(1, nb) * c->n_cu;
     // k_shadow_finish streams shadow records in 256-thread blocks: its own occupancy grid
     // (k_shade's 512-thread grid gave it 0.4x the threads: 0.333 vs 0.314 ms per frame)
     nb = 0;
@@ -4162,16 +4178,16 @@ static khp_status enqueue_frames(khp_ctx* c, const khp_render_params* p, float* 
                     hipLaunchKernelGGL(k_hit_scatter, dim3(c->grid_shade), dim3(256), 0, sA, Wb, cur);
                 }
                 if (c->S.textured && bdm)
-                    hipLaunchKernelGGL((k_shade<true, true>), dim3(c->grid_shade), dim3(SHADE_BLOCK), 0, sA, c->S, Wb, cur, b);
+                    hipLaunchKernelGGL((k_shade<true, true>), dim3(c->grid_shade_bd), dim3(shade_block<true, true>()), 0, sA, c->S, Wb, cur, b);
                 else if (c->S.textured)
-                    hipLaunchKernelGGL((k_shade<true, false>), dim3(c->grid_shade), dim3(SHADE_BLOCK), 0, sA, c->S, Wb, cur, b);
+                    hipLaunchKernelGGL((k_shade<true, false>), dim3(c->grid_shade), dim3(shade_block<true, false>()), 0, sA, c->S, Wb, cur, b);
                 else if (bdm)
-                    hipLaunchKernelGGL((k_shade<false, true>), dim3(c->grid_shade), dim3(SHADE_BLOCK), 0, sA, c->S, Wb, cur, b);
+                    hipLaunchKernelGGL((k_shade<false, true>), dim3(c->grid_shade_bd), dim3(shade_block<false, true>()), 0, sA, c->S, Wb, cur, b);
                 else if ((c->bsdf_kinds & ~KINDS_FUR) == 0u)   // fur scenes: the other BSDF kinds compiled out
-                    hipLaunchKernelGGL((k_shade<false, false, KINDS_FUR>), dim3(c->grid_shade), dim3(SHADE_BLOCK), 0, sA, c->S, Wb,
+                    hipLaunchKernelGGL((k_shade<false, false, KINDS_FUR>), dim3(c->grid_shade), dim3(shade_block<false, false>()), 0, sA, c->S, Wb,
                                        cur, b);
                 else
-                    hipLaunchKernelGGL((k_shade<false, false>), dim3(c->grid_shade), dim3(SHADE_BLOCK), 0, sA, c->S, Wb, cur, b);
+                    hipLaunchKernelGGL((k_shade<false, false>), dim3(c->grid_shade), dim3(shade_block<false, false>()), 0, sA, c->S, Wb, cur, b);
                 timed(c, f, 1, false, sA);
                 // ray sorting: regroup the next bounce's queue by origin cell
                 auto sort_next = [&]() -> khp_status {
