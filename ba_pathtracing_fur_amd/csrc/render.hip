@@ -2935,7 +2935,8 @@ extern "C" void khp_ctx_params_defaults(khp_ctx_params* out) {
     out->fuse_frames = 32;      // 8 -> 470, 16 -> 485, 32 -> 497 Msamples/s
     out->frames_in_flight = 1;  // with fusion one batch at a time is fastest
     out->chunk_paths = 0;       // min(2^28, fits in half the free HBM)
-    out->heavy_iters = 160;
+    out->heavy_iters = 0xFFFFFFFFu;   // longest-first split off (round 6: +0.4% driver, +0.6% 8-spp sync calls, ranks
+                                      // unchanged, profiles/r06zzb_heavy_split_off.txt); 160 before
     out->dump_bounce = -1;
     out->trace_kernels = 0;
     out->shade_order = 0;       // hit sorting measured, off

@@ -283,9 +283,11 @@ typedef struct {
     uint64_t chunk_paths;        /* paths per wavefront chunk, >= 4096; 0 (default): the smaller of
                                     2^28 (2^27 before round 6) and what fits in half the free HBM    */
     uint32_t heavy_iters;        /* longest-first queues: a path whose last traversal took more
-                                    iterations has its next rays claimed first (default 160).  No
-                                    effect on the extension rays of bounces regrouped by ray_sort_from
-                                    (their claim order is the cell order; shadow rays keep it)      */
+                                    iterations has its next rays claimed first (default 0xFFFFFFFF =
+                                    off since round 6; 160 before).  No effect on the extension rays
+                                    of bounces regrouped by ray_sort_from (their claim order is the
+                                    cell order; shadow rays keep it); path_order 2 marks its heavy
+                                    pixels with it                                                  */
     int32_t dump_bounce;         /* debug: keep the extension rays of this bounce of the next
                                     synchronous render for khp_debug_queue (-1: off, default)       */
     uint32_t trace_kernels;      /* khp_trace_closest / khp_trace_any run on 0: one-ray-per-thread

@@ -145,7 +145,7 @@ def test_ctx_params_struct_matches_header():
     lib = N.load_library()
     prm = N.CtxParams()
     lib.khp_ctx_params_defaults(prm)
-    assert prm.as_dict() == {"fuse_frames": 32, "frames_in_flight": 1, "chunk_paths": 0, "heavy_iters": 160,
+    assert prm.as_dict() == {"fuse_frames": 32, "frames_in_flight": 1, "chunk_paths": 0, "heavy_iters": 0xFFFFFFFF,
                              "dump_bounce": -1, "trace_kernels": 0, "shade_order": 0, "serial_stages": 0, "path_order": 1,
                              "wide_from": 2, "path_kernel": 0, "ray_sort_from": 0, "lds_nodes": 0,
                              "render_ahead": 3, "path_from": 0}

@@ -536,13 +536,14 @@ def test_fused_frames(fuse, order):
     after every pass, as bench.py does at N > 1, the gathers keep their place.
     Both path numberings (path_order 0 frame-major, 1 pixel-major) and the
     heavy-first pixel order (2: each batch's pixel list permuted by the previous
-    batch's camera-ray lengths)."""
+    batch's camera-ray lengths), with the longest-first queues on (heavy_iters
+    160, off by default since round 6) so both orderings are exercised."""
     from ba_pathtracing_fur_amd.pathtracer import comm_unique_id
     sd = S.config2(72, 48, n_strands=1500)
     want = oracle_ffi.Oracle(sd).render(72, 48, 8, 5, threads=16)
     ctx = HipContext(0)
     try:
-        ctx.set_params(fuse_frames=int(fuse), path_order=int(order))
+        ctx.set_params(fuse_frames=int(fuse), path_order=int(order), heavy_iters=160)
         ctx.set_scene(sd)
         ctx.build_accel()
         for first in range(0, 8, 2):
@@ -568,9 +569,10 @@ def test_fused_frames(fuse, order):
 
 def test_fused_full_size_matches_passes():
     """The metric scene (1M strands, 1080p): 16 progressive 4-spp passes
-    fused into one batch (133M paths: 1 chunk at the default 2^27 paths per
-    chunk, 2 at 2^26; frame-major and pixel-major path numbering, and the
-    heavy-first pixel order, whose later batches run a permuted pixel list) give the
+    fused into one batch (133M paths: 1 chunk at the automatic cap, 2 at 2^26;
+    frame-major and pixel-major path numbering, and the heavy-first pixel order
+    with the longest-first queues on, whose later batches run a permuted pixel
+    list) give the
     framebuffer of the same passes rendered one by one, bit for bit; sampled
     rows are the oracle's 64-spp frame."""
     ctx = HipContext(0)
@@ -581,7 +583,7 @@ def test_fused_full_size_matches_passes():
             ctx.render(1920, 1080, 4, 5, first_sample=4 * k, readback=False)
         want = ctx.read_framebuffer(1920, 1080)
         for cap, order in ((0, 0), (1 << 26, 0), (0, 1), (1 << 26, 1), (0, 2), (1 << 26, 2), (0, 2)):
-            ctx.set_params(chunk_paths=cap, path_order=order)
+            ctx.set_params(chunk_paths=cap, path_order=order, heavy_iters=160 if order == 2 else 0xFFFFFFFF)
             for k in range(16):
                 ctx.render(1920, 1080, 4, 5, first_sample=4 * k, async_=True)
             ctx.sync()

@@ -120,6 +120,17 @@ chunks)  # default 32 passes and the driver's 20 with the automatic chunk cap vs
     done
   done
   ;;
+heavy)  # longest-first split off (heavy_iters 2^32-1) vs the default: sync/GUI lines and the rank-of-8 shares
+  for r in 1 2; do
+    for h in 160 4294967295; do
+      timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --iso-steps 0 --gui-steps 0 --heavy-iters $h > gpurun_out/$T/h${h}_$r.json 2> gpurun_out/$T/h${h}_$r.log || exit 1
+      python -c "import json; d=json.loads(open('gpurun_out/$T/h${h}_$r.json').read().strip().splitlines()[-1]); print($r, 'heavy_iters', $h, 'sync', d['sync_steps']['value'])" | tee -a gpurun_out/$T/heavy.txt
+    done
+  done
+  for h in 160 4294967295; do
+    timeout -k 10 300 python -u tools/scale_probe.py --nranks 8 --steps 20 --set heavy_iters=$h > gpurun_out/$T/scale_h$h.txt 2>&1 || exit 1
+  done
+  ;;
 partests)  # the wavefront/path-kernel parity suites (render-ahead, hybrid, parity)
   KHP_NO_BUILD=1 timeout -k 10 900 $PYT tests/test_gpu_parity.py tests/test_render_ahead.py tests/test_hybrid_batches.py > gpurun_out/$T/tests_par.log 2>&1 || exit 1
   ;;
